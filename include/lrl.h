@@ -1,0 +1,275 @@
+/*
+ * lrl.h — C ABI of liblrl.so, the MI355X-native hot path of rapid-locomotion-rl.
+ *
+ * What this library replaces (the reference's lower boundary): the Isaac Gym
+ * Preview 3 gymapi/gymtorch calls that mini_gym/envs/base/legged_robot.py makes on every env step
+ * and the torch elementwise work around them, plus the PPO numeric core of mini_gym_learn.
+ *
+ *   lrl_sim_create         ~ gym.create_sim + load_asset + create_env/create_actor loop + prepare_sim
+ *                            (legged_robot.py:419-441, 1162-1319; base_task.py:17,70)
+ *   lrl_sim_tensor         ~ gym.acquire_{actor_root_state,dof_state,net_contact_force,rigid_body_state}
+ *                            _tensor + gymtorch.wrap_tensor (legged_robot.py:939-970)
+ *   lrl_sim_step           ~ LeggedRobot.step (legged_robot.py:106-137): clip actions, 4 x
+ *                            {_compute_torques :653-688, set_dof_actuation_force_tensor :118,
+ *                            simulate/fetch_results :119-121, refresh_dof_state :122}, then
+ *                            post_physics_step :139-188 (teleport :768-791, DR :544-560,
+ *                            check_termination :190-202, compute_reward :314-340,
+ *                            compute_observations :342-417), obs clip :133-136 and the
+ *                            HistoryWrapper shift (history_wrapper.py:23) — one fused launch.
+ *   lrl_sim_reset_idx      ~ LeggedRobot.reset_idx device part (:227-290: _reset_dofs :690-712,
+ *                            _reset_root_states :714-755, buffer zeroing :255-259)
+ *   lrl_sim_set_root_state_indexed / lrl_sim_set_dof_state_indexed
+ *                          ~ gym.set_actor_root_state_tensor_indexed / set_dof_state_tensor_indexed
+ *                            (legged_robot.py:303-312, 710-712, 739-741)
+ *   lrl_sim_refresh_rigid_body_state ~ gym.refresh_rigid_body_state_tensor (:147)
+ *   lrl_gae                ~ RolloutStorage.compute_returns (rollout_storage.py:76-90)
+ *   lrl_policy_act         ~ PPO.act teacher path (ppo.py:62-74 -> actor_critic.py:137-147,170-173)
+ *                            fused with RolloutStorage.add_transitions (rollout_storage.py:57-71)
+ *
+ * Conventions: every function returns 0 on success or a negative LRL_E* code, with a message
+ * available from lrl_last_error() (thread-local).  All data pointers passed to compute entry points
+ * are DEVICE pointers (HBM); `stream` is a hipStream_t passed as void*.  A sim handle is bound to one
+ * device and is not thread-safe.  No torch types cross this boundary.
+ */
+#ifndef LRL_H_
+#define LRL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LRL_ABI_VERSION 1
+
+#define LRL_OK 0
+#define LRL_E_INVALID (-1)  /* bad argument / unsupported configuration */
+#define LRL_E_HIP (-2)      /* HIP runtime error */
+#define LRL_E_NOMEM (-3)
+#define LRL_E_NOGPU (-4)
+
+#define LRL_MAX_BODIES 20
+#define LRL_MAX_SPHERES 40
+#define LRL_NUM_DOF 12
+#define LRL_NUM_LEGS 4
+#define LRL_MAX_OBS 64
+#define LRL_MAX_REWARD_TERMS 24
+#define LRL_NUM_PRIV 18
+
+/* ------------------------------------------------------------------------------------------
+ * Robot model: a floating base with 4 legs x 3 revolute joints (hip, thigh, calf) and an optional
+ * fixed foot body per leg (Go1 `dont_collapse` feet).  Produced on the host from the URDF after
+ * collapse_fixed_joints (legged_robot_config.py:128).  Body order = Isaac Gym asset order.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct lrl_model {
+  int32_t num_bodies;                 /* reported bodies B (13 Mini Cheetah, 17 Go1) */
+  int32_t body_leg[LRL_MAX_BODIES];   /* -1 = base, else leg 0..3 */
+  int32_t body_link[LRL_MAX_BODIES];  /* 0 hip, 1 thigh, 2 calf, 3 fixed foot (merged into calf) */
+  /* per leg, per revolute joint j (0 hip, 1 thigh, 2 calf) */
+  float joint_xyz[LRL_NUM_LEGS][3][3];   /* joint origin in parent-body frame */
+  float joint_quat[LRL_NUM_LEGS][3][4];  /* fixed joint-origin rotation (xyzw) */
+  float joint_axis[LRL_NUM_LEGS][3][3];  /* rotation axis in the child frame */
+  float foot_xyz[LRL_NUM_LEGS][3];       /* fixed foot origin in calf frame (if present) */
+  /* inertial data in the body frame: mass, COM, inertia about COM (xx yy zz xy xz yz) */
+  float base_mass, base_com[3], base_inertia[6];
+  float link_mass[LRL_NUM_LEGS][3], link_com[LRL_NUM_LEGS][3][3], link_inertia[LRL_NUM_LEGS][3][6];
+  /* collision geometry as spheres (box corners radius 0): owning body index, center, radius */
+  int32_t num_spheres;
+  int32_t sphere_body[LRL_MAX_SPHERES];
+  float sphere_pos[LRL_MAX_SPHERES][3];
+  float sphere_radius[LRL_MAX_SPHERES];
+  /* joint data in asset DOF order (FL hip, thigh, calf, FR ..., RL ..., RR ...) */
+  float dof_lower[LRL_NUM_DOF], dof_upper[LRL_NUM_DOF], dof_effort[LRL_NUM_DOF], dof_velocity[LRL_NUM_DOF];
+} lrl_model;
+
+/* Reward terms the fused kernel implements (legged_robot.py:1506-1646); the host passes the
+ * active ones in the order of vars(Cfg.rewards.scales) after zero-scale removal. */
+enum lrl_reward_term {
+  LRL_R_LIN_VEL_Z = 0, LRL_R_ANG_VEL_XY, LRL_R_ORIENTATION, LRL_R_BASE_HEIGHT, LRL_R_TORQUES,
+  LRL_R_ENERGY, LRL_R_ENERGY_EXPENDITURE, LRL_R_DOF_VEL, LRL_R_DOF_ACC, LRL_R_ACTION_RATE,
+  LRL_R_COLLISION, LRL_R_SURVIVAL, LRL_R_DOF_POS_LIMITS, LRL_R_DOF_VEL_LIMITS, LRL_R_TORQUE_LIMITS,
+  LRL_R_TRACKING_LIN_VEL, LRL_R_TRACKING_ANG_VEL, LRL_R_FEET_AIR_TIME, LRL_R_STUMBLE,
+  LRL_R_STAND_STILL, LRL_R_FEET_CONTACT_FORCES, LRL_R_NUM_TERMS
+};
+
+/* Everything LeggedRobot derives from Cfg at construction time (_parse_cfg :1417-1429,
+ * _init_buffers :935-1030, _prepare_reward_function :1074-1110, _get_noise_scale_vec :882-932). */
+typedef struct lrl_env_params {
+  /* timing */
+  float sim_dt;      /* float32(Cfg.sim.dt) */
+  int32_t decimation;
+  float dt;          /* decimation * sim_dt, as float */
+  float gravity[3];
+  /* contact solver (own model; PhysX is closed: see DESIGN.md §physics) */
+  float contact_offset, max_depenetration_velocity, bounce_threshold_velocity;
+  float ground_friction, ground_restitution;
+  int32_t solver_iterations;
+  float baumgarte;
+  /* control (legged_robot.py:653-688) */
+  int32_t control_type; /* 0 = 'P' (only one supported) */
+  float action_scale, hip_scale_reduction, clip_actions;
+  float p_gains[LRL_NUM_DOF], d_gains[LRL_NUM_DOF], default_dof_pos[LRL_NUM_DOF];
+  float torque_limits[LRL_NUM_DOF];
+  float soft_dof_pos_lower[LRL_NUM_DOF], soft_dof_pos_upper[LRL_NUM_DOF], dof_vel_limits[LRL_NUM_DOF];
+  /* bodies */
+  int32_t num_feet, feet[LRL_NUM_LEGS];
+  uint32_t termination_mask, penalised_mask; /* bit b = body b */
+  /* rewards */
+  int32_t num_reward_terms;
+  int32_t reward_term[LRL_MAX_REWARD_TERMS];    /* enum lrl_reward_term */
+  float reward_scale[LRL_MAX_REWARD_TERMS];     /* already x dt, as float */
+  int32_t reward_slot[LRL_MAX_REWARD_TERMS];    /* row of episode_sums / command_sums */
+  int32_t num_sum_keys;                         /* len(reward_scales) after zero removal */
+  float termination_scale;                      /* 0 = no termination term */
+  int32_t termination_slot;
+  int32_t only_positive_rewards;
+  float tracking_sigma, tracking_sigma_yaw, base_height_target, soft_dof_vel_limit, soft_torque_limit,
+      max_contact_force;
+  int32_t use_terminal_body_height;
+  float terminal_body_height;
+  /* observations (compute_observations :342-417) */
+  int32_t num_obs, observe_vel, observe_command;
+  float obs_scale_lin_vel, obs_scale_ang_vel, obs_scale_dof_pos, obs_scale_dof_vel;
+  float commands_scale[3];
+  int32_t add_noise;
+  float noise_vec[LRL_MAX_OBS];
+  float clip_obs;
+  /* privileged obs: (x - shift) * scale for friction, restitution, payload, com, motor strength */
+  float priv_scale[5], priv_shift[5];
+  /* domain randomisation (legged_robot.py:519-560) */
+  int32_t rand_interval;  /* steps */
+  int32_t randomize_motor_strength, randomize_kp, randomize_kd;
+  float motor_strength_range[2], kp_range[2], kd_range[2];
+  /* teleport (legged_robot.py:768-791) */
+  int32_t teleport;
+  float teleport_thresh, teleport_x_offset, terrain_length, terrain_width;
+  int32_t terrain_rows, terrain_cols;
+  /* reset (legged_robot.py:690-755) */
+  float base_init_state[13];
+  int32_t num_history; /* HistoryWrapper length (15) */
+  int32_t auto_reset;  /* 0 = fork semantics (no resets inside step, Q2); 1 = upstream */
+  int32_t max_episode_length;
+} lrl_env_params;
+
+/* ------------------------------------------------------------------------------------------
+ * Sim object and its device tensors (acquire_*_tensor).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct lrl_sim lrl_sim;
+
+enum lrl_dtype { LRL_F32 = 0, LRL_I32 = 1, LRL_U8 = 2 };
+
+typedef struct lrl_tensor {
+  void* data;          /* device pointer */
+  int32_t dtype;       /* enum lrl_dtype */
+  int32_t ndim;
+  int64_t shape[4];
+  int64_t strides[4];  /* in elements */
+} lrl_tensor;
+
+enum lrl_tensor_id {
+  LRL_T_ROOT_STATE = 0,  /* [N,13] pos, quat xyzw, lin vel (COM, world), ang vel (world) */
+  LRL_T_DOF_POS,         /* [N,12] */
+  LRL_T_DOF_VEL,         /* [N,12] */
+  LRL_T_CONTACT_FORCE,   /* [N,B,3] net contact force per body, world frame, last sub-step */
+  LRL_T_RIGID_BODY_STATE,/* [N,B,13] (valid after lrl_sim_refresh_rigid_body_state) */
+  LRL_T_TORQUES,         /* [N,12] last sub-step torques */
+  LRL_T_ACTIONS,         /* [N,12] clipped actions of the last step */
+  LRL_T_LAST_ACTIONS, LRL_T_LAST_DOF_VEL, /* [N,12] */
+  LRL_T_LAST_ROOT_VEL,   /* [N,6] */
+  LRL_T_COMMANDS,        /* [N,4] */
+  LRL_T_OBS,             /* [N,num_obs] */
+  LRL_T_PRIV_OBS,        /* [N,18] */
+  LRL_T_OBS_HISTORY,     /* [N,num_history*num_obs] */
+  LRL_T_REWARD,          /* [N] */
+  LRL_T_RESET,           /* [N] u8 */
+  LRL_T_TIME_OUT,        /* [N] u8 */
+  LRL_T_EPISODE_LENGTH,  /* [N] i32 */
+  LRL_T_EPISODE_SUMS,    /* [num_terms+1(+1 if termination), N]  (dict order of episode_sums) */
+  LRL_T_COMMAND_SUMS,    /* [num_terms(+1) + 5, N]                (dict order of command_sums) */
+  LRL_T_FEET_AIR_TIME,   /* [N,4] */
+  LRL_T_LAST_CONTACTS,   /* [N,4] u8 */
+  LRL_T_FRICTION,        /* [N] */
+  LRL_T_RESTITUTION,     /* [N] */
+  LRL_T_PAYLOAD,         /* [N] */
+  LRL_T_COM_DISPLACEMENT,/* [N,3] */
+  LRL_T_MOTOR_STRENGTH,  /* [N,12] */
+  LRL_T_KP_FACTOR, LRL_T_KD_FACTOR, /* [N,12] */
+  LRL_T_ENV_ORIGINS,     /* [N,3] */
+  LRL_T_BASE_LIN_VEL, LRL_T_BASE_ANG_VEL, LRL_T_PROJECTED_GRAVITY, /* [N,3] body frame */
+  LRL_T_JOINT_POS_TARGET,/* [N,12] */
+  LRL_T_NUM
+};
+
+/* step flags */
+#define LRL_STEP_PHYSICS 1u        /* run the 4 physics sub-steps (off: identity physics, test hook) */
+#define LRL_STEP_HISTORY 2u        /* shift obs into the history buffer (HistoryWrapper.step) */
+#define LRL_STEP_INJECT_UNIFORM 4u /* read noise / DR uniforms from lrl_sim_inject_uniforms buffers */
+
+int32_t lrl_abi_version(void);
+const char* lrl_last_error(void);
+int32_t lrl_device_count(void);
+
+int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int32_t num_envs,
+                       int64_t global_env_offset, uint64_t seed, int32_t device, lrl_sim** out);
+int32_t lrl_sim_destroy(lrl_sim* sim);
+int32_t lrl_sim_tensor(lrl_sim* sim, int32_t tensor_id, lrl_tensor* out);
+
+/* Initialise the per-env domain randomisation draws (legged_robot.py:519-542, 544-560) */
+int32_t lrl_sim_randomize(lrl_sim* sim, const float* friction_range, const float* restitution_range,
+                          const float* payload_range, const float* com_range, uint32_t which, void* stream);
+
+/* One policy step for all envs: the fused LeggedRobot.step hot path. `actions` [N,12] f32 device. */
+int32_t lrl_sim_step(lrl_sim* sim, const float* actions, uint32_t flags, void* stream);
+
+/* Injected uniforms for parity tests: noise_u [N,num_obs], dr_u [N] (NaN = no redraw). */
+int32_t lrl_sim_inject_uniforms(lrl_sim* sim, const float* noise_u, const float* dr_u);
+
+int32_t lrl_sim_reset_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, void* stream);
+int32_t lrl_sim_set_root_state_indexed(lrl_sim* sim, const float* root /*[N,13] full tensor*/,
+                                       const int32_t* env_ids, int32_t n, void* stream);
+int32_t lrl_sim_set_dof_state_indexed(lrl_sim* sim, const float* dof_pos, const float* dof_vel,
+                                      const int32_t* env_ids, int32_t n, void* stream);
+int32_t lrl_sim_refresh_rigid_body_state(lrl_sim* sim, void* stream);
+/* HistoryWrapper.get_observations side effect (history_wrapper.py:26-30) */
+int32_t lrl_sim_shift_history(lrl_sim* sim, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * PPO numeric core.
+ * ------------------------------------------------------------------------------------------ */
+
+/* GAE + advantage normalisation (rollout_storage.py:76-90). rewards/values/returns/advantages
+ * [T,N] f32, dones [T,N] u8, last_values [N].  Normalisation uses mean and unbiased std over T*N. */
+int32_t lrl_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+                int32_t T, int32_t N, float gamma, float lam, float* returns, float* advantages,
+                float* workspace /* >= 4*1024 floats */, void* stream);
+
+/* Teacher-policy MLP stack (actor_critic.py:23-173) in one flat fp32 parameter block. Layer l of a
+ * chain is W_l [out,in] row-major followed by b_l [out] (torch nn.Linear layout). */
+typedef struct lrl_mlp_desc {
+  int32_t num_layers;
+  int32_t dims[8];              /* dims[0] = in, dims[l+1] = out of layer l */
+  const float* weight[7];       /* device pointers */
+  const float* bias[7];
+} lrl_mlp_desc;
+
+/* Rollout step of PPO.act (ppo.py:62-74): latent = enc(priv); mu = actor([obs, latent]);
+ * a = mu + std * eps; value = critic([obs, latent]); logp = sum log N(a; mu, std).
+ * eps [N,12] is given (injected) or drawn from the counter RNG when eps == NULL.
+ * Optional storage writes (rollout_storage.py:60-70): if `store` != NULL the transition fields are
+ * written to row `store_row` of the [T,N,...] storage arrays. */
+typedef struct lrl_rollout_store {
+  float *obs, *priv, *hist, *actions, *values, *logp, *mu, *sigma;
+  int32_t hist_dim;
+} lrl_rollout_store;
+
+int32_t lrl_policy_act(const lrl_mlp_desc* encoder, const lrl_mlp_desc* actor, const lrl_mlp_desc* critic,
+                       const float* std, const float* obs, const float* priv, const float* hist, int32_t n,
+                       int32_t num_obs, int32_t num_priv, const float* eps, uint64_t seed, uint64_t counter,
+                       float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
+                       int32_t store_row, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LRL_H_ */

@@ -1,0 +1,125 @@
+"""ORACLE (test infrastructure only): ctypes front-end to oracle/build/liblrl_oracle.so plus numpy
+restatements of the PPO bookkeeping.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the
+product path (rapid-locomotion-rl_amd/) never does.
+
+* ``env_step``         — lrl_oracle.c:lrlo_env_step (LeggedRobot.step, legged_robot.py:106-137).
+* ``physics_substep``  — lrl_oracle.c:lrlo_physics_substep (own dense dynamics; PhysX parity unpinned).
+* ``gae``              — RolloutStorage.compute_returns (rollout_storage.py:76-90) in numpy.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "build", "liblrl_oracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            build()
+        _lib = C.CDLL(SO)
+        _lib.lrlo_env_step.restype = C.c_int
+        _lib.lrlo_physics_substep.restype = C.c_int
+        _lib.lrlo_energy.restype = C.c_double
+    return _lib
+
+
+ENV_FIELDS = ["root", "dof_pos", "dof_vel", "contact", "torques", "actions", "last_actions", "last_dof_vel",
+              "last_root_vel", "commands", "obs", "priv", "hist", "rew", "reset", "last_contacts", "episode_length",
+              "episode_sums", "command_sums", "feet_air_time", "friction", "restitution", "payload", "com",
+              "motor_strength", "kp", "kd", "base_lin_vel", "base_ang_vel", "projected_gravity",
+              "joint_pos_target"]
+
+
+class _Env(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in ENV_FIELDS]
+
+
+def _dtype(f):
+    return {"reset": np.uint8, "last_contacts": np.uint8, "episode_length": np.int32}.get(f, np.float32)
+
+
+def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs):
+    """Zero-initialised logical-layout host state."""
+    shp = dict(root=(n, 13), dof_pos=(n, 12), dof_vel=(n, 12), contact=(n, num_bodies, 3), torques=(n, 12),
+               actions=(n, 12), last_actions=(n, 12), last_dof_vel=(n, 12), last_root_vel=(n, 6),
+               commands=(n, 4), obs=(n, num_obs), priv=(n, 18), hist=(n, num_hist * num_obs), rew=(n,),
+               reset=(n,), last_contacts=(n, 4), episode_length=(n,), episode_sums=(n_es, n),
+               command_sums=(n_cs, n), feet_air_time=(n, 4), friction=(n,), restitution=(n,), payload=(n,),
+               com=(n, 3), motor_strength=(n, 12), kp=(n, 12), kd=(n, 12), base_lin_vel=(n, 3),
+               base_ang_vel=(n, 3), projected_gravity=(n, 3), joint_pos_target=(n, 12))
+    st = {k: np.zeros(v, _dtype(k)) for k, v in shp.items()}
+    st["root"][:, 6] = 1.0
+    st["motor_strength"][:] = 1
+    st["kp"][:] = 1
+    st["kd"][:] = 1
+    return st
+
+
+def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_step_counter=1, noise_u=None,
+             dr_u=None):
+    """In-place LeggedRobot.step on a logical-layout state dict (see make_state)."""
+    for k in ENV_FIELDS:
+        a = state[k]
+        assert a.flags["C_CONTIGUOUS"] and a.dtype == _dtype(k), k
+    e = _Env(**{k: state[k].ctypes.data for k in ENV_FIELDS})
+    n = state["root"].shape[0]
+    act = np.ascontiguousarray(actions, np.float32)
+    nu = np.ascontiguousarray(noise_u, np.float32) if noise_u is not None else None
+    du = np.ascontiguousarray(dr_u, np.float32) if dr_u is not None else None
+    rc = lib().lrlo_env_step(C.byref(model), C.byref(params), C.c_int32(n), C.c_int64(env_offset),
+                             C.c_uint64(seed), C.c_int64(common_step_counter), C.byref(e),
+                             act.ctypes.data_as(C.c_void_p), C.c_uint32(flags),
+                             nu.ctypes.data_as(C.c_void_p) if nu is not None else None,
+                             du.ctypes.data_as(C.c_void_p) if du is not None else None)
+    if rc != 0:
+        raise RuntimeError("oracle env_step failed (non-SPD mass matrix)")
+    return state
+
+
+def physics_substep(model, params, root, q, qd, tau, friction, restitution, payload, com):
+    f = lambda a, n: np.ascontiguousarray(a, np.float32).reshape(n)
+    root, q, qd, tau, com = f(root, 13), f(q, 12), f(qd, 12), f(tau, 12), f(com, 3)
+    ro, qo, qdo = np.zeros(13, np.float32), np.zeros(12, np.float32), np.zeros(12, np.float32)
+    co = np.zeros((model.num_bodies, 3), np.float32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)
+    n = lib().lrlo_physics_substep(C.byref(model), C.byref(params), p(root), p(q), p(qd), p(tau),
+                                   C.c_float(friction), C.c_float(restitution), C.c_float(payload), p(com), p(ro),
+                                   p(qo), p(qdo), p(co))
+    return ro, qo, qdo, co, n
+
+
+def energy(model, params, root, q, qd, payload=0.0, com=(0, 0, 0)):
+    f = lambda a, n: np.ascontiguousarray(a, np.float32).reshape(n)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)
+    root, q, qd, com = f(root, 13), f(q, 12), f(qd, 12), f(com, 3)
+    return lib().lrlo_energy(C.byref(model), C.byref(params), p(root), p(q), p(qd), C.c_float(payload), p(com))
+
+
+def gae(rewards, dones, values, last_values, gamma, lam):
+    """rollout_storage.py:76-90 in numpy float32 (same recurrence and normalisation)."""
+    T = rewards.shape[0]
+    rewards, values = rewards.astype(np.float32), values.astype(np.float32)
+    returns = np.zeros_like(values)
+    adv = np.zeros_like(values[0])
+    g, gl = np.float32(gamma), np.float32(gamma * lam)
+    for t in reversed(range(T)):
+        nv = last_values.astype(np.float32) if t == T - 1 else values[t + 1]
+        nt = np.float32(1.0) - dones[t].astype(np.float32)
+        delta = rewards[t] + nt * g * nv - values[t]
+        adv = delta + nt * gl * adv
+        returns[t] = adv + values[t]
+    a = returns - values
+    return returns, (a - a.mean(dtype=np.float64)) / (a.std(ddof=1, dtype=np.float64) + 1e-8)

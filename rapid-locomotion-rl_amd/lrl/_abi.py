@@ -1,0 +1,130 @@
+"""ctypes mirror of include/lrl.h (structs, enums) and the loader for liblrl.so.
+
+The product path goes through liblrl.so only: if the library is missing or no GPU is visible the
+env / PPO entry points raise instead of falling back to any CPU or eager implementation.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "liblrl.so")
+
+MAX_BODIES, MAX_SPHERES, NUM_DOF, NUM_LEGS, MAX_OBS, MAX_REWARD_TERMS, NUM_PRIV = 20, 40, 12, 4, 64, 24, 18
+f32, i32, u32 = C.c_float, C.c_int32, C.c_uint32
+
+REWARD_TERMS = ["lin_vel_z", "ang_vel_xy", "orientation", "base_height", "torques", "energy",
+                "energy_expenditure", "dof_vel", "dof_acc", "action_rate", "collision", "survival",
+                "dof_pos_limits", "dof_vel_limits", "torque_limits", "tracking_lin_vel", "tracking_ang_vel",
+                "feet_air_time", "stumble", "stand_still", "feet_contact_forces"]
+
+STEP_PHYSICS, STEP_HISTORY, STEP_INJECT_UNIFORM = 1, 2, 4
+
+(T_ROOT_STATE, T_DOF_POS, T_DOF_VEL, T_CONTACT_FORCE, T_RIGID_BODY_STATE, T_TORQUES, T_ACTIONS, T_LAST_ACTIONS,
+ T_LAST_DOF_VEL, T_LAST_ROOT_VEL, T_COMMANDS, T_OBS, T_PRIV_OBS, T_OBS_HISTORY, T_REWARD, T_RESET, T_TIME_OUT,
+ T_EPISODE_LENGTH, T_EPISODE_SUMS, T_COMMAND_SUMS, T_FEET_AIR_TIME, T_LAST_CONTACTS, T_FRICTION, T_RESTITUTION,
+ T_PAYLOAD, T_COM_DISPLACEMENT, T_MOTOR_STRENGTH, T_KP_FACTOR, T_KD_FACTOR, T_ENV_ORIGINS, T_BASE_LIN_VEL,
+ T_BASE_ANG_VEL, T_PROJECTED_GRAVITY, T_JOINT_POS_TARGET, T_NUM) = range(35)
+
+
+class LrlModel(C.Structure):
+    _fields_ = [
+        ("num_bodies", i32), ("body_leg", i32 * MAX_BODIES), ("body_link", i32 * MAX_BODIES),
+        ("joint_xyz", f32 * 3 * 3 * NUM_LEGS), ("joint_quat", f32 * 4 * 3 * NUM_LEGS),
+        ("joint_axis", f32 * 3 * 3 * NUM_LEGS), ("foot_xyz", f32 * 3 * NUM_LEGS),
+        ("base_mass", f32), ("base_com", f32 * 3), ("base_inertia", f32 * 6),
+        ("link_mass", f32 * 3 * NUM_LEGS), ("link_com", f32 * 3 * 3 * NUM_LEGS),
+        ("link_inertia", f32 * 6 * 3 * NUM_LEGS),
+        ("num_spheres", i32), ("sphere_body", i32 * MAX_SPHERES), ("sphere_pos", f32 * 3 * MAX_SPHERES),
+        ("sphere_radius", f32 * MAX_SPHERES),
+        ("dof_lower", f32 * NUM_DOF), ("dof_upper", f32 * NUM_DOF), ("dof_effort", f32 * NUM_DOF),
+        ("dof_velocity", f32 * NUM_DOF),
+    ]
+
+
+class LrlEnvParams(C.Structure):
+    _fields_ = [
+        ("sim_dt", f32), ("decimation", i32), ("dt", f32), ("gravity", f32 * 3),
+        ("contact_offset", f32), ("max_depenetration_velocity", f32), ("bounce_threshold_velocity", f32),
+        ("ground_friction", f32), ("ground_restitution", f32), ("solver_iterations", i32), ("baumgarte", f32),
+        ("control_type", i32), ("action_scale", f32), ("hip_scale_reduction", f32), ("clip_actions", f32),
+        ("p_gains", f32 * NUM_DOF), ("d_gains", f32 * NUM_DOF), ("default_dof_pos", f32 * NUM_DOF),
+        ("torque_limits", f32 * NUM_DOF), ("soft_dof_pos_lower", f32 * NUM_DOF),
+        ("soft_dof_pos_upper", f32 * NUM_DOF), ("dof_vel_limits", f32 * NUM_DOF),
+        ("num_feet", i32), ("feet", i32 * NUM_LEGS), ("termination_mask", u32), ("penalised_mask", u32),
+        ("num_reward_terms", i32), ("reward_term", i32 * MAX_REWARD_TERMS), ("reward_scale", f32 * MAX_REWARD_TERMS),
+        ("reward_slot", i32 * MAX_REWARD_TERMS), ("num_sum_keys", i32), ("termination_scale", f32),
+        ("termination_slot", i32), ("only_positive_rewards", i32),
+        ("tracking_sigma", f32), ("tracking_sigma_yaw", f32), ("base_height_target", f32),
+        ("soft_dof_vel_limit", f32), ("soft_torque_limit", f32), ("max_contact_force", f32),
+        ("use_terminal_body_height", i32), ("terminal_body_height", f32),
+        ("num_obs", i32), ("observe_vel", i32), ("observe_command", i32),
+        ("obs_scale_lin_vel", f32), ("obs_scale_ang_vel", f32), ("obs_scale_dof_pos", f32),
+        ("obs_scale_dof_vel", f32), ("commands_scale", f32 * 3), ("add_noise", i32), ("noise_vec", f32 * MAX_OBS),
+        ("clip_obs", f32), ("priv_scale", f32 * 5), ("priv_shift", f32 * 5),
+        ("rand_interval", i32), ("randomize_motor_strength", i32), ("randomize_kp", i32), ("randomize_kd", i32),
+        ("motor_strength_range", f32 * 2), ("kp_range", f32 * 2), ("kd_range", f32 * 2),
+        ("teleport", i32), ("teleport_thresh", f32), ("teleport_x_offset", f32), ("terrain_length", f32),
+        ("terrain_width", f32), ("terrain_rows", i32), ("terrain_cols", i32),
+        ("base_init_state", f32 * 13), ("num_history", i32), ("auto_reset", i32), ("max_episode_length", i32),
+    ]
+
+
+class LrlTensor(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("dtype", i32), ("ndim", i32), ("shape", C.c_int64 * 4),
+                ("strides", C.c_int64 * 4)]
+
+
+class LrlMlpDesc(C.Structure):
+    _fields_ = [("num_layers", i32), ("dims", i32 * 8), ("weight", C.c_void_p * 7), ("bias", C.c_void_p * 7)]
+
+
+class LrlRolloutStore(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("priv", C.c_void_p), ("hist", C.c_void_p), ("actions", C.c_void_p),
+                ("values", C.c_void_p), ("logp", C.c_void_p), ("mu", C.c_void_p), ("sigma", C.c_void_p),
+                ("hist_dim", i32)]
+
+
+def fill(struct, **kw):
+    """Assign python values (scalars / nested lists) into a ctypes struct."""
+    for k, v in kw.items():
+        cur = getattr(struct, k)
+        if isinstance(cur, C.Array):
+            _fill_array(cur, v)
+        else:
+            setattr(struct, k, v)
+    return struct
+
+
+def _fill_array(arr, v):
+    for i, x in enumerate(v):
+        if isinstance(arr[i], C.Array):
+            _fill_array(arr[i], x)
+        else:
+            arr[i] = x
+
+
+_lib = None
+
+
+def lib():
+    """liblrl.so, loaded once.  Raises (no fallback) if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"liblrl.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        L.lrl_last_error.restype = C.c_char_p
+        for name in ["lrl_sim_create", "lrl_sim_destroy", "lrl_sim_tensor", "lrl_sim_step", "lrl_sim_reset_idx",
+                     "lrl_sim_set_root_state_indexed", "lrl_sim_set_dof_state_indexed", "lrl_sim_inject_uniforms",
+                     "lrl_sim_refresh_rigid_body_state", "lrl_sim_shift_history", "lrl_sim_randomize", "lrl_gae",
+                     "lrl_policy_act", "lrl_abi_version", "lrl_device_count"]:
+            getattr(L, name).restype = C.c_int32
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().lrl_last_error()
+        raise RuntimeError(f"liblrl error {rc}: {msg.decode() if msg else ''}")
+    return rc

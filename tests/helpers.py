@@ -1,0 +1,33 @@
+"""Shared test helpers: configs, fixture loading, oracle state set-up."""
+import os
+
+import numpy as np
+
+from lrl import config as lcfg
+from lrl import params as lparams
+from lrl.robot import load_robot
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+ROBOT_FILES = {"mc": "mini_cheetah.urdf", "go1": "go1.urdf"}
+
+
+def make(robot="mc", **over):
+    cfg = lcfg.make_cfg()
+    (lcfg.config_mini_cheetah if robot == "mc" else lcfg.config_go1)(cfg)
+    for k, v in over.items():
+        node = cfg
+        *ps, leaf = k.split(".")
+        for p in ps:
+            node = getattr(node, p)
+        setattr(node, leaf, v)
+    rob = load_robot(ROBOT_FILES[robot])
+    if robot == "mc":
+        cfg.terrain.x_offset = 0
+    P = lparams.build_params(cfg, rob)
+    M = lparams.build_model(rob)
+    return cfg, rob, M, P
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
