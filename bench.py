@@ -1,0 +1,154 @@
+"""Benchmark: env-steps/s for 4096 Mini Cheetah envs per GPU (weak scaling) + PPO iters/s.
+
+One timed "step" = one PPO iteration of mini_gym_learn's Runner.learn (mini_gym_learn/ppo/
+__init__.py:123-242): 24 rollout steps (fused policy kernel + fused env-step kernel per step),
+GAE, then 5 epochs x 4 minibatches of the PPO + adaptation update.  value = all ranks' env-steps
+(N_gpu x 4096 x 24 x K) / max-over-ranks wall time of the K timed iterations.
+
+  python bench.py [--gpus N --steps K --warmup W]           (N > 1: under torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ENVS_PER_GPU = 4096
+B_ENV = 1325            # algorithmic HBM bytes per env-step; history shift adds 4872
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(seconds=12.0):
+    """The CPU oracle (oracle/lrl_oracle.c: dense fp64 dynamics + fp32 bookkeeping), one core, on a
+    bounded sample of the same workload: 256 Mini Cheetah envs stepping with random actions."""
+    from oracle import oracle
+    from lrl import _abi
+    from lrl import config as lcfg
+    from lrl import params as lparams
+    from lrl.robot import load_robot
+    cfg = lcfg.make_cfg()
+    lcfg.config_mini_cheetah(cfg)
+    cfg.terrain.x_offset = 0
+    rob = load_robot("mini_cheetah.urdf")
+    P, M = lparams.build_params(cfg, rob), lparams.build_model(rob)
+    n = 256
+    st = oracle.make_state(n, M.num_bodies, P.num_obs, P.num_history, P.num_sum_keys + 1, P.num_sum_keys + 5)
+    st["root"][:, 2] = 0.32
+    st["root"][:, :2] = np.random.default_rng(0).uniform(10, 60, (n, 2))
+    st["dof_pos"][:] = np.array(P.default_dof_pos[:], np.float32)
+    st["friction"][:] = 1.0
+    rng = np.random.default_rng(1)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        oracle.env_step(M, P, st, rng.normal(size=(n, 12)).astype(np.float32) * 0.3,
+                        _abi.STEP_PHYSICS | _abi.STEP_HISTORY, common_step_counter=steps + 1)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return dict(value=round(n * steps / dt, 1), unit="env-steps/s", cores=1, kind="port",
+                sample=f"{n} Mini Cheetah envs x {steps} steps ({dt:.1f} s), oracle/lrl_oracle.c, 1 thread; "
+                       "the reference's Isaac Gym CPU pipeline is proprietary and absent (BASELINE.md §3)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+
+    from lrl import config as lcfg
+    from lrl.env import LeggedRobotEnv
+    from lrl.history import HistoryWrapper
+    from lrl.ppo import runner as R
+
+    cfg = lcfg.make_cfg()
+    lcfg.config_mini_cheetah(cfg)
+    cfg.env.num_envs = ENVS_PER_GPU
+    R.RunnerArgs.save_interval = 0
+    R.RunnerArgs.log_freq = 10 ** 9
+    env = HistoryWrapper(LeggedRobotEnv(dev, cfg=cfg, seed=1234, env_offset=rank * ENVS_PER_GPU))
+    g = torch.Generator(device=dev).manual_seed(1 + rank)
+    cmd = torch.rand(ENVS_PER_GPU, 3, device=dev, generator=g)
+    env.env.commands[:, 0] = cmd[:, 0] * 1.2 - 0.6
+    env.env.commands[:, 1] = cmd[:, 1] * 1.2 - 0.6
+    env.env.commands[:, 2] = cmd[:, 2] * 2.0 - 1.0
+    runner = R.Runner(env, device=dev, seed=1234)
+    runner.learn(args.warmup, init_at_random_ep_len=True)
+    timer = []
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    env.env.kernel_timer = timer
+    t0 = time.perf_counter()
+    runner.learn(args.steps)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    env.env.kernel_timer = None
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in timer]))
+    # env-only rate: the fused step kernel alone, random actions, same env
+    a = torch.randn(ENVS_PER_GPU, 12, device=dev) * 0.3
+    for _ in range(10):
+        env.step(a)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    ne = 100
+    for _ in range(ne):
+        env.step(a)
+    torch.cuda.synchronize()
+    env_only = ENVS_PER_GPU * ne / (time.perf_counter() - te)
+
+    steps_total = world * ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env * args.steps
+    value = steps_total / elapsed
+    if rank == 0:
+        achieved = B_ENV * ENVS_PER_GPU / (k_ms * 1e-3) / 1e9
+        out = {
+            "metric": "env-steps/sec, 4096 Mini Cheetah envs, 1/2/4/8 MI355X; PPO iters/sec",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "4096 Mini Cheetah envs flat terrain, PPO teacher policy (BASELINE configs[1])",
+                       "envs_per_gpu": ENVS_PER_GPU, "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
+                       "parallelism": f"dp{world}", "policy": "ActorCritic 42/18/630->12, random init"},
+            "ppo_iters_per_s": round(args.steps / elapsed, 3),
+            "env_only_env_steps_per_s_per_gpu": round(env_only, 1),
+            "env_step_kernel_ms": round(k_ms, 4),
+            "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel", "achieved": round(achieved, 3),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": None,
+                         "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch; the kernel is "
+                                 "latency/VALU-bound (one env per lane), see DESIGN.md"},
+            "reference_context": {"upstream_example_run_env_steps_per_s": 41176, "upstream_ppo_iters_per_s": 0.429,
+                                  "hardware": "unspecified NVIDIA GPU, 4000 envs (BASELINE.md §1)"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -226,6 +226,12 @@ int32_t lrl_sim_step(lrl_sim* sim, const float* actions, uint32_t flags, void* s
 int32_t lrl_sim_inject_uniforms(lrl_sim* sim, const float* noise_u, const float* dr_u);
 
 int32_t lrl_sim_reset_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, void* stream);
+/* reset_idx with the root-state policy made explicit: root_mode 0 leaves the root untouched (the
+ * fork's custom-origin quirk), 1 writes base_init_state + env_origin + (xo, yo). */
+int32_t lrl_sim_reset_idx_ex(lrl_sim* sim, const int32_t* env_ids, int32_t n, int32_t root_mode, float xo, float yo,
+                             void* stream);
+/* common_step_counter (legged_robot.py:153); lrl_sim_step increments it before the launch */
+int32_t lrl_sim_set_step_counter(lrl_sim* sim, int64_t counter);
 int32_t lrl_sim_set_root_state_indexed(lrl_sim* sim, const float* root /*[N,13] full tensor*/,
                                        const int32_t* env_ids, int32_t n, void* stream);
 int32_t lrl_sim_set_dof_state_indexed(lrl_sim* sim, const float* dof_pos, const float* dof_vel,
@@ -242,7 +248,14 @@ int32_t lrl_sim_shift_history(lrl_sim* sim, void* stream);
  * [T,N] f32, dones [T,N] u8, last_values [N].  Normalisation uses mean and unbiased std over T*N. */
 int32_t lrl_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
                 int32_t T, int32_t N, float gamma, float lam, float* returns, float* advantages,
-                float* workspace /* >= 4*1024 floats */, void* stream);
+                float* workspace /* >= 4096 floats */, void* stream);
+
+/* Multi-GPU split of lrl_gae: returns + raw advantages and stats = (sum, sum of squares, count) as
+ * fp64 (all-reduce them across ranks), then normalise with the (global) stats. */
+int32_t lrl_gae_partial(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
+                        int32_t T, int32_t N, float gamma, float lam, float* returns, float* advantages,
+                        float* workspace, double* stats /*[3] device*/, void* stream);
+int32_t lrl_adv_normalize(float* advantages, int64_t total, const double* stats /*[3] device*/, void* stream);
 
 /* Teacher-policy MLP stack (actor_critic.py:23-173) in one flat fp32 parameter block. Layer l of a
  * chain is W_l [out,in] row-major followed by b_l [out] (torch nn.Linear layout). */

@@ -1,0 +1,233 @@
+// lrl_aux.hip — the non-step env kernels: reset_idx (device part), indexed state setters,
+// rigid-body-state refresh (forward kinematics), HistoryWrapper shift, DR initialisation.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/lrl_philox.h"
+#include "lrl_kparams.h"
+
+namespace lrl {
+
+// reset_idx (legged_robot.py:227-290) device part: _randomize_dof_props (:544-560), _reset_dofs
+// (:690-712), _reset_root_states (:714-755), buffer zeroing (:255-259).  root_mode: 0 = leave the root
+// (fork quirk Q4 for custom origins), 1 = base_init_state + env_origin (+ xy_offset).
+__global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
+                             int32_t root_mode, float xy_off_x, float xy_off_y, int64_t counter) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const lrl_env_params& P = K->p;
+  const int N = S.stride;
+  int e = ids[t];
+  if (e < 0 || e >= S.n) return;
+  uint64_t genv = (uint64_t)(S.env_offset + e);
+  lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)counter, (LRL_RNG_RESET << 16) ^ (uint32_t)(counter >> 32), 0, S.seed);
+  int k = 0;
+  if (P.randomize_motor_strength) {
+    float v = lrl_u01(r.v[k++]) * (P.motor_strength_range[1] - P.motor_strength_range[0]) + P.motor_strength_range[0];
+    for (int j = 0; j < 12; ++j) S.motor_strength[j * N + e] = v;
+  }
+  if (P.randomize_kp) {
+    float v = lrl_u01(r.v[k++]) * (P.kp_range[1] - P.kp_range[0]) + P.kp_range[0];
+    for (int j = 0; j < 12; ++j) S.kp[j * N + e] = v;
+  }
+  if (P.randomize_kd) {
+    float v = lrl_u01(r.v[k++]) * (P.kd_range[1] - P.kd_range[0]) + P.kd_range[0];
+    for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
+  }
+  for (int j = 0; j < 12; ++j) {
+    S.dof_pos[j * N + e] = P.default_dof_pos[j];
+    S.dof_vel[j * N + e] = 0.f;
+    S.last_actions[j * N + e] = 0.f;
+    S.last_dof_vel[j * N + e] = 0.f;
+  }
+  if (root_mode == 1) {
+    for (int c = 0; c < 13; ++c) {
+      float v = P.base_init_state[c];
+      if (c < 3) v += S.env_origins[c * N + e];
+      if (c == 0) v += xy_off_x;
+      if (c == 1) v += xy_off_y;
+      S.root[c * N + e] = v;
+    }
+  }
+  for (int f = 0; f < 4; ++f) S.feet_air_time[f * N + e] = 0.f;
+  S.episode_length[e] = 0;
+  S.reset[e] = 1;
+}
+
+// gym.set_actor_root_state_tensor_indexed: rows `ids` of an AoS [n,13] source
+__global__ void set_root_kernel(KState S, const float* __restrict__ src, const int32_t* __restrict__ ids, int32_t n) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int e = ids[t];
+  if (e < 0 || e >= S.n) return;
+  for (int c = 0; c < 13; ++c) S.root[c * S.stride + e] = src[(size_t)e * 13 + c];
+}
+
+__global__ void set_dof_kernel(KState S, const float* __restrict__ pos, const float* __restrict__ vel,
+                               const int32_t* __restrict__ ids, int32_t n) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int e = ids[t];
+  if (e < 0 || e >= S.n) return;
+  for (int j = 0; j < 12; ++j) {
+    S.dof_pos[j * S.stride + e] = pos[(size_t)e * 12 + j];
+    S.dof_vel[j * S.stride + e] = vel[(size_t)e * 12 + j];
+  }
+}
+
+// forward kinematics -> rigid body state [B][13][N]: pos, quat (xyzw), lin vel (origin), ang vel; world
+__device__ inline void mat_to_quat(const float* m, float* q) {
+  float t = m[0] + m[4] + m[8];
+  if (t > 0.f) {
+    float s = sqrtf(t + 1.f) * 2.f;
+    q[3] = 0.25f * s; q[0] = (m[7] - m[5]) / s; q[1] = (m[2] - m[6]) / s; q[2] = (m[3] - m[1]) / s;
+  } else if (m[0] > m[4] && m[0] > m[8]) {
+    float s = sqrtf(1.f + m[0] - m[4] - m[8]) * 2.f;
+    q[3] = (m[7] - m[5]) / s; q[0] = 0.25f * s; q[1] = (m[1] + m[3]) / s; q[2] = (m[2] + m[6]) / s;
+  } else if (m[4] > m[8]) {
+    float s = sqrtf(1.f + m[4] - m[0] - m[8]) * 2.f;
+    q[3] = (m[2] - m[6]) / s; q[0] = (m[1] + m[3]) / s; q[1] = 0.25f * s; q[2] = (m[5] + m[7]) / s;
+  } else {
+    float s = sqrtf(1.f + m[8] - m[0] - m[4]) * 2.f;
+    q[3] = (m[3] - m[1]) / s; q[0] = (m[2] + m[6]) / s; q[1] = (m[5] + m[7]) / s; q[2] = 0.25f * s;
+  }
+}
+__device__ inline void mm3(const float* A, const float* B, float* C) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+__device__ inline void mv3(const float* A, const float* v, float* o) {
+  for (int i = 0; i < 3; ++i) o[i] = A[3 * i] * v[0] + A[3 * i + 1] * v[1] + A[3 * i + 2] * v[2];
+}
+__device__ inline void cr3(const float* a, const float* b, float* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__global__ void rigid_body_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ body_leg,
+                                  const int32_t* __restrict__ body_link, const float* __restrict__ foot_xyz) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  const int N = S.stride;
+  float q[4], p[3], V[3], W[3];
+  for (int k = 0; k < 4; ++k) q[k] = S.root[(3 + k) * N + e];
+  for (int k = 0; k < 3; ++k) { p[k] = S.root[k * N + e]; V[k] = S.root[(7 + k) * N + e]; W[k] = S.root[(10 + k) * N + e]; }
+  float x = q[0], y = q[1], z = q[2], w = q[3];
+  float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w), 2 * (x * y + z * w),
+                1 - 2 * (x * x + z * z), 2 * (y * z - x * w), 2 * (x * z - y * w), 2 * (y * z + x * w),
+                1 - 2 * (x * x + y * y)};
+  // base origin velocity = COM velocity - w x (R c)
+  float c[3] = {S.com[e], S.com[N + e], S.com[2 * N + e]}, Rc[3], wc[3], vo[3];
+  mv3(R, c, Rc);
+  cr3(W, Rc, wc);
+  for (int k = 0; k < 3; ++k) vo[k] = V[k] - wc[k];
+  for (int b = 0; b < K->num_bodies; ++b) {
+    int leg = body_leg[b], link = body_link[b];
+    float Rb[9], ob[3], vb[3], wb[3];
+    for (int k = 0; k < 9; ++k) Rb[k] = R[k];
+    for (int k = 0; k < 3; ++k) { ob[k] = p[k]; vb[k] = vo[k]; wb[k] = W[k]; }
+    if (leg >= 0) {
+      const KLeg& L = K->leg[leg];
+      int nj = link > 2 ? 3 : link + 1;
+      for (int j = 0; j < nj; ++j) {
+        float off[3], tmp[9], Rj[9], ax[3], axw[3];
+        mv3(Rb, L.xyz[j], off);
+        for (int k = 0; k < 3; ++k) ob[k] += off[k];
+        // velocity of the new origin: v += w x off
+        float wo[3];
+        cr3(wb, off, wo);
+        for (int k = 0; k < 3; ++k) vb[k] += wo[k];
+        mm3(Rb, L.rfix[j], tmp);
+        float th = S.dof_pos[(3 * leg + j) * N + e], sn, cs;
+        sincosf(th, &sn, &cs);
+        float t1 = 1.f - cs;
+        for (int k = 0; k < 3; ++k) ax[k] = L.axis[j][k];
+        float Ra[9] = {t1 * ax[0] * ax[0] + cs, t1 * ax[0] * ax[1] - sn * ax[2], t1 * ax[0] * ax[2] + sn * ax[1],
+                       t1 * ax[0] * ax[1] + sn * ax[2], t1 * ax[1] * ax[1] + cs, t1 * ax[1] * ax[2] - sn * ax[0],
+                       t1 * ax[0] * ax[2] - sn * ax[1], t1 * ax[1] * ax[2] + sn * ax[0], t1 * ax[2] * ax[2] + cs};
+        mm3(tmp, Ra, Rj);
+        for (int k = 0; k < 9; ++k) Rb[k] = Rj[k];
+        mv3(Rb, ax, axw);
+        float qd = S.dof_vel[(3 * leg + j) * N + e];
+        for (int k = 0; k < 3; ++k) wb[k] += qd * axw[k];
+      }
+      if (link == 3) {
+        float off[3], wo[3];
+        mv3(Rb, &foot_xyz[3 * leg], off);
+        cr3(wb, off, wo);
+        for (int k = 0; k < 3; ++k) { ob[k] += off[k]; vb[k] += wo[k]; }
+      }
+    }
+    float qb[4];
+    mat_to_quat(Rb, qb);
+    float* out = S.rb_state + (size_t)b * 13 * N;
+    for (int k = 0; k < 3; ++k) out[k * N + e] = ob[k];
+    for (int k = 0; k < 4; ++k) out[(3 + k) * N + e] = qb[k];
+    for (int k = 0; k < 3; ++k) { out[(7 + k) * N + e] = vb[k]; out[(10 + k) * N + e] = wb[k]; }
+  }
+}
+
+// HistoryWrapper.get_observations shift: hist = cat(hist[:, NO:], obs)  (history_wrapper.py:26-30)
+__global__ void shift_history_kernel(KState S, int NO, int H) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  float* h = S.hist + (size_t)e * H;
+  const float* o = S.obs + (size_t)e * NO;
+  for (int k = 0; k < H - NO; ++k) h[k] = h[k + NO];
+  for (int k = 0; k < NO; ++k) h[H - NO + k] = o[k];
+}
+
+// _randomize_rigid_body_props (legged_robot.py:519-542) for all envs
+__global__ void randomize_kernel(KState S, float f0, float f1, float r0, float r1, float p0, float p1, float c0,
+                                 float c1, uint32_t which) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.stride) return;
+  const int N = S.stride;
+  uint64_t genv = (uint64_t)(S.env_offset + e);
+  lrl_u32x4 a = lrl_philox((uint32_t)genv, 0u, (LRL_RNG_INIT << 16), 0, S.seed);
+  lrl_u32x4 b = lrl_philox((uint32_t)genv, 0u, (LRL_RNG_INIT << 16), 1, S.seed);
+  if (which & 1u) S.payload[e] = lrl_u01(a.v[0]) * (p1 - p0) + p0;
+  if (which & 2u)
+    for (int k = 0; k < 3; ++k) S.com[k * N + e] = lrl_u01(k == 0 ? a.v[1] : k == 1 ? a.v[2] : a.v[3]) * (c1 - c0) + c0;
+  if (which & 4u) S.friction[e] = lrl_u01(b.v[0]) * (f1 - f0) + f0;
+  if (which & 8u) S.restitution[e] = lrl_u01(b.v[1]) * (r1 - r0) + r0;
+}
+
+}  // namespace lrl
+
+extern "C" {
+hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* ids, int32_t n, int32_t root_mode,
+                            float xo, float yo, int64_t counter, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, root_mode, xo, yo,
+                     counter);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_set_root(const KState* S, const float* src, const int32_t* ids, int32_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lrl::set_root_kernel, dim3((n + 255) / 256), dim3(256), 0, st, *S, src, ids, n);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_set_dof(const KState* S, const float* pos, const float* vel, const int32_t* ids, int32_t n,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lrl::set_dof_kernel, dim3((n + 255) / 256), dim3(256), 0, st, *S, pos, vel, ids, n);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_rigid_body(const KParams* K, const KState* S, const int32_t* body_leg, const int32_t* body_link,
+                                 const float* foot_xyz, hipStream_t st) {
+  hipLaunchKernelGGL(lrl::rigid_body_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, K, *S, body_leg, body_link,
+                     foot_xyz);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_shift_history(const KState* S, int NO, int H, hipStream_t st) {
+  hipLaunchKernelGGL(lrl::shift_history_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, *S, NO, H);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_randomize(const KState* S, const float* fr, const float* rr, const float* pr, const float* cr,
+                                uint32_t which, hipStream_t st) {
+  hipLaunchKernelGGL(lrl::randomize_kernel, dim3((S->stride + 255) / 256), dim3(256), 0, st, *S, fr[0], fr[1], rr[0],
+                     rr[1], pr[0], pr[1], cr[0], cr[1], which);
+  return hipGetLastError();
+}
+}

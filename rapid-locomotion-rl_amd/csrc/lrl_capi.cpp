@@ -1,0 +1,349 @@
+// lrl_capi.cpp — the extern "C" boundary of liblrl.so (include/lrl.h): sim object lifetime, the
+// SoA HBM arena, tensor descriptors (acquire_*_tensor) and the launch entry points.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "lrl_kparams.h"
+
+static thread_local char g_err[512];
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+#define HIPCHECK(x)                                                                     \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) return fail(LRL_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" {
+hipError_t lrl_launch_env_step(const KParams*, const KState*, int, const float*, uint32_t, int64_t, hipStream_t);
+hipError_t lrl_env_kernel_setup(int lds_bytes);
+hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, int64_t,
+                            hipStream_t);
+hipError_t lrl_launch_set_root(const KState*, const float*, const int32_t*, int32_t, hipStream_t);
+hipError_t lrl_launch_set_dof(const KState*, const float*, const float*, const int32_t*, int32_t, hipStream_t);
+hipError_t lrl_launch_rigid_body(const KParams*, const KState*, const int32_t*, const int32_t*, const float*,
+                                 hipStream_t);
+hipError_t lrl_launch_shift_history(const KState*, int, int, hipStream_t);
+hipError_t lrl_launch_randomize(const KState*, const float*, const float*, const float*, const float*, uint32_t,
+                                hipStream_t);
+}
+
+struct lrl_sim {
+  int device = 0;
+  KParams hk;
+  KParams* dk = nullptr;
+  KState S;
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  int lds_bytes = 0;
+  int64_t step_counter = 0;
+  int64_t reset_counter = 0;
+  lrl_tensor t[LRL_T_NUM];
+  int32_t* d_body_leg = nullptr;
+  int32_t* d_body_link = nullptr;
+  float* d_foot_xyz = nullptr;
+};
+
+static void quat_to_rowmajor(const float* q, float* R) {
+  float x = q[0], y = q[1], z = q[2], w = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
+  R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+  R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
+  memset(k, 0, sizeof(*k));
+  k->p = *p;
+  if (m->num_bodies < 5 || m->num_bodies > LRL_MAX_BODIES) return fail(LRL_E_INVALID, "num_bodies %d", m->num_bodies);
+  if (m->num_spheres < 0 || m->num_spheres > LRL_MAX_SPHERES) return fail(LRL_E_INVALID, "num_spheres %d", m->num_spheres);
+  if (p->num_obs <= 0 || p->num_obs > LRL_MAX_OBS) return fail(LRL_E_INVALID, "num_obs %d", p->num_obs);
+  if (p->decimation < 1 || p->sim_dt <= 0.f) return fail(LRL_E_INVALID, "bad timing");
+  if (p->num_reward_terms < 0 || p->num_reward_terms > LRL_MAX_REWARD_TERMS) return fail(LRL_E_INVALID, "reward terms");
+  for (int t = 0; t < p->num_reward_terms; ++t)
+    if (p->reward_term[t] < 0 || p->reward_term[t] >= LRL_R_NUM_TERMS) return fail(LRL_E_INVALID, "reward term id");
+  int obs_expected = 3 + (p->observe_command ? 3 : 0) + 36 + (p->observe_vel ? 6 : 0);
+  if (obs_expected != p->num_obs) return fail(LRL_E_INVALID, "obs layout %d != num_obs %d", obs_expected, p->num_obs);
+  for (int l = 0; l < 4; ++l)
+    for (int j = 0; j < 3; ++j) {
+      KLeg& L = k->leg[l];
+      for (int c = 0; c < 3; ++c) {
+        L.xyz[j][c] = m->joint_xyz[l][j][c];
+        L.axis[j][c] = m->joint_axis[l][j][c];
+        L.com[j][c] = m->link_com[l][j][c];
+      }
+      quat_to_rowmajor(m->joint_quat[l][j], L.rfix[j]);
+      L.mass[j] = m->link_mass[l][j];
+      for (int c = 0; c < 6; ++c) L.inertia[j][c] = m->link_inertia[l][j][c];
+    }
+  k->base_mass = m->base_mass;
+  for (int c = 0; c < 6; ++c) k->base_inertia[c] = m->base_inertia[c];
+  k->num_bodies = m->num_bodies;
+  k->num_spheres = m->num_spheres;
+  // spheres must be grouped: base first, then legs in order, bodies contiguous
+  int prev_key = -1;
+  for (int b = 0; b < LRL_MAX_BODIES; ++b) { k->body_sph_begin[b] = 0; k->body_sph_end[b] = 0; k->body_foot[b] = -1; }
+  for (int l = 0; l < 4; ++l) { k->leg_sph_begin[l] = k->leg_sph_end[l] = 0; }
+  k->base_sph_end = 0;
+  for (int s = 0; s < m->num_spheres; ++s) {
+    int b = m->sphere_body[s];
+    if (b < 0 || b >= m->num_bodies) return fail(LRL_E_INVALID, "sphere body");
+    int leg = m->body_leg[b], link = m->body_link[b];
+    int key = (leg + 1) * 64 + b;
+    if (key < prev_key) return fail(LRL_E_INVALID, "spheres not grouped by leg/body");
+    if (key != prev_key) k->body_sph_begin[b] = s;
+    k->body_sph_end[b] = s + 1;
+    prev_key = key;
+    for (int c = 0; c < 3; ++c) k->sph_pos[s][c] = m->sphere_pos[s][c];
+    k->sph_rad[s] = m->sphere_radius[s];
+    k->sph_link[s] = leg < 0 ? -1 : (link > 2 ? 2 : link);
+    if (leg < 0) k->base_sph_end = s + 1;
+  }
+  for (int l = 0; l < 4; ++l) {
+    int b0 = -1, e0 = -1;
+    for (int s = 0; s < m->num_spheres; ++s)
+      if (m->body_leg[m->sphere_body[s]] == l) {
+        if (b0 < 0) b0 = s;
+        e0 = s + 1;
+      }
+    if (b0 < 0) b0 = e0 = k->base_sph_end;
+    k->leg_sph_begin[l] = b0;
+    k->leg_sph_end[l] = e0;
+  }
+  for (int f = 0; f < p->num_feet; ++f) {
+    int b = p->feet[f];
+    if (b < 0 || b >= m->num_bodies) return fail(LRL_E_INVALID, "foot index");
+    k->body_foot[b] = f;
+  }
+  k->num_history = p->num_history;
+  k->n_es = p->num_sum_keys + 1;
+  k->n_cs = p->num_sum_keys + 5;
+  return 0;
+}
+
+static void set_t(lrl_tensor* t, void* data, int dtype, int ndim, const int64_t* shape, const int64_t* strides) {
+  t->data = data;
+  t->dtype = dtype;
+  t->ndim = ndim;
+  for (int i = 0; i < 4; ++i) { t->shape[i] = i < ndim ? shape[i] : 1; t->strides[i] = i < ndim ? strides[i] : 0; }
+}
+
+extern "C" {
+
+int32_t lrl_abi_version(void) { return LRL_ABI_VERSION; }
+const char* lrl_last_error(void) { return g_err; }
+int32_t lrl_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int32_t num_envs,
+                       int64_t global_env_offset, uint64_t seed, int32_t device, lrl_sim** out) {
+  if (!model || !params || !out || num_envs <= 0) return fail(LRL_E_INVALID, "bad arguments");
+  int ndev = lrl_device_count();
+  if (ndev <= 0) return fail(LRL_E_NOGPU, "no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(LRL_E_INVALID, "device %d of %d", device, ndev);
+  lrl_sim* s = new lrl_sim();
+  s->device = device;
+  int rc = digest(model, params, &s->hk);
+  if (rc) { delete s; return rc; }
+  HIPCHECK(hipSetDevice(device));
+  const int n = num_envs, N = (n + 63) / 64 * 64;
+  const int B = model->num_bodies, NO = params->num_obs, H = params->num_history * NO;
+  const int nes = s->hk.n_es, ncs = s->hk.n_cs;
+  KState& S = s->S;
+  memset(&S, 0, sizeof(S));
+  S.n = n;
+  S.stride = N;
+  S.env_offset = global_env_offset;
+  S.seed = seed;
+  // arena layout (floats unless noted), every field 256-B aligned
+  struct F { void** p; size_t bytes; };
+  std::vector<F> fields;
+  auto addf = [&](float** p, size_t cnt) { fields.push_back({(void**)p, cnt * 4}); };
+  addf(&S.root, 13ull * N); addf(&S.dof_pos, 12ull * N); addf(&S.dof_vel, 12ull * N);
+  addf(&S.contact, 3ull * B * N); addf(&S.rb_state, 13ull * B * N); addf(&S.torques, 12ull * N);
+  addf(&S.actions, 12ull * N); addf(&S.last_actions, 12ull * N); addf(&S.last_dof_vel, 12ull * N);
+  addf(&S.last_root_vel, 6ull * N); addf(&S.commands, 4ull * N); addf(&S.obs, (size_t)N * NO);
+  addf(&S.priv, (size_t)N * LRL_NUM_PRIV); addf(&S.hist, (size_t)N * H); addf(&S.rew, N);
+  fields.push_back({(void**)&S.reset, (size_t)N}); fields.push_back({(void**)&S.time_out, (size_t)N});
+  fields.push_back({(void**)&S.last_contacts, 4ull * N}); fields.push_back({(void**)&S.episode_length, 4ull * N});
+  addf(&S.episode_sums, (size_t)nes * N); addf(&S.command_sums, (size_t)ncs * N); addf(&S.feet_air_time, 4ull * N);
+  addf(&S.friction, N); addf(&S.restitution, N); addf(&S.payload, N); addf(&S.com, 3ull * N);
+  addf(&S.motor_strength, 12ull * N); addf(&S.kp, 12ull * N); addf(&S.kd, 12ull * N); addf(&S.env_origins, 3ull * N);
+  addf(&S.base_lin_vel, 3ull * N); addf(&S.base_ang_vel, 3ull * N); addf(&S.projected_gravity, 3ull * N);
+  addf(&S.joint_pos_target, 12ull * N);
+  size_t total = 0;
+  for (auto& f : fields) total += (f.bytes + 255) / 256 * 256;
+  void* arena = nullptr;
+  if (hipMalloc(&arena, total) != hipSuccess) { delete s; return fail(LRL_E_NOMEM, "hipMalloc %zu bytes", total); }
+  s->arena = arena;
+  s->arena_bytes = total;
+  size_t off = 0;
+  for (auto& f : fields) { *f.p = (char*)arena + off; off += (f.bytes + 255) / 256 * 256; }
+  HIPCHECK(hipMemset(arena, 0, total));
+  // initial values: identity quaternion, unit DR factors, default friction 1
+  std::vector<float> ones(N, 1.f);
+  HIPCHECK(hipMemcpy(S.root + 6ull * N, ones.data(), N * 4, hipMemcpyHostToDevice));
+  for (int j = 0; j < 12; ++j) {
+    HIPCHECK(hipMemcpy(S.motor_strength + (size_t)j * N, ones.data(), N * 4, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(S.kp + (size_t)j * N, ones.data(), N * 4, hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(S.kd + (size_t)j * N, ones.data(), N * 4, hipMemcpyHostToDevice));
+  }
+  HIPCHECK(hipMemcpy(S.friction, ones.data(), N * 4, hipMemcpyHostToDevice));
+  HIPCHECK(hipMalloc(&s->dk, sizeof(KParams)));
+  HIPCHECK(hipMemcpy(s->dk, &s->hk, sizeof(KParams), hipMemcpyHostToDevice));
+  HIPCHECK(hipMalloc(&s->d_body_leg, sizeof(int32_t) * LRL_MAX_BODIES));
+  HIPCHECK(hipMalloc(&s->d_body_link, sizeof(int32_t) * LRL_MAX_BODIES));
+  HIPCHECK(hipMalloc(&s->d_foot_xyz, sizeof(float) * 12));
+  HIPCHECK(hipMemcpy(s->d_body_leg, model->body_leg, sizeof(int32_t) * LRL_MAX_BODIES, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(s->d_body_link, model->body_link, sizeof(int32_t) * LRL_MAX_BODIES, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(s->d_foot_xyz, model->foot_xyz, sizeof(float) * 12, hipMemcpyHostToDevice));
+  int lds_contacts = (4 * 45 + model->num_spheres * 13) * 64 * 4;  // leg blocks + contact rows
+  int lds_tiles = (NO + LRL_NUM_PRIV) * 64 * 4;
+  s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
+  if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);
+  HIPCHECK(lrl_env_kernel_setup(s->lds_bytes));
+  // tensor descriptors: [n, k] views over SoA [k][N] -> strides (1, N)
+  const int64_t sN = N;
+  auto soa2 = [&](int id, void* d, int k, int dt) {
+    int64_t sh[2] = {n, k}, st[2] = {1, sN};
+    set_t(&s->t[id], d, dt, 2, sh, st);
+  };
+  auto soa1 = [&](int id, void* d, int dt) {
+    int64_t sh[1] = {n}, st[1] = {1};
+    set_t(&s->t[id], d, dt, 1, sh, st);
+  };
+  soa2(LRL_T_ROOT_STATE, S.root, 13, LRL_F32);
+  soa2(LRL_T_DOF_POS, S.dof_pos, 12, LRL_F32);
+  soa2(LRL_T_DOF_VEL, S.dof_vel, 12, LRL_F32);
+  { int64_t sh[3] = {n, B, 3}, st[3] = {1, 3 * sN, sN}; set_t(&s->t[LRL_T_CONTACT_FORCE], S.contact, LRL_F32, 3, sh, st); }
+  { int64_t sh[3] = {n, B, 13}, st[3] = {1, 13 * sN, sN}; set_t(&s->t[LRL_T_RIGID_BODY_STATE], S.rb_state, LRL_F32, 3, sh, st); }
+  soa2(LRL_T_TORQUES, S.torques, 12, LRL_F32);
+  soa2(LRL_T_ACTIONS, S.actions, 12, LRL_F32);
+  soa2(LRL_T_LAST_ACTIONS, S.last_actions, 12, LRL_F32);
+  soa2(LRL_T_LAST_DOF_VEL, S.last_dof_vel, 12, LRL_F32);
+  soa2(LRL_T_LAST_ROOT_VEL, S.last_root_vel, 6, LRL_F32);
+  soa2(LRL_T_COMMANDS, S.commands, 4, LRL_F32);
+  { int64_t sh[2] = {n, NO}, st[2] = {NO, 1}; set_t(&s->t[LRL_T_OBS], S.obs, LRL_F32, 2, sh, st); }
+  { int64_t sh[2] = {n, LRL_NUM_PRIV}, st[2] = {LRL_NUM_PRIV, 1}; set_t(&s->t[LRL_T_PRIV_OBS], S.priv, LRL_F32, 2, sh, st); }
+  { int64_t sh[2] = {n, H}, st[2] = {H, 1}; set_t(&s->t[LRL_T_OBS_HISTORY], S.hist, LRL_F32, 2, sh, st); }
+  soa1(LRL_T_REWARD, S.rew, LRL_F32);
+  soa1(LRL_T_RESET, S.reset, LRL_U8);
+  soa1(LRL_T_TIME_OUT, S.time_out, LRL_U8);
+  soa1(LRL_T_EPISODE_LENGTH, S.episode_length, LRL_I32);
+  { int64_t sh[2] = {nes, n}, st[2] = {sN, 1}; set_t(&s->t[LRL_T_EPISODE_SUMS], S.episode_sums, LRL_F32, 2, sh, st); }
+  { int64_t sh[2] = {ncs, n}, st[2] = {sN, 1}; set_t(&s->t[LRL_T_COMMAND_SUMS], S.command_sums, LRL_F32, 2, sh, st); }
+  soa2(LRL_T_FEET_AIR_TIME, S.feet_air_time, 4, LRL_F32);
+  soa2(LRL_T_LAST_CONTACTS, S.last_contacts, 4, LRL_U8);
+  soa1(LRL_T_FRICTION, S.friction, LRL_F32);
+  soa1(LRL_T_RESTITUTION, S.restitution, LRL_F32);
+  soa1(LRL_T_PAYLOAD, S.payload, LRL_F32);
+  soa2(LRL_T_COM_DISPLACEMENT, S.com, 3, LRL_F32);
+  soa2(LRL_T_MOTOR_STRENGTH, S.motor_strength, 12, LRL_F32);
+  soa2(LRL_T_KP_FACTOR, S.kp, 12, LRL_F32);
+  soa2(LRL_T_KD_FACTOR, S.kd, 12, LRL_F32);
+  soa2(LRL_T_ENV_ORIGINS, S.env_origins, 3, LRL_F32);
+  soa2(LRL_T_BASE_LIN_VEL, S.base_lin_vel, 3, LRL_F32);
+  soa2(LRL_T_BASE_ANG_VEL, S.base_ang_vel, 3, LRL_F32);
+  soa2(LRL_T_PROJECTED_GRAVITY, S.projected_gravity, 3, LRL_F32);
+  soa2(LRL_T_JOINT_POS_TARGET, S.joint_pos_target, 12, LRL_F32);
+  *out = s;
+  return 0;
+}
+
+int32_t lrl_sim_destroy(lrl_sim* s) {
+  if (!s) return 0;
+  hipSetDevice(s->device);
+  hipFree(s->arena);
+  hipFree(s->dk);
+  hipFree(s->d_body_leg);
+  hipFree(s->d_body_link);
+  hipFree(s->d_foot_xyz);
+  delete s;
+  return 0;
+}
+
+int32_t lrl_sim_tensor(lrl_sim* s, int32_t id, lrl_tensor* out) {
+  if (!s || !out || id < 0 || id >= LRL_T_NUM) return fail(LRL_E_INVALID, "bad tensor id %d", id);
+  *out = s->t[id];
+  return 0;
+}
+
+int32_t lrl_sim_inject_uniforms(lrl_sim* s, const float* noise_u, const float* dr_u) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  s->S.inj_noise = noise_u;
+  s->S.inj_dr = dr_u;
+  return 0;
+}
+
+int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* stream) {
+  if (!s || !actions) return fail(LRL_E_INVALID, "null argument");
+  if ((flags & LRL_STEP_INJECT_UNIFORM) && (!s->S.inj_noise || !s->S.inj_dr))
+    return fail(LRL_E_INVALID, "injected uniforms not set");
+  s->step_counter += 1;  // common_step_counter (legged_robot.py:153)
+  HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_set_step_counter(lrl_sim* s, int64_t c) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  s->step_counter = c;
+  return 0;
+}
+
+int32_t lrl_sim_reset_idx(lrl_sim* s, const int32_t* ids, int32_t n, void* stream) {
+  return lrl_sim_reset_idx_ex(s, ids, n, 1, 0.f, 0.f, stream);
+}
+
+int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t root_mode, float xo, float yo,
+                             void* stream) {
+  if (!s || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  s->reset_counter += 1;
+  HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, root_mode, xo, yo, s->reset_counter, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_set_root_state_indexed(lrl_sim* s, const float* root, const int32_t* ids, int32_t n, void* stream) {
+  if (!s || !root || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  HIPCHECK(lrl_launch_set_root(&s->S, root, ids, n, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_set_dof_state_indexed(lrl_sim* s, const float* pos, const float* vel, const int32_t* ids, int32_t n,
+                                      void* stream) {
+  if (!s || !pos || !vel || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  HIPCHECK(lrl_launch_set_dof(&s->S, pos, vel, ids, n, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_refresh_rigid_body_state(lrl_sim* s, void* stream) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  HIPCHECK(lrl_launch_rigid_body(s->dk, &s->S, s->d_body_leg, s->d_body_link, s->d_foot_xyz, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_shift_history(lrl_sim* s, void* stream) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  HIPCHECK(lrl_launch_shift_history(&s->S, s->hk.p.num_obs, s->hk.p.num_history * s->hk.p.num_obs,
+                                    (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_randomize(lrl_sim* s, const float* fr, const float* rr, const float* pr, const float* cr,
+                          uint32_t which, void* stream) {
+  if (!s || !fr || !rr || !pr || !cr) return fail(LRL_E_INVALID, "null argument");
+  HIPCHECK(lrl_launch_randomize(&s->S, fr, rr, pr, cr, which, (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

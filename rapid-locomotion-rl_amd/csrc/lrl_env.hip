@@ -1,0 +1,980 @@
+// lrl_env.hip — fused LeggedRobot.step for gfx950 (CDNA4).
+//
+// One env per lane, 64 envs per single-wave workgroup.  A launch performs the whole policy step
+// (legged_robot.py:106-137): action clip, `decimation` x {PD torques (:653-688) + one physics
+// sub-step}, post_physics_step (:139-188) with teleport (:768-791), DR redraw (:544-560, :591-593),
+// termination (:190-202), rewards (:314-340, :1506-1646), observations + noise (:342-417), the
+// obs/priv clip (:133-136) and the HistoryWrapper shift (history_wrapper.py:23).
+//
+// State lives in HBM as struct-of-arrays [field][N] (coalesced: lane i touches word i of each
+// field).  Physics (own model; PhysX is closed and unavailable — DESIGN.md §physics):
+//   * joint-space dynamics of the 18-DOF floating quadruped in the BASE frame: per-leg composite
+//     inertias and 3x3 leg blocks D_l, K_l = D_l^-1 B_l^T, the 6x6 base Schur complement
+//     S = A - sum B_l K_l (Cholesky in registers), RNEA bias with gravity as base acceleration;
+//   * contacts of collision spheres with the ground plane: speculative/Baumgarte velocity targets,
+//     restitution above the bounce threshold, Coulomb cone, projected Gauss-Seidel on 3x3 Delassus
+//     blocks computed through the Schur complement;  per-sphere solver rows are staged in LDS as
+//     [sphere][field][lane] tiles (bank-conflict free, each lane owns one column);
+//   * semi-implicit Euler, quaternion exponential map for the base.
+// Post-physics arithmetic runs with FP contraction OFF so it follows torch's op order (the
+// reference's elementwise kernels do not fuse multiply-adds).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/lrl_philox.h"
+#include "lrl_kparams.h"
+
+#define WAVE 64
+#define NSF 13  // LDS fields per contact sphere
+
+namespace lrl {
+
+struct V3 {
+  float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+struct M3 {
+  float m[9];
+};
+__device__ __forceinline__ V3 mul(const M3& R, V3 v) {
+  return v3(R.m[0] * v.x + R.m[1] * v.y + R.m[2] * v.z, R.m[3] * v.x + R.m[4] * v.y + R.m[5] * v.z,
+            R.m[6] * v.x + R.m[7] * v.y + R.m[8] * v.z);
+}
+__device__ __forceinline__ V3 mulT(const M3& R, V3 v) {
+  return v3(R.m[0] * v.x + R.m[3] * v.y + R.m[6] * v.z, R.m[1] * v.x + R.m[4] * v.y + R.m[7] * v.z,
+            R.m[2] * v.x + R.m[5] * v.y + R.m[8] * v.z);
+}
+__device__ __forceinline__ M3 mul(const M3& A, const M3& B) {
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C.m[3 * i + j] = A.m[3 * i] * B.m[j] + A.m[3 * i + 1] * B.m[3 + j] + A.m[3 * i + 2] * B.m[6 + j];
+  return C;
+}
+__device__ __forceinline__ M3 quat_mat(float x, float y, float z, float w) {
+  M3 R;
+  R.m[0] = 1.f - 2.f * (y * y + z * z); R.m[1] = 2.f * (x * y - z * w); R.m[2] = 2.f * (x * z + y * w);
+  R.m[3] = 2.f * (x * y + z * w); R.m[4] = 1.f - 2.f * (x * x + z * z); R.m[5] = 2.f * (y * z - x * w);
+  R.m[6] = 2.f * (x * z - y * w); R.m[7] = 2.f * (y * z + x * w); R.m[8] = 1.f - 2.f * (x * x + y * y);
+  return R;
+}
+__device__ __forceinline__ M3 axis_rot(V3 a, float th) {
+  float s, c;
+  sincosf(th, &s, &c);
+  float t = 1.f - c;
+  M3 R;
+  R.m[0] = t * a.x * a.x + c; R.m[1] = t * a.x * a.y - s * a.z; R.m[2] = t * a.x * a.z + s * a.y;
+  R.m[3] = t * a.x * a.y + s * a.z; R.m[4] = t * a.y * a.y + c; R.m[5] = t * a.y * a.z - s * a.x;
+  R.m[6] = t * a.x * a.z - s * a.y; R.m[7] = t * a.y * a.z + s * a.x; R.m[8] = t * a.z * a.z + c;
+  return R;
+}
+
+// spatial inertia about the base origin, base coordinates: mass, h = m*c, I_O (xx yy zz xy xz yz)
+struct SI {
+  float m;
+  V3 h;
+  float i[6];
+};
+struct SV {
+  V3 a, l;  // angular; linear
+};
+__device__ __forceinline__ SV operator+(SV p, SV q) { return SV{p.a + q.a, p.l + q.l}; }
+__device__ __forceinline__ SV scale(SV p, float s) { return SV{s * p.a, s * p.l}; }
+__device__ __forceinline__ float sdot(SV p, SV q) { return dot(p.a, q.a) + dot(p.l, q.l); }
+__device__ __forceinline__ V3 symmul(const float* I, V3 v) {
+  return v3(I[0] * v.x + I[3] * v.y + I[4] * v.z, I[3] * v.x + I[1] * v.y + I[5] * v.z,
+            I[4] * v.x + I[5] * v.y + I[2] * v.z);
+}
+__device__ __forceinline__ SV simul(const SI& I, SV v) {  // f = (I_O w + h x v, m v - h x w)
+  return SV{symmul(I.i, v.a) + cross(I.h, v.l), I.m * v.l - cross(I.h, v.a)};
+}
+__device__ __forceinline__ SI siadd(const SI& p, const SI& q) {
+  SI r;
+  r.m = p.m + q.m;
+  r.h = p.h + q.h;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) r.i[k] = p.i[k] + q.i[k];
+  return r;
+}
+__device__ __forceinline__ SI make_si(float m, V3 c, const M3& R, const float* Ib) {
+  // Ic = R Ib R^T (Ib symmetric about COM in body frame), then shift to the base origin
+  float Ibm[9] = {Ib[0], Ib[3], Ib[4], Ib[3], Ib[1], Ib[5], Ib[4], Ib[5], Ib[2]};
+  float T[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) T[3 * r + k] = R.m[3 * r] * Ibm[k] + R.m[3 * r + 1] * Ibm[3 + k] + R.m[3 * r + 2] * Ibm[6 + k];
+  float Ic[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Ic[3 * r + k] = T[3 * r] * R.m[3 * k] + T[3 * r + 1] * R.m[3 * k + 1] + T[3 * r + 2] * R.m[3 * k + 2];
+  SI s;
+  s.m = m;
+  s.h = m * c;
+  float cc = dot(c, c);
+  s.i[0] = Ic[0] + m * (cc - c.x * c.x);
+  s.i[1] = Ic[4] + m * (cc - c.y * c.y);
+  s.i[2] = Ic[8] + m * (cc - c.z * c.z);
+  s.i[3] = Ic[1] - m * c.x * c.y;
+  s.i[4] = Ic[2] - m * c.x * c.z;
+  s.i[5] = Ic[5] - m * c.y * c.z;
+  return s;
+}
+__device__ __forceinline__ SV crm(SV v, SV m) { return SV{cross(v.a, m.a), cross(v.a, m.l) + cross(v.l, m.a)}; }
+__device__ __forceinline__ SV crf(SV v, SV f) { return SV{cross(v.a, f.a) + cross(v.l, f.l), cross(v.a, f.l)}; }
+__device__ __forceinline__ float sv_get(const SV& s, int r) {
+  return r == 0 ? s.a.x : r == 1 ? s.a.y : r == 2 ? s.a.z : r == 3 ? s.l.x : r == 4 ? s.l.y : s.l.z;
+}
+
+// Per-leg solver blocks live in LDS as [leg][field][lane] columns (each lane owns one column, so
+// the accesses are bank-conflict free).  Field map inside a leg (LEGF floats):
+//   0..8  joint axes a_j (base frame)   9..17 joint origins o_j   18..35 K = D^-1 B^T (3x6)
+//   36..41 D^-1 (00 11 22 01 02 12)   42..44 per-joint bias / solve scratch
+#define LEGF 45  // + 42..44: joint bias C_l, then y_l = D^-1 (tau - C)_l
+#define LI(r, c) ((r) * ((r) + 1) / 2 + (c))
+
+struct Lds {
+  float* base;     // leg blocks, then contact rows
+  int sph_off;     // field offset of the contact rows
+  __device__ __forceinline__ float& leg(int l, int f) const { return base[(l * LEGF + f) * WAVE + threadIdx.x]; }
+  __device__ __forceinline__ float& sph(int s, int f) const {
+    return base[(sph_off + s * NSF + f) * WAVE + threadIdx.x];
+  }
+  __device__ __forceinline__ V3 a(int l, int j) const { return v3(leg(l, 3 * j), leg(l, 3 * j + 1), leg(l, 3 * j + 2)); }
+  __device__ __forceinline__ V3 o(int l, int j) const {
+    return v3(leg(l, 9 + 3 * j), leg(l, 9 + 3 * j + 1), leg(l, 9 + 3 * j + 2));
+  }
+  __device__ __forceinline__ float Kx(int l, int j, int r) const { return leg(l, 18 + 6 * j + r); }
+  __device__ __forceinline__ float Di(int l, int k) const { return leg(l, 36 + k); }
+};
+
+// uniform-index read of a 12-entry register array without dynamic register indexing
+__device__ __forceinline__ float pick12(const float* a, int i) {
+  float v = a[0];
+#pragma unroll
+  for (int k = 1; k < 12; ++k) v = (i == k) ? a[k] : v;
+  return v;
+}
+
+__device__ __forceinline__ void chol6(float* L) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float s = L[LI(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= L[LI(j, k)] * L[LI(j, k)];
+    float d = sqrtf(fmaxf(s, 1e-12f));
+    L[LI(j, j)] = d;
+    float inv = 1.f / d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      float t = L[LI(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= L[LI(i, k)] * L[LI(j, k)];
+      L[LI(i, j)] = t * inv;
+    }
+  }
+}
+__device__ __forceinline__ void fwd6(const float* L, float* b) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= L[LI(i, k)] * b[k];
+    b[i] = s / L[LI(i, i)];
+  }
+}
+__device__ __forceinline__ void bwd6(const float* L, float* b) {
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float s = b[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= L[LI(k, i)] * b[k];
+    b[i] = s / L[LI(i, i)];
+  }
+}
+__device__ __forceinline__ V3 sym3mul(float d0, float d1, float d2, float d3, float d4, float d5, V3 v) {
+  return v3(d0 * v.x + d3 * v.y + d4 * v.z, d3 * v.x + d1 * v.y + d5 * v.z, d4 * v.x + d5 * v.y + d2 * v.z);
+}
+__device__ __forceinline__ V3 di_mul(const Lds& M, int l, V3 v) {
+  return sym3mul(M.Di(l, 0), M.Di(l, 1), M.Di(l, 2), M.Di(l, 3), M.Di(l, 4), M.Di(l, 5), v);
+}
+__device__ __forceinline__ void sym3inv(const float* D, float* Di) {
+  float a = D[0], b = D[3], c = D[4], d = D[1], e = D[5], f = D[2];
+  float c00 = d * f - e * e, c01 = c * e - b * f, c02 = b * e - c * d;
+  float det = a * c00 + b * c01 + c * c02;
+  float id = 1.f / det;
+  Di[0] = c00 * id;
+  Di[3] = c01 * id;
+  Di[4] = c02 * id;
+  Di[1] = (a * f - c * c) * id;
+  Di[5] = (b * c - a * e) * id;
+  Di[2] = (a * d - b * b) * id;
+}
+
+// M^-1 applied to a generalized impulse that is nonzero in the base part pb and in leg `lsel` (pl):
+//   x_b = S^-1 (pb - K_L^T pl),  x_l = -K_l x_b (+ D_L^-1 pl for l == L).  Accumulates into nu.
+__device__ __forceinline__ void apply_minv_add(const Lds& M, const float* Lc, float* pb, int lsel, V3 pl, float* nu) {
+  if (lsel >= 0) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) pb[r] -= M.Kx(lsel, 0, r) * pl.x + M.Kx(lsel, 1, r) * pl.y + M.Kx(lsel, 2, r) * pl.z;
+  }
+  fwd6(Lc, pb);
+  bwd6(Lc, pb);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) nu[r] += pb[r];
+  V3 y = lsel >= 0 ? di_mul(M, lsel, pl) : v3(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float kx = 0.f;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) kx += M.Kx(l, j, r) * pb[r];
+      float yj = (l == lsel) ? (j == 0 ? y.x : j == 1 ? y.y : y.z) : 0.f;
+      nu[6 + 3 * l + j] += yj - kx;
+    }
+  }
+}
+
+// point velocity (base frame) of body point x on leg lsel / link (lsel < 0: base)
+__device__ __forceinline__ V3 point_vel(const Lds& M, const float* nu, V3 x, int lsel, int link) {
+  V3 u = cross(v3(nu[0], nu[1], nu[2]), x) + v3(nu[3], nu[4], nu[5]);
+  if (lsel >= 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float qd = 0.f;
+#pragma unroll
+      for (int l = 0; l < 4; ++l)
+        if (l == lsel) qd = nu[6 + 3 * l + j];
+      if (j <= link) u = u + qd * cross(M.a(lsel, j), x - M.o(lsel, j));
+    }
+  }
+  return u;
+}
+
+// One contact sphere's 3x3 Delassus block W = G S^-1 G^T + J_l D^-1 J_l^T (n, t1, t2 rows)
+__device__ __forceinline__ void contact_setup(const Lds& M, const float* Lc, const M3& R, int s, int lsel, int link) {
+  V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
+  V3 c[3] = {v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f)};
+  if (lsel >= 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j <= link) c[j] = cross(M.a(lsel, j), x - M.o(lsel, j));
+  }
+  float z[3][6];
+  V3 h[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    V3 nd = d == 0 ? v3(R.m[6], R.m[7], R.m[8]) : d == 1 ? v3(R.m[0], R.m[1], R.m[2]) : v3(R.m[3], R.m[4], R.m[5]);
+    V3 xn = cross(x, nd);
+    float g[6] = {xn.x, xn.y, xn.z, nd.x, nd.y, nd.z};
+    h[d] = v3(dot(c[0], nd), dot(c[1], nd), dot(c[2], nd));
+    if (lsel >= 0) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+        g[r] -= M.Kx(lsel, 0, r) * h[d].x + M.Kx(lsel, 1, r) * h[d].y + M.Kx(lsel, 2, r) * h[d].z;
+    }
+    fwd6(Lc, g);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) z[d][r] = g[r];
+  }
+  float W[3][3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+#pragma unroll
+    for (int e = d; e < 3; ++e) {
+      float w = 0.f;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) w += z[d][r] * z[e][r];
+      if (lsel >= 0) w += dot(h[d], di_mul(M, lsel, h[e]));
+      W[d][e] = w;
+      W[e][d] = w;
+    }
+  float id = 1.f / (W[1][1] * W[2][2] - W[1][2] * W[2][1]);
+  M.sph(s, 3) = W[0][0];
+  M.sph(s, 4) = W[1][0];
+  M.sph(s, 5) = W[2][0];
+  M.sph(s, 6) = W[2][2] * id;  // (W_tt)^-1: 11, 12, 22
+  M.sph(s, 7) = -W[1][2] * id;
+  M.sph(s, 8) = W[1][1] * id;
+  M.sph(s, 10) = 0.f;
+  M.sph(s, 11) = 0.f;
+  M.sph(s, 12) = 0.f;
+}
+
+// One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone)
+__device__ __forceinline__ void contact_pgs(const Lds& M, const float* Lc, const M3& R, int s, int lsel, int link,
+                                            float mu, float* nu) {
+  V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
+  V3 uw = mul(R, point_vel(M, nu, x, lsel, link));  // world: (t1, t2, n) = (x, y, z)
+  float Wnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
+  float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
+  float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
+  float ln = fmaxf(ln0 - (uw.z - b) / Wnn, 0.f);
+  float dn = ln - ln0;
+  float ut1 = uw.x + Wt1n * dn, ut2 = uw.y + Wt2n * dn;
+  float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
+  float lim = mu * ln, nt = sqrtf(lt1 * lt1 + lt2 * lt2);
+  if (nt > lim) {
+    float sc = nt > 0.f ? lim / nt : 0.f;
+    lt1 *= sc;
+    lt2 *= sc;
+  }
+  M.sph(s, 10) = ln;
+  M.sph(s, 11) = lt1;
+  M.sph(s, 12) = lt2;
+  V3 fb = mulT(R, v3(lt1 - lt10, lt2 - lt20, dn));
+  V3 tq = cross(x, fb);
+  float pb[6] = {tq.x, tq.y, tq.z, fb.x, fb.y, fb.z};
+  V3 pl = v3(0.f, 0.f, 0.f);
+  if (lsel >= 0) {
+    float cj[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j <= link) cj[j] = dot(cross(M.a(lsel, j), x - M.o(lsel, j)), fb);
+    pl = v3(cj[0], cj[1], cj[2]);
+  }
+  apply_minv_add(M, Lc, pb, lsel, pl, nu);
+}
+
+struct Body {  // per-lane env state during the step
+  float pos[3], quat[4], V[3], W[3];
+  float q[12], qd[12];
+};
+
+__device__ __forceinline__ int sphere_leg(const KParams* __restrict__ K, int s) {
+  int l = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (s >= K->leg_sph_begin[k] && s < K->leg_sph_end[k]) l = k;
+  return l;
+}
+
+// ------------------------------------------------------------------------------------------------
+// One physics sub-step.  Contact impulses of the sub-step stay in the LDS rows (fields 10..12).
+// ------------------------------------------------------------------------------------------------
+__device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau, float mb, const float* Ib, V3 cb,
+                        float mu, float rest, const Lds& M, uint64_t& active) {
+  const lrl_env_params& P = K->p;
+  const float dt = P.sim_dt;
+  const M3 R = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
+  const V3 wb = mulT(R, v3(st.W[0], st.W[1], st.W[2]));
+  const V3 vb = mulT(R, v3(st.V[0], st.V[1], st.V[2])) - cross(wb, cb);
+  float nu[18];
+  nu[0] = wb.x; nu[1] = wb.y; nu[2] = wb.z; nu[3] = vb.x; nu[4] = vb.y; nu[5] = vb.z;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) nu[6 + j] = st.qd[j];
+  const V3 gb = mulT(R, v3(P.gravity[0], P.gravity[1], P.gravity[2]));
+  const SV v0 = SV{wb, vb};
+  const SV a0 = SV{v3(0.f, 0.f, 0.f), v3(-gb.x, -gb.y, -gb.z)};
+  const V3 Rz = v3(R.m[6], R.m[7], R.m[8]);  // world z in base coordinates
+  const float pz = st.pos[2];
+
+  SI A;
+  {
+    M3 E;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) E.m[k] = (k % 4 == 0) ? 1.f : 0.f;
+    A = make_si(mb, cb, E, Ib);
+  }
+  SV Cb = simul(A, a0) + crf(v0, simul(A, v0));
+  float Sch[21];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) Sch[k] = 0.f;
+  active = 0;
+
+  // contact detection helper: separation, restitution/speculative target (needs nu at sub-step start)
+  auto detect = [&](int s, V3 x, int lsel, int link) {
+    float sep = pz + dot(Rz, x) - K->sph_rad[s];
+    if (sep < P.contact_offset) {
+      active |= (1ull << s);
+      M.sph(s, 0) = x.x;
+      M.sph(s, 1) = x.y;
+      M.sph(s, 2) = x.z;
+      float u0 = dot(Rz, point_vel(M, nu, x, lsel, link));
+      float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+      if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
+      M.sph(s, 9) = tgt;
+    }
+  };
+  for (int s = 0; s < K->base_sph_end; ++s) detect(s, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2]), -1, 0);
+
+#pragma unroll 1
+  for (int l = 0; l < 4; ++l) {
+    const KLeg& kl = K->leg[l];
+    M3 Rp;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Rp.m[k] = (k % 4 == 0) ? 1.f : 0.f;
+    V3 op = v3(0.f, 0.f, 0.f);
+    SI Ij[3];
+    SV S[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      M3 Rf;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) Rf.m[k] = kl.rfix[j][k];
+      const V3 ax = v3(kl.axis[j][0], kl.axis[j][1], kl.axis[j][2]);
+      const M3 Rj = mul(mul(Rp, Rf), axis_rot(ax, pick12(st.q, 3 * l + j)));
+      const V3 o = op + mul(Rp, v3(kl.xyz[j][0], kl.xyz[j][1], kl.xyz[j][2]));
+      const V3 a = mul(Rj, ax);
+      M.leg(l, 3 * j) = a.x; M.leg(l, 3 * j + 1) = a.y; M.leg(l, 3 * j + 2) = a.z;
+      M.leg(l, 9 + 3 * j) = o.x; M.leg(l, 9 + 3 * j + 1) = o.y; M.leg(l, 9 + 3 * j + 2) = o.z;
+      S[j] = SV{a, cross(o, a)};
+      const V3 c = o + mul(Rj, v3(kl.com[j][0], kl.com[j][1], kl.com[j][2]));
+      Ij[j] = make_si(kl.mass[j], c, Rj, kl.inertia[j]);
+      // contact detection for this link's spheres (needs only a_j', o_j' for j' <= j, already in LDS)
+      for (int s = K->leg_sph_begin[l]; s < K->leg_sph_end[l]; ++s)
+        if (K->sph_link[s] == j) detect(s, o + mul(Rj, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2])), l, j);
+      Rp = Rj;
+      op = o;
+    }
+    const SI Ic2 = Ij[2], Ic1 = siadd(Ij[1], Ic2), Ic0 = siadd(Ij[0], Ic1);
+    A = siadd(A, Ic0);
+    const SV F0 = simul(Ic0, S[0]), F1 = simul(Ic1, S[1]), F2 = simul(Ic2, S[2]);
+    float D[6] = {sdot(S[0], F0), sdot(S[1], F1), sdot(S[2], F2), sdot(S[0], F1), sdot(S[0], F2), sdot(S[1], F2)};
+    float Di[6];
+    sym3inv(D, Di);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) M.leg(l, 36 + k) = Di[k];
+    float Kl[3][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      float b0 = sv_get(F0, r), b1 = sv_get(F1, r), b2 = sv_get(F2, r);
+      Kl[0][r] = Di[0] * b0 + Di[3] * b1 + Di[4] * b2;
+      Kl[1][r] = Di[3] * b0 + Di[1] * b1 + Di[5] * b2;
+      Kl[2][r] = Di[4] * b0 + Di[5] * b1 + Di[2] * b2;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) M.leg(l, 18 + 6 * j + r) = Kl[j][r];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = 0; c <= r; ++c)
+        Sch[LI(r, c)] -= sv_get(F0, r) * Kl[0][c] + sv_get(F1, r) * Kl[1][c] + sv_get(F2, r) * Kl[2][c];
+    // RNEA (qdd = 0): velocity-product and gravity forces
+    SV vj = v0, aj = a0, f[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const SV sq = scale(S[j], pick12(st.qd, 3 * l + j));
+      vj = vj + sq;
+      aj = aj + crm(vj, sq);
+      f[j] = simul(Ij[j], aj) + crf(vj, simul(Ij[j], vj));
+    }
+    const SV Fc2 = f[2], Fc1 = f[1] + Fc2, Fc0 = f[0] + Fc1;
+    M.leg(l, 42) = sdot(S[0], Fc0);
+    M.leg(l, 43) = sdot(S[1], Fc1);
+    M.leg(l, 44) = sdot(S[2], Fc2);
+    Cb = Cb + Fc0;
+  }
+  // base block A (6x6) + Schur complement, Cholesky in registers
+  Sch[LI(0, 0)] += A.i[0]; Sch[LI(1, 1)] += A.i[1]; Sch[LI(2, 2)] += A.i[2];
+  Sch[LI(1, 0)] += A.i[3]; Sch[LI(2, 0)] += A.i[4]; Sch[LI(2, 1)] += A.i[5];
+  Sch[LI(3, 1)] += A.h.z;  Sch[LI(3, 2)] -= A.h.y;
+  Sch[LI(4, 0)] -= A.h.z;  Sch[LI(4, 2)] += A.h.x;
+  Sch[LI(5, 0)] += A.h.y;  Sch[LI(5, 1)] -= A.h.x;
+  Sch[LI(3, 3)] += A.m; Sch[LI(4, 4)] += A.m; Sch[LI(5, 5)] += A.m;
+  chol6(Sch);
+  // free acceleration: M acc = [0; tau] - C
+  {
+    float pb[6] = {-Cb.a.x, -Cb.a.y, -Cb.a.z, -Cb.l.x, -Cb.l.y, -Cb.l.z};
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const V3 rl = v3(tau[3 * l] - M.leg(l, 42), tau[3 * l + 1] - M.leg(l, 43), tau[3 * l + 2] - M.leg(l, 44));
+#pragma unroll
+      for (int r = 0; r < 6; ++r) pb[r] -= M.Kx(l, 0, r) * rl.x + M.Kx(l, 1, r) * rl.y + M.Kx(l, 2, r) * rl.z;
+      const V3 y = di_mul(M, l, rl);
+      M.leg(l, 42) = y.x;  // reuse as y_l
+      M.leg(l, 43) = y.y;
+      M.leg(l, 44) = y.z;
+    }
+    fwd6(Sch, pb);
+    bwd6(Sch, pb);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) nu[r] += dt * pb[r];
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        float kx = 0.f;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) kx += M.Kx(l, j, r) * pb[r];
+        nu[6 + 3 * l + j] += dt * (M.leg(l, 42 + j) - kx);
+      }
+  }
+  // contact rows and projected Gauss-Seidel; spheres visited in model order (base, legs 0..3) and
+  // only when active in some lane of the wave
+  for (int s = 0; s < K->num_spheres; ++s)
+    if (__any((int)((active >> s) & 1ull)))
+      if ((active >> s) & 1ull) contact_setup(M, Sch, R, s, sphere_leg(K, s), K->sph_link[s]);
+  for (int it = 0; it < P.solver_iterations; ++it)
+    for (int s = 0; s < K->num_spheres; ++s)
+      if (__any((int)((active >> s) & 1ull)))
+        if ((active >> s) & 1ull) contact_pgs(M, Sch, R, s, sphere_leg(K, s), K->sph_link[s], mu, nu);
+  // semi-implicit integration
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    st.qd[j] = nu[6 + j];
+    st.q[j] += dt * st.qd[j];
+  }
+  const V3 vw = mul(R, v3(nu[3], nu[4], nu[5]));
+  st.pos[0] += dt * vw.x;
+  st.pos[1] += dt * vw.y;
+  st.pos[2] += dt * vw.z;
+  const V3 w = v3(nu[0], nu[1], nu[2]);
+  const float wn = sqrtf(dot(w, w)), th = wn * dt;
+  float dq[4];
+  if (th > 1e-12f) {
+    float sn, cs;
+    sincosf(0.5f * th, &sn, &cs);
+    const float k = sn / wn;
+    dq[0] = w.x * k; dq[1] = w.y * k; dq[2] = w.z * k; dq[3] = cs;
+  } else {
+    dq[0] = 0.5f * dt * w.x; dq[1] = 0.5f * dt * w.y; dq[2] = 0.5f * dt * w.z; dq[3] = 1.f;
+  }
+  const float x1 = st.quat[0], y1 = st.quat[1], z1 = st.quat[2], w1 = st.quat[3];
+  float nq[4] = {w1 * dq[0] + x1 * dq[3] + y1 * dq[2] - z1 * dq[1], w1 * dq[1] - x1 * dq[2] + y1 * dq[3] + z1 * dq[0],
+                 w1 * dq[2] + x1 * dq[1] - y1 * dq[0] + z1 * dq[3], w1 * dq[3] - x1 * dq[0] - y1 * dq[1] - z1 * dq[2]};
+  const float inv = 1.f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st.quat[k] = nq[k] * inv;
+  const M3 R2 = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
+  const V3 V = mul(R2, v3(nu[3], nu[4], nu[5]) + cross(w, cb)), Wv = mul(R2, w);
+  st.V[0] = V.x; st.V[1] = V.y; st.V[2] = V.z;
+  st.W[0] = Wv.x; st.W[1] = Wv.y; st.W[2] = Wv.z;
+}
+
+// ------------------------------------------------------------------------------------------------
+// post-physics helpers: torch op order, no contraction
+// ------------------------------------------------------------------------------------------------
+#pragma clang fp contract(off)
+__device__ __forceinline__ float pos_target(const lrl_env_params& P, const float* act, int j) {
+  float as = act[j] * P.action_scale;
+  if (j % 3 == 0) as = as * P.hip_scale_reduction;  // hip columns 0,3,6,9 (legged_robot.py:666)
+  return as + P.default_dof_pos[j];
+}
+// kpf/kdf/ms point at this env's column of the SoA [12][N] factor arrays
+__device__ __forceinline__ void compute_torques(const lrl_env_params& P, const float* act, const float* q,
+                                                const float* qd, const float* kpf, const float* kdf, const float* ms,
+                                                int N, float* tau) {
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    float t0 = pos_target(P, act, j);
+    float t = P.p_gains[j] * kpf[j * N] * (t0 - q[j]) - P.d_gains[j] * kdf[j * N] * qd[j];
+    t = t * ms[j * N];
+    float lim = P.torque_limits[j];
+    tau[j] = fminf(fmaxf(t, -lim), lim);
+  }
+}
+__device__ __forceinline__ V3 quat_rotate_inverse(const float* q, V3 v) {
+  float w = q[3];
+  float s = 2.0f * (w * w) - 1.0f;
+  V3 a = v3(v.x * s, v.y * s, v.z * s);
+  V3 c = v3(q[1] * v.z - q[2] * v.y, q[2] * v.x - q[0] * v.z, q[0] * v.y - q[1] * v.x);
+  V3 b = v3(c.x * w * 2.0f, c.y * w * 2.0f, c.z * w * 2.0f);
+  float d = q[0] * v.x + q[1] * v.y + q[2] * v.z;
+  V3 e = v3(q[0] * d * 2.0f, q[1] * d * 2.0f, q[2] * d * 2.0f);
+  return v3(a.x - b.x + e.x, a.y - b.y + e.y, a.z - b.z + e.z);
+}
+__device__ __forceinline__ float sq(float x) { return x * x; }
+__device__ __forceinline__ float nrm3(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
+
+// ------------------------------------------------------------------------------------------------
+// the fused step kernel
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
+                                                        const float* __restrict__ actions_in, uint32_t flags,
+                                                        int64_t step_counter) {
+  extern __shared__ float lds[];
+  const lrl_env_params& P = K->p;
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * WAVE + lane;
+  const int N = S.stride;
+  const bool valid = e < S.n;
+  const uint64_t genv = (uint64_t)(S.env_offset + e);
+
+  Body st;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    st.pos[k] = S.root[k * N + e];
+    st.V[k] = S.root[(7 + k) * N + e];
+    st.W[k] = S.root[(10 + k) * N + e];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st.quat[k] = S.root[(3 + k) * N + e];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    st.q[j] = S.dof_pos[j * N + e];
+    st.qd[j] = S.dof_vel[j * N + e];
+  }
+  float act[12], tau[12];
+  {
+    const float c = P.clip_actions;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      float a = valid ? actions_in[(size_t)e * 12 + j] : 0.f;
+      act[j] = fminf(fmaxf(a, -c), c);
+    }
+  }
+  const Lds M{lds, 4 * LEGF};  // leg blocks first, then the contact rows
+  const float payload = S.payload[e];
+  const V3 cb = v3(S.com[e], S.com[N + e], S.com[2 * N + e]);
+  const float mb = K->base_mass + payload;
+  float Ib[6];
+  {
+    float sc = mb / K->base_mass;  // recomputeInertia: inertia scales with the new mass
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Ib[k] = K->base_inertia[k] * sc;
+  }
+  const float mu = 0.5f * (S.friction[e] + P.ground_friction);
+  const float rest = 0.5f * (S.restitution[e] + P.ground_restitution);
+  const bool physics = flags & LRL_STEP_PHYSICS;
+  uint64_t active = 0;
+
+  for (int sub = 0; sub < P.decimation; ++sub) {
+    compute_torques(P, act, st.q, st.qd, S.kp + e, S.kd + e, S.motor_strength + e, N, tau);
+    if (physics) substep(K, st, tau, mb, Ib, cb, mu, rest, M, active);
+  }
+
+  // ---- contact forces per body (last sub-step) and the contact-derived signals ----
+  int rst = 0;
+  float collision = 0.f;
+  float ff[4][3];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) ff[f][0] = ff[f][1] = ff[f][2] = 0.f;
+  const float inv_dt = 1.f / P.sim_dt;
+  for (int b = 0; b < K->num_bodies; ++b) {
+    float fx = 0.f, fy = 0.f, fz = 0.f;
+    if (physics) {
+      for (int s = K->body_sph_begin[b]; s < K->body_sph_end[b]; ++s)
+        if ((active >> s) & 1ull) {
+          fx += M.sph(s, 11);
+          fy += M.sph(s, 12);
+          fz += M.sph(s, 10);
+        }
+      fx *= inv_dt;
+      fy *= inv_dt;
+      fz *= inv_dt;
+      S.contact[(3 * b) * N + e] = fx;
+      S.contact[(3 * b + 1) * N + e] = fy;
+      S.contact[(3 * b + 2) * N + e] = fz;
+    } else {
+      fx = S.contact[(3 * b) * N + e];
+      fy = S.contact[(3 * b + 1) * N + e];
+      fz = S.contact[(3 * b + 2) * N + e];
+    }
+    float n = nrm3(fx, fy, fz);
+    if ((P.termination_mask >> b) & 1u) rst |= n > 1.0f;
+    if ((P.penalised_mask >> b) & 1u) collision += n > 0.1f ? 1.f : 0.f;
+    int fs = K->body_foot[b];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      if (fs == f) { ff[f][0] = fx; ff[f][1] = fy; ff[f][2] = fz; }
+  }
+  __syncthreads();  // LDS contact rows are dead from here on; the obs tile reuses them
+
+  // ---- post_physics_step ----
+  int32_t eplen = S.episode_length[e] + 1;
+  const float* quat = st.quat;
+  V3 blv = quat_rotate_inverse(quat, v3(st.V[0], st.V[1], st.V[2]));
+  V3 bav = quat_rotate_inverse(quat, v3(st.W[0], st.W[1], st.W[2]));
+  V3 pg = quat_rotate_inverse(quat, v3(0.f, 0.f, -1.f));
+  if (P.teleport) {
+    float th = P.teleport_thresh, xo = (float)(int)P.teleport_x_offset;
+    if (st.pos[0] < th + xo) st.pos[0] += P.terrain_length * (float)(P.terrain_rows - 1);
+    if (st.pos[0] > P.terrain_length * (float)P.terrain_rows - th + xo) st.pos[0] -= P.terrain_length * (float)(P.terrain_rows - 1);
+    if (st.pos[1] < th) st.pos[1] += P.terrain_width * (float)(P.terrain_cols - 1);
+    if (st.pos[1] > P.terrain_width * (float)P.terrain_cols - th) st.pos[1] -= P.terrain_width * (float)(P.terrain_cols - 1);
+  }
+  const bool inject = flags & LRL_STEP_INJECT_UNIFORM;
+  float ms_e[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ms_e[j] = S.motor_strength[j * N + e];
+  if (P.rand_interval > 0 && eplen % P.rand_interval == 0) {
+    int k = 0;
+    lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter, (LRL_RNG_DR << 16) ^ (uint32_t)(step_counter >> 32), 0,
+                             S.seed);
+    if (P.randomize_motor_strength) {
+      float u = inject ? S.inj_dr[e] : lrl_u01(r.v[k]);
+      k++;
+      float v = u * (P.motor_strength_range[1] - P.motor_strength_range[0]) + P.motor_strength_range[0];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        ms_e[j] = v;
+        S.motor_strength[j * N + e] = v;
+      }
+    }
+    if (P.randomize_kp) {
+      float u = lrl_u01(r.v[k++]);
+      float v = u * (P.kp_range[1] - P.kp_range[0]) + P.kp_range[0];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) S.kp[j * N + e] = v;
+    }
+    if (P.randomize_kd) {
+      float u = lrl_u01(r.v[k++]);
+      float v = u * (P.kd_range[1] - P.kd_range[0]) + P.kd_range[0];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
+    }
+  }
+  if (P.use_terminal_body_height && st.pos[2] < P.terminal_body_height) rst = 1;
+
+  // rewards
+  float cmd[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cmd[k] = S.commands[k * N + e];
+  float la[12], lqd[12], fat[4];
+  uint8_t lc[4];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    la[j] = S.last_actions[j * N + e];
+    lqd[j] = S.last_dof_vel[j * N + e];
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    fat[f] = S.feet_air_time[f * N + e];
+    lc[f] = S.last_contacts[f * N + e];
+  }
+  float rew = 0.f;
+  for (int t = 0; t < P.num_reward_terms; ++t) {
+    float r = 0.f;
+    switch (P.reward_term[t]) {
+      case LRL_R_LIN_VEL_Z: r = sq(blv.z); break;
+      case LRL_R_ANG_VEL_XY: r = sq(bav.x) + sq(bav.y); break;
+      case LRL_R_ORIENTATION: r = sq(pg.x) + sq(pg.y); break;
+      case LRL_R_BASE_HEIGHT: r = sq(st.pos[2] - P.base_height_target); break;
+      case LRL_R_TORQUES:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += sq(tau[j]);
+        break;
+      case LRL_R_ENERGY:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += tau[j] * st.qd[j];
+        break;
+      case LRL_R_ENERGY_EXPENDITURE:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += fmaxf(tau[j] * st.qd[j], 0.f);
+        break;
+      case LRL_R_DOF_VEL:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += sq(st.qd[j]);
+        break;
+      case LRL_R_DOF_ACC:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += sq((lqd[j] - st.qd[j]) / P.dt);
+        break;
+      case LRL_R_ACTION_RATE:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += sq(la[j] - act[j]);
+        break;
+      case LRL_R_COLLISION: r = collision; break;
+      case LRL_R_SURVIVAL: r = rst ? 0.f : 1.f; break;
+      case LRL_R_DOF_POS_LIMITS:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+          float o = -fminf(st.q[j] - P.soft_dof_pos_lower[j], 0.f);
+          o += fmaxf(st.q[j] - P.soft_dof_pos_upper[j], 0.f);
+          r += o;
+        }
+        break;
+      case LRL_R_DOF_VEL_LIMITS:
+#pragma unroll
+        for (int j = 0; j < 12; ++j)
+          r += fminf(fmaxf(fabsf(st.qd[j]) - P.dof_vel_limits[j] * P.soft_dof_vel_limit, 0.f), 1.f);
+        break;
+      case LRL_R_TORQUE_LIMITS:
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += fmaxf(fabsf(tau[j]) - P.torque_limits[j] * P.soft_torque_limit, 0.f);
+        break;
+      case LRL_R_TRACKING_LIN_VEL: {
+        float err = sq(cmd[0] - blv.x) + sq(cmd[1] - blv.y);
+        r = expf(-err / P.tracking_sigma);
+      } break;
+      case LRL_R_TRACKING_ANG_VEL: r = expf(-sq(cmd[2] - bav.z) / P.tracking_sigma_yaw); break;
+      case LRL_R_FEET_AIR_TIME: {
+        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          int c = ff[f][2] > 1.0f;
+          int filt = c || lc[f];
+          lc[f] = (uint8_t)c;
+          float first = (fat[f] > 0.f && filt) ? 1.f : 0.f;
+          fat[f] = fat[f] + P.dt;
+          r += (fat[f] - 0.5f) * first;
+          if (filt) fat[f] = 0.f;
+        }
+        r = r * (cn > 0.1f ? 1.f : 0.f);
+      } break;
+      case LRL_R_STUMBLE:
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          if (sqrtf(ff[f][0] * ff[f][0] + ff[f][1] * ff[f][1]) > 5.f * fabsf(ff[f][2])) r = 1.f;
+        break;
+      case LRL_R_STAND_STILL: {
+        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+#pragma unroll
+        for (int j = 0; j < 12; ++j) r += fabsf(st.q[j] - P.default_dof_pos[j]);
+        r = r * (cn < 0.1f ? 1.f : 0.f);
+      } break;
+      case LRL_R_FEET_CONTACT_FORCES:
+#pragma unroll
+        for (int f = 0; f < 4; ++f) r += fmaxf(nrm3(ff[f][0], ff[f][1], ff[f][2]) - P.max_contact_force, 0.f);
+        break;
+      default: break;
+    }
+    r = r * P.reward_scale[t];
+    rew += r;
+    const int slot = P.reward_slot[t];
+    S.episode_sums[slot * N + e] += r;
+    S.command_sums[slot * N + e] += r;
+  }
+  if (P.only_positive_rewards) rew = fmaxf(rew, 0.f);
+  const int KS = P.num_sum_keys;
+  S.episode_sums[KS * N + e] += rew;
+  if (P.termination_scale != 0.f) {
+    float r = (rst ? 1.f : 0.f) * P.termination_scale;
+    rew += r;
+    S.episode_sums[P.termination_slot * N + e] += r;
+    S.command_sums[P.termination_slot * N + e] += r;
+  }
+  S.command_sums[(KS + 0) * N + e] += blv.x;
+  S.command_sums[(KS + 1) * N + e] += bav.z;
+  S.command_sums[(KS + 2) * N + e] += sq(blv.x - cmd[0]);
+  S.command_sums[(KS + 3) * N + e] += sq(bav.z - cmd[2]);
+  S.command_sums[(KS + 4) * N + e] += 1.f;
+
+  // observations -> LDS tile [lane][NO]
+  const int NO = P.num_obs;
+  float* otile = lds;                  // [64][NO]
+  float* ptile = lds + WAVE * NO;      // [64][18]
+  {
+    float* ob = otile + lane * NO;
+    int o = 0;
+    if (P.observe_vel) {
+      ob[o++] = blv.x * P.obs_scale_lin_vel; ob[o++] = blv.y * P.obs_scale_lin_vel; ob[o++] = blv.z * P.obs_scale_lin_vel;
+      ob[o++] = bav.x * P.obs_scale_ang_vel; ob[o++] = bav.y * P.obs_scale_ang_vel; ob[o++] = bav.z * P.obs_scale_ang_vel;
+    }
+    ob[o++] = pg.x; ob[o++] = pg.y; ob[o++] = pg.z;
+    if (P.observe_command) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ob[o++] = cmd[k] * P.commands_scale[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) ob[o + j] = (st.q[j] - P.default_dof_pos[j]) * P.obs_scale_dof_pos;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) ob[o + 12 + j] = st.qd[j] * P.obs_scale_dof_vel;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) ob[o + 24 + j] = act[j];
+    if (P.add_noise) {
+      for (int i0 = 0; i0 < NO; i0 += 4) {
+        lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter,
+                                 (LRL_RNG_OBS_NOISE << 16) ^ (uint32_t)(step_counter >> 32), (uint32_t)(i0 >> 2), S.seed);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int i = i0 + k;
+          if (i < NO) {
+            float u = inject ? S.inj_noise[(size_t)e * NO + i] : lrl_u01(r.v[k]);
+            ob[i] += (2.f * u - 1.f) * P.noise_vec[i];
+          }
+        }
+      }
+    }
+    for (int i = 0; i < NO; ++i) ob[i] = fminf(fmaxf(ob[i], -P.clip_obs), P.clip_obs);
+    float* pr = ptile + lane * LRL_NUM_PRIV;
+    pr[0] = (S.friction[e] - P.priv_shift[0]) * P.priv_scale[0];
+    pr[1] = (S.restitution[e] - P.priv_shift[1]) * P.priv_scale[1];
+    pr[2] = (payload - P.priv_shift[2]) * P.priv_scale[2];
+    pr[3] = (cb.x - P.priv_shift[3]) * P.priv_scale[3];
+    pr[4] = (cb.y - P.priv_shift[3]) * P.priv_scale[3];
+    pr[5] = (cb.z - P.priv_shift[3]) * P.priv_scale[3];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) pr[6 + j] = (ms_e[j] - P.priv_shift[4]) * P.priv_scale[4];
+#pragma unroll
+    for (int i = 0; i < LRL_NUM_PRIV; ++i) pr[i] = fminf(fmaxf(pr[i], -P.clip_obs), P.clip_obs);
+  }
+
+  // ---- write back the SoA state ----
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    S.root[k * N + e] = st.pos[k];
+    S.root[(7 + k) * N + e] = st.V[k];
+    S.root[(10 + k) * N + e] = st.W[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) S.root[(3 + k) * N + e] = st.quat[k];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    S.dof_pos[j * N + e] = st.q[j];
+    S.dof_vel[j * N + e] = st.qd[j];
+    S.torques[j * N + e] = tau[j];
+    S.joint_pos_target[j * N + e] = pos_target(P, act, j);
+    S.actions[j * N + e] = act[j];
+    S.last_actions[j * N + e] = act[j];
+    S.last_dof_vel[j * N + e] = st.qd[j];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    S.last_root_vel[k * N + e] = st.V[k];
+    S.last_root_vel[(3 + k) * N + e] = st.W[k];
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    S.feet_air_time[f * N + e] = fat[f];
+    S.last_contacts[f * N + e] = lc[f];
+  }
+  S.base_lin_vel[e] = blv.x; S.base_lin_vel[N + e] = blv.y; S.base_lin_vel[2 * N + e] = blv.z;
+  S.base_ang_vel[e] = bav.x; S.base_ang_vel[N + e] = bav.y; S.base_ang_vel[2 * N + e] = bav.z;
+  S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
+  S.episode_length[e] = eplen;
+  S.reset[e] = (uint8_t)rst;
+  S.rew[e] = rew;
+
+  // ---- AoS tiles (obs, priv) and the history shift: coalesced over the wave's contiguous rows ----
+  __syncthreads();
+  const size_t row0 = (size_t)blockIdx.x * WAVE;
+  {
+    float* og = S.obs + row0 * NO;
+    for (int i = lane; i < WAVE * NO; i += WAVE) og[i] = otile[i];
+    float* pgp = S.priv + row0 * LRL_NUM_PRIV;
+    for (int i = lane; i < WAVE * LRL_NUM_PRIV; i += WAVE) pgp[i] = ptile[i];
+  }
+  if (flags & LRL_STEP_HISTORY) {
+    const int H = K->num_history * NO;
+    float* hg = S.hist + row0 * H;
+    // in place: new[r][k] = old[r][k + NO] (k < H - NO) else obs[r][k - (H - NO)].  Reads run ahead of
+    // writes within a row, and each wave-iteration reads only addresses above the ones it writes.
+    const int total = WAVE * H;
+    for (int i0 = 0; i0 < total; i0 += WAVE) {
+      int i = i0 + lane;
+      int r = i / H, k = i - r * H;
+      float v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
+      __builtin_amdgcn_wave_barrier();
+      hg[i] = v;
+    }
+  }
+}
+
+}  // namespace lrl
+
+extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
+  return hipFuncSetAttribute((const void*)lrl::env_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+}
+
+extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int lds_bytes, const float* actions,
+                                          uint32_t flags, int64_t step_counter, hipStream_t stream) {
+  int blocks = S->stride / WAVE;
+  hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
+                     step_counter);
+  return hipGetLastError();
+}

@@ -1,0 +1,47 @@
+// Device-side parameter block of one sim: lrl_env_params + the model tables pre-digested for the
+// quadruped kernel (per-leg joint frames, contact spheres grouped by leg and body).  Uploaded once
+// by lrl_sim_create; every kernel reads it through a __restrict__ const pointer, so the compiler
+// turns the (wave-uniform) accesses into scalar loads.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/lrl.h"
+
+struct KLeg {
+  float xyz[3][3];   // joint origin in the parent frame
+  float rfix[3][9];  // fixed joint-origin rotation (row-major)
+  float axis[3][3];  // joint axis (child frame)
+  float mass[3], com[3][3], inertia[3][6];  // calf includes the fixed foot
+};
+
+struct KParams {
+  lrl_env_params p;
+  KLeg leg[LRL_NUM_LEGS];
+  float base_mass, base_inertia[6];
+  int32_t num_bodies, num_spheres;
+  // spheres sorted by body (model order: base, then leg 0..3)
+  float sph_pos[LRL_MAX_SPHERES][3];
+  float sph_rad[LRL_MAX_SPHERES];
+  int32_t sph_link[LRL_MAX_SPHERES];  // 0..2 dynamic link inside the leg, -1 base
+  int32_t base_sph_end;               // spheres [0, base_sph_end) are on the base
+  int32_t leg_sph_begin[LRL_NUM_LEGS], leg_sph_end[LRL_NUM_LEGS];
+  int32_t body_sph_begin[LRL_MAX_BODIES], body_sph_end[LRL_MAX_BODIES];
+  int32_t body_foot[LRL_MAX_BODIES];  // foot slot 0..3 or -1
+  int32_t num_history;
+  int32_t n_es, n_cs;                 // rows of episode_sums / command_sums
+};
+
+// SoA device buffers of a sim (each [.][N] with N = padded env count unless noted).
+struct KState {
+  int32_t n;       // real env count
+  int32_t stride;  // padded N (multiple of 64)
+  int64_t env_offset;
+  uint64_t seed;
+  float *root, *dof_pos, *dof_vel, *contact, *rb_state, *torques, *actions, *last_actions, *last_dof_vel,
+      *last_root_vel, *commands, *obs, *priv, *hist, *rew;
+  uint8_t *reset, *time_out, *last_contacts;
+  int32_t* episode_length;
+  float *episode_sums, *command_sums, *feet_air_time, *friction, *restitution, *payload, *com, *motor_strength,
+      *kp, *kd, *env_origins, *base_lin_vel, *base_ang_vel, *projected_gravity, *joint_pos_target;
+  const float *inj_noise, *inj_dr;
+};

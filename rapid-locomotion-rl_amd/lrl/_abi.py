@@ -117,7 +117,8 @@ def lib():
         for name in ["lrl_sim_create", "lrl_sim_destroy", "lrl_sim_tensor", "lrl_sim_step", "lrl_sim_reset_idx",
                      "lrl_sim_set_root_state_indexed", "lrl_sim_set_dof_state_indexed", "lrl_sim_inject_uniforms",
                      "lrl_sim_refresh_rigid_body_state", "lrl_sim_shift_history", "lrl_sim_randomize", "lrl_gae",
-                     "lrl_policy_act", "lrl_abi_version", "lrl_device_count"]:
+                     "lrl_policy_act", "lrl_abi_version", "lrl_device_count", "lrl_gae_partial", "lrl_adv_normalize",
+                     "lrl_sim_reset_idx_ex", "lrl_sim_set_step_counter"]:
             getattr(L, name).restype = C.c_int32
         _lib = L
     return _lib

@@ -1,0 +1,443 @@
+"""Legged-robot vector env over liblrl.so — the reference's env surface, MI355X underneath.
+
+``LeggedRobotEnv`` mirrors ``LeggedRobot`` (mini_gym/envs/base/legged_robot.py) plus the
+``VelocityTrackingEasyEnv`` 4-tuple ``step`` (mini_gym/envs/mini_cheetah/velocity_tracking/
+velocity_tracking_easy_env.py:42-69): the same constructor arguments, attribute names and
+buffers (``root_states``, ``dof_pos``, ``commands``, ``episode_sums``, ``extras`` ...), with every
+per-env computation of ``step`` fused into one HIP launch (``lrl_sim_step``).  The torch tensors
+exposed here are zero-copy views of the sim's struct-of-arrays HBM buffers, so writes such as
+``env.commands[:, 0] = 1.0`` act on the simulation directly (the reference needs a
+``set_*_tensor`` call for that; here those calls exist but the data is already in place).
+
+Semantics follow the fork by default (no automatic resets inside ``step``,
+commands only written by callers).  Host-side bookkeeping that the reference also does on the
+host — the command curriculum (numpy MT19937) and the per-reset episode logging — stays in Python.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _abi, _dlpack
+from . import params as lparams
+from .config import Section
+from .curriculum import RewardThresholdCurriculum
+from .robot import load_robot
+
+MINI_GYM_ROOT_DIR = "/root/reference"  # only used to format Cfg.asset.file; tables ship in lrl/robots
+
+
+class _LazyExtras(dict):
+    """``extras`` dict whose per-step numpy copies (velocity_tracking_easy_env.py:48-62) are only
+    materialised when a caller reads them — the reference pays 11 device->host syncs per step."""
+
+    def __init__(self, env):
+        super().__init__()
+        self._env = env
+        self._lazy = {}
+
+    def set_lazy(self, key, fn):
+        self._lazy[key] = fn
+        dict.pop(self, key, None)
+
+    def __getitem__(self, key):
+        if key in self._lazy and not dict.__contains__(self, key):
+            return self._lazy[key]()
+        return dict.__getitem__(self, key)
+
+    def __contains__(self, key):
+        return dict.__contains__(self, key) or key in self._lazy
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def keys(self):
+        return list(dict.keys(self)) + [k for k in self._lazy if not dict.__contains__(self, k)]
+
+
+class LeggedRobotEnv:
+    def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
+                 eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=0,
+                 solver_iterations=None):
+        if cfg is None:
+            from .config import Cfg as cfg
+        if num_envs is not None:
+            cfg.env.num_envs = num_envs
+        if prone:  # velocity_tracking_easy_env.py:16-19
+            cfg.init_state.rot = [0.0, 1.0, 0.0, 0.0]
+            cfg.init_state.pos = [0.0, 0.0, 0.15]
+            cfg.asset.fix_base_link = True
+        if deploy:
+            cfg.noise.add_noise = False
+            cfg.domain_rand.push_robots = False
+            cfg.domain_rand.randomize_friction = False
+            cfg.env.episode_length_s = 100
+        if eval_cfg is not None:
+            raise NotImplementedError("train/eval env split is a next-row item (SURVEY.md §8(f) rank 2)")
+        self.cfg, self.eval_cfg = cfg, eval_cfg
+        self.device = torch.device(sim_device)
+        if self.device.type != "cuda" or not torch.cuda.is_available():
+            raise RuntimeError("LeggedRobotEnv runs on the GPU through liblrl.so; no CPU path exists")
+        self.headless = True
+        self.num_train_envs = self.num_envs = cfg.env.num_envs
+        self.num_eval_envs = 0
+        self.num_obs = cfg.env.num_observations
+        self.num_privileged_obs = cfg.env.num_privileged_obs
+        self.num_actions = cfg.env.num_actions
+        self.seed = int(seed)
+
+        # ---- asset + terrain + derived params (legged_robot.py:1162-1319, 1417-1429) ----
+        asset_file = cfg.asset.file.format(MINI_GYM_ROOT_DIR=MINI_GYM_ROOT_DIR)
+        self.robot = load_robot(asset_file)
+        self.num_bodies = self.robot["num_bodies"]
+        self.num_dof = self.num_dofs = 12
+        self.dof_names = self.robot["dof_names"]
+        self.body_names = self.robot["body_names"]
+        self.custom_origins = cfg.terrain.mesh_type in ("heightfield", "trimesh")
+        if self.custom_origins:
+            self._flat_terrain()
+        self._P = lparams.build_params(cfg, self.robot, solver_iterations=solver_iterations)
+        self._M = lparams.build_model(self.robot)
+        self.sim_params = Section(dt=lparams.sim_dt(cfg))
+        self.dt = cfg.control.decimation * self.sim_params.dt
+        self.max_episode_length = cfg.env.max_episode_length
+        self.obs_scales = cfg.normalization.obs_scales
+        self.reward_scales = {k: v for k, v in lparams.reward_layout(cfg)[1].items()}
+        self.reward_names = [k for k in self.reward_scales if k != "termination"]
+        feet, pen, term = lparams.body_sets(cfg, self.robot)
+        self.feet_indices = torch.tensor(feet, dtype=torch.long, device=self.device)
+        self.penalised_contact_indices = torch.tensor(pen, dtype=torch.long, device=self.device)
+        self.termination_contact_indices = torch.tensor(term, dtype=torch.long, device=self.device)
+
+        # ---- sim ----
+        L = _abi.lib()
+        self._L = L
+        self._sim = C.c_void_p()
+        torch.cuda.set_device(self.device)
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        _abi.check(L.lrl_sim_create(C.byref(self._M), C.byref(self._P), C.c_int32(self.num_envs),
+                                    C.c_int64(env_offset), C.c_uint64(self.seed), C.c_int32(dev_index),
+                                    C.byref(self._sim)))
+        self._dev_index = dev_index
+        T = self._tensor
+        self.root_states = self.all_root_states = T(_abi.T_ROOT_STATE)
+        self.dof_pos = T(_abi.T_DOF_POS)
+        self.dof_vel = T(_abi.T_DOF_VEL)
+        self.contact_forces = T(_abi.T_CONTACT_FORCE)
+        self.rigid_body_state = T(_abi.T_RIGID_BODY_STATE)
+        self.torques = T(_abi.T_TORQUES)
+        self.actions = T(_abi.T_ACTIONS)
+        self.last_actions = T(_abi.T_LAST_ACTIONS)
+        self.last_dof_vel = T(_abi.T_LAST_DOF_VEL)
+        self.last_root_vel = T(_abi.T_LAST_ROOT_VEL)
+        self.commands = T(_abi.T_COMMANDS)
+        self.obs_buf = T(_abi.T_OBS)
+        self.privileged_obs_buf = T(_abi.T_PRIV_OBS)
+        self.obs_history_buf = T(_abi.T_OBS_HISTORY)
+        self.rew_buf = T(_abi.T_REWARD)
+        self._reset_u8 = T(_abi.T_RESET)
+        self._time_out_u8 = T(_abi.T_TIME_OUT)
+        self.episode_length_buf = T(_abi.T_EPISODE_LENGTH)
+        self._episode_sums = T(_abi.T_EPISODE_SUMS)
+        self._command_sums = T(_abi.T_COMMAND_SUMS)
+        self.feet_air_time = T(_abi.T_FEET_AIR_TIME)
+        self._last_contacts_u8 = T(_abi.T_LAST_CONTACTS)
+        self.friction_coeffs = T(_abi.T_FRICTION)
+        self.restitutions = T(_abi.T_RESTITUTION)
+        self.payloads = T(_abi.T_PAYLOAD)
+        self.com_displacements = T(_abi.T_COM_DISPLACEMENT)
+        self.motor_strengths = T(_abi.T_MOTOR_STRENGTH)
+        self.Kp_factors = T(_abi.T_KP_FACTOR)
+        self.Kd_factors = T(_abi.T_KD_FACTOR)
+        self.env_origins = T(_abi.T_ENV_ORIGINS)
+        self.base_lin_vel = T(_abi.T_BASE_LIN_VEL)
+        self.base_ang_vel = T(_abi.T_BASE_ANG_VEL)
+        self.projected_gravity = T(_abi.T_PROJECTED_GRAVITY)
+        self.joint_pos_target = T(_abi.T_JOINT_POS_TARGET)
+        self.base_quat = self.root_states[:, 3:7]
+        keys = list(self.reward_scales)
+        self.episode_sums = {k: self._episode_sums[i] for i, k in enumerate(keys + ["total"])}
+        self.command_sums = {k: self._command_sums[i] for i, k in enumerate(
+            keys + ["lin_vel_raw", "ang_vel_raw", "lin_vel_residual", "ang_vel_residual", "ep_timesteps"])}
+        self.default_dof_pos = torch.tensor(self._P.default_dof_pos[:], device=self.device).unsqueeze(0)
+        self.p_gains = torch.tensor(self._P.p_gains[:], device=self.device)
+        self.d_gains = torch.tensor(self._P.d_gains[:], device=self.device)
+        self.torque_limits = torch.tensor(self._P.torque_limits[:], device=self.device)
+        self.dof_pos_limits = torch.stack([torch.tensor(self._P.soft_dof_pos_lower[:]),
+                                           torch.tensor(self._P.soft_dof_pos_upper[:])], 1).to(self.device)
+        self.base_init_state = torch.tensor(self._P.base_init_state[:], device=self.device)
+        self.default_body_mass = self.robot["base_mass"]
+        self.measured_heights = 0
+        self.common_step_counter = 0
+        self.extras = _LazyExtras(self)
+        self.record_now = False
+        self.complete_video_frames = []
+        self.kernel_timer = None
+
+        # ---- origins, DR draws at creation (legged_robot.py:1216-1231, 1385-1415, 519-542) ----
+        self._set_env_origins()
+        self.all_root_states[:, 0:3] = self.env_origins
+        self.all_root_states[:, 3:7] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device)
+        self.all_root_states[:, 7:13] = 0.0
+        dr = cfg.domain_rand
+        which = (int(dr.randomize_base_mass) | (int(dr.randomize_com_displacement) << 1) |
+                 (int(dr.randomize_friction) << 2) | (int(dr.randomize_restitution) << 3))
+        arr = lambda r: (C.c_float * 2)(*[float(x) for x in r])
+        _abi.check(L.lrl_sim_randomize(self._sim, arr(dr.friction_range), arr(dr.restitution_range),
+                                       arr(dr.added_mass_range), arr(dr.com_displacement_range), C.c_uint32(which),
+                                       self._stream()))
+        if initial_dynamics_dict is not None:
+            for k, v in initial_dynamics_dict.items():
+                if hasattr(self, k) and isinstance(getattr(self, k), torch.Tensor):
+                    getattr(self, k).copy_(v.to(self.device).view_as(getattr(self, k)))
+        self._init_command_distribution()
+        self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
+        self._ids_all = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
+
+    # -------------------------------------------------------------------------------- plumbing
+    def _tensor(self, tid):
+        d = _abi.LrlTensor()
+        _abi.check(self._L.lrl_sim_tensor(self._sim, C.c_int32(tid), C.byref(d)))
+        return _dlpack.wrap(d, self._dev_index)
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "_sim", None):
+            torch.cuda.synchronize(self.device)
+            self._L.lrl_sim_destroy(self._sim)
+            self._sim = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def reset_buf(self):
+        return self._reset_u8.bool()
+
+    @property
+    def time_out_buf(self):
+        return self._time_out_u8.bool()
+
+    @property
+    def last_contacts(self):
+        return self._last_contacts_u8.bool()
+
+    # -------------------------------------------------------------------------------- terrain
+    def _flat_terrain(self):
+        """Terrain bookkeeping for the flat trimesh the Mini Cheetah preset uses (terrain.py:12-184 with
+        terrain_noise_magnitude 0: every sub-terrain is flat at z = 0)."""
+        t = self.cfg.terrain
+        if any(p > 0 for p in t.terrain_proportions[:8]) or t.terrain_noise_magnitude != 0:
+            raise NotImplementedError("rough terrain generation is a next-row item (SURVEY.md §8(f) rank 1)")
+        t.x_offset = 0
+        t.rows_offset = 0
+        t.env_length, t.env_width = t.terrain_length, t.terrain_width
+        origins = np.zeros((t.num_rows, t.num_cols, 3))
+        for i in range(t.num_rows):
+            for j in range(t.num_cols):
+                origins[i, j] = [(i + 0.5) * t.terrain_length, (j + 0.5) * t.terrain_width, 0.0]
+        t.env_origins = origins
+
+    def _set_env_origins(self):
+        """legged_robot.py:1385-1415"""
+        cfg, n = self.cfg, self.num_envs
+        if self.custom_origins:
+            t = cfg.terrain
+            max_l = t.num_rows - 1 if not t.curriculum else t.max_init_terrain_level
+            min_l = 0 if not t.curriculum else t.min_init_terrain_level
+            g = torch.Generator().manual_seed(self.seed)
+            self.terrain_levels = torch.randint(min_l, max_l + 1, (n,), generator=g).to(self.device)
+            self.terrain_types = torch.div(torch.arange(n), (n / t.num_cols), rounding_mode="floor").long().to(self.device)
+            t.max_terrain_level = t.num_rows
+            t.terrain_origins = torch.from_numpy(t.env_origins).to(self.device).float()
+            self.env_origins[:] = t.terrain_origins[self.terrain_levels, self.terrain_types]
+        else:
+            num_cols = np.floor(np.sqrt(n))
+            num_rows = np.ceil(n / num_cols)
+            xx, yy = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
+            sp = cfg.env.env_spacing
+            self.env_origins[:, 0] = (sp * xx.flatten()[:n]).to(self.device)
+            self.env_origins[:, 1] = (sp * yy.flatten()[:n]).to(self.device)
+            self.env_origins[:, 2] = 0.0
+
+    # -------------------------------------------------------------------------------- commands
+    def _init_command_distribution(self):
+        """legged_robot.py:1056-1072"""
+        c = self.cfg.commands
+        self.curriculum = RewardThresholdCurriculum(
+            seed=c.curriculum_seed, x_vel=(c.limit_vel_x[0], c.limit_vel_x[1], 51),
+            y_vel=(c.limit_vel_y[0], c.limit_vel_y[1], 2), yaw_vel=(c.limit_vel_yaw[0], c.limit_vel_yaw[1], 51))
+        self.env_command_bins = np.zeros(self.num_envs, dtype=int)
+        low = np.array([c.lin_vel_x[0], c.lin_vel_y[0], c.ang_vel_yaw[0]])
+        high = np.array([c.lin_vel_x[1], c.lin_vel_y[1], c.ang_vel_yaw[1]])
+        self.curriculum.set_to(low=low, high=high)
+
+    def resample_commands(self, env_ids):
+        """_resample_commands (legged_robot.py:595-626); disconnected in the fork (Q3), callable here."""
+        if len(env_ids) == 0:
+            return
+        ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
+        ids_np = ids.cpu().numpy()
+        timesteps = int(self.cfg.commands.resampling_time / self.dt)
+        ep_len = min(self.cfg.env.max_episode_length, timesteps)
+        lin = (self.command_sums["tracking_lin_vel"][ids] / ep_len).cpu().numpy()
+        ang = (self.command_sums["tracking_ang_vel"][ids] / ep_len).cpu().numpy()
+        lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
+        ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
+        old_bins = self.env_command_bins[ids_np]
+        self.curriculum.update(old_bins, lin, ang, lin_thr, ang_thr, local_range=0.5)
+        new_cmds, new_bins = self.curriculum.sample(batch_size=len(ids_np))
+        self.env_command_bins[ids_np] = new_bins
+        self.commands[ids, :3] = torch.tensor(new_cmds, dtype=torch.float, device=self.device)
+        self.commands[ids, :2] *= (torch.norm(self.commands[ids, :2], dim=1) > 0.2).unsqueeze(1)
+        self._command_sums[:, ids] = 0.0
+
+    # -------------------------------------------------------------------------------- API
+    def step(self, actions, _history=False):
+        """VelocityTrackingEasyEnv.step: returns (obs, rew, done, extras)."""
+        if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous():
+            actions = actions.to(self.device, torch.float32).contiguous()
+        if actions.shape != (self.num_envs, self.num_actions):
+            raise ValueError(f"actions must be [{self.num_envs}, {self.num_actions}], got {tuple(actions.shape)}")
+        flags = _abi.STEP_PHYSICS | (_abi.STEP_HISTORY if _history else 0)
+        timer = self.kernel_timer
+        if timer is not None:  # HIP events on the launch stream around the fused kernel (bench.py)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        _abi.check(self._L.lrl_sim_step(self._sim, C.c_void_p(actions.data_ptr()), C.c_uint32(flags), self._stream()))
+        if timer is not None:
+            ev1.record()
+            timer.append((ev0, ev1))
+        self.common_step_counter += 1
+        ex = self.extras
+        ex["privileged_obs"] = self.privileged_obs_buf
+        ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())
+        ex.set_lazy("joint_vel", lambda: self.dof_vel.cpu().numpy())
+        ex.set_lazy("joint_pos_target", lambda: self.joint_pos_target.cpu().numpy())
+        ex["joint_vel_target"] = torch.zeros(12)
+        ex.set_lazy("body_linear_vel", lambda: self.base_lin_vel.cpu().numpy())
+        ex.set_lazy("body_angular_vel", lambda: self.base_ang_vel.cpu().numpy())
+        ex.set_lazy("body_linear_vel_cmd", lambda: self.commands.cpu().numpy()[:, 0:2])
+        ex.set_lazy("body_angular_vel_cmd", lambda: self.commands.cpu().numpy()[:, 2:])
+        ex.set_lazy("contact_states", lambda: (self.contact_forces[:, self.feet_indices, 2] > 1.0).cpu().numpy().copy())
+        ex.set_lazy("foot_positions", lambda: self._foot_positions().cpu().numpy().copy())
+        ex.set_lazy("body_pos", lambda: self.root_states[:, 0:3].cpu().numpy())
+        ex.set_lazy("torques", lambda: self.torques.cpu().numpy())
+        return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
+
+    def _foot_positions(self):
+        self.refresh_rigid_body_state()
+        return self.rigid_body_state[:, self.feet_indices, 0:3]
+
+    def refresh_rigid_body_state(self):
+        _abi.check(self._L.lrl_sim_refresh_rigid_body_state(self._sim, self._stream()))
+
+    def get_observations(self):
+        return self.obs_buf
+
+    def get_privileged_observations(self, horizon=0):
+        return self.privileged_obs_buf
+
+    def reset(self):
+        """VelocityTrackingEasyEnv.reset (:66-69): reset all, then one zero-action step."""
+        self.reset_idx(torch.arange(self.num_envs, device=self.device))
+        obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
+        return obs
+
+    def reset_idx(self, env_ids):
+        """legged_robot.py:227-290 (train envs)."""
+        env_ids = torch.as_tensor(env_ids, device=self.device).long()
+        if len(env_ids) == 0:
+            return
+        self.update_command_curriculum(env_ids, self.cfg)
+        ids32 = env_ids.to(torch.int32).contiguous()
+        xo = yo = 0.0
+        if self.custom_origins:  # torch_rand_float(x_init_range, y_init_range) == constant (Q8)
+            t = self.cfg.terrain
+            xo = float(t.x_init_range) + float(t.x_init_offset)
+            yo = float(t.x_init_range) + float(t.y_init_offset)
+        # episode logging before the kernel zeroes the per-env state (:261-267)
+        ep = {}
+        sel = self._episode_sums[:, env_ids]
+        means = sel.mean(dim=1)
+        for i, k in enumerate(self.episode_sums):
+            ep["rew_" + k] = means[i]
+        self._episode_sums[:, env_ids] = 0.0
+        _abi.check(self._L.lrl_sim_reset_idx_ex(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
+                                                C.c_int32(1), C.c_float(xo), C.c_float(yo), self._stream()))
+        self.extras["train/episode"] = ep
+        if self.cfg.commands.command_curriculum:
+            self.env_command_bins_t = torch.tensor(self.env_command_bins, dtype=torch.float, device=self.device)
+            self.extras["env_bins"] = self.env_command_bins_t[:self.num_train_envs]
+            ep["command_area"] = np.sum(self.curriculum.weights) / self.curriculum.weights.shape[0]
+        if self.cfg.env.send_timeouts:
+            self.extras["time_outs"] = self.time_out_buf[:self.num_train_envs]
+
+    def update_command_curriculum(self, env_ids, cfg, episode_sums=None):
+        """_update_command_curriculum_uniform (legged_robot.py:851-880)."""
+        c = cfg.commands
+        if c.command_curriculum and (self.common_step_counter % cfg.env.max_episode_length == 0):
+            if self.reward_scales.get("tracking_lin_vel", 0) > 0:
+                m = torch.mean(self.episode_sums["tracking_lin_vel"][env_ids]) / cfg.env.max_episode_length
+                if m > c.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]:
+                    cfg.command_ranges["lin_vel_x"][0] = np.clip(cfg.command_ranges["lin_vel_x"][0] - 0.2,
+                                                                 -c.max_reverse_curriculum, 0.0)
+                    cfg.command_ranges["lin_vel_x"][1] = np.clip(cfg.command_ranges["lin_vel_x"][1] + 0.2, 0.0,
+                                                                 c.max_forward_curriculum)
+        if c.yaw_command_curriculum and (self.common_step_counter % cfg.env.max_episode_length == 0):
+            if self.reward_scales.get("tracking_ang_vel", 0) > 0:
+                m = torch.mean(self.episode_sums["tracking_ang_vel"][env_ids]) / cfg.env.max_episode_length
+                if m > c.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]:
+                    cfg.command_ranges["ang_vel_yaw"][0] = np.clip(cfg.command_ranges["ang_vel_yaw"][0] - 0.2,
+                                                                   -c.max_yaw_curriculum, 0.0)
+                    cfg.command_ranges["ang_vel_yaw"][1] = np.clip(cfg.command_ranges["ang_vel_yaw"][1] + 0.2, 0.0,
+                                                                   c.max_yaw_curriculum)
+
+    def reset_evaluation_envs(self):
+        return None  # no eval_cfg (legged_robot.py:205)
+
+    # ---- gymapi-style setters (data is already in place when written through the views) ----
+    def set_actor_root_state_tensor_indexed(self, root_states, env_ids):
+        ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).contiguous()
+        src = root_states.contiguous()
+        _abi.check(self._L.lrl_sim_set_root_state_indexed(self._sim, C.c_void_p(src.data_ptr()),
+                                                          C.c_void_p(ids.data_ptr()), C.c_int32(len(ids)),
+                                                          self._stream()))
+
+    def set_dof_state_tensor_indexed(self, dof_pos, dof_vel, env_ids):
+        ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).contiguous()
+        p, v = dof_pos.contiguous(), dof_vel.contiguous()
+        _abi.check(self._L.lrl_sim_set_dof_state_indexed(self._sim, C.c_void_p(p.data_ptr()), C.c_void_p(v.data_ptr()),
+                                                         C.c_void_p(ids.data_ptr()), C.c_int32(len(ids)),
+                                                         self._stream()))
+
+    def shift_history(self):
+        _abi.check(self._L.lrl_sim_shift_history(self._sim, self._stream()))
+
+    # ---- recording hooks used by Runner.log_video (rendering is out of scope) ----
+    def start_recording(self):
+        self.record_now = True
+
+    def start_recording_eval(self):
+        pass
+
+    def pause_recording(self):
+        self.record_now = False
+
+    def pause_recording_eval(self):
+        pass
+
+    def get_complete_frames(self):
+        return []
+
+    def get_complete_frames_eval(self):
+        return []
+
+
+VelocityTrackingEasyEnv = LeggedRobotEnv

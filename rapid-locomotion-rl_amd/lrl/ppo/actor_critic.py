@@ -1,0 +1,157 @@
+"""Teacher/student actor-critic (mini_gym_learn/ppo/actor_critic.py:23-173).
+
+Parameters live in torch (nn.Module, so state dicts / checkpoints keep the reference's 35-key
+layout, including the duplicate ``encoder.*`` registration of ``env_factor_encoder`` — Q13).  The
+rollout forward of the teacher path (encoder -> actor / critic -> Normal sample -> log-prob) runs as
+ONE fused HIP launch (``lrl_policy_act``, fp32 MFMA); the minibatch update currently uses torch
+autograd on the same parameters.
+"""
+import ctypes as C
+
+import torch
+import torch.nn as nn
+
+from .. import _abi
+
+
+class AC_Args:
+    """actor_critic.py:9-20"""
+    init_noise_std = 1.0
+    actor_hidden_dims = [512, 256, 128]
+    critic_hidden_dims = [512, 256, 128]
+    activation = "elu"
+    adaptation_module_branch_hidden_dims = [[256, 32]]
+    env_factor_encoder_branch_input_dims = [18]
+    env_factor_encoder_branch_latent_dims = [18]
+    env_factor_encoder_branch_hidden_dims = [[256, 128]]
+
+
+def get_activation(name):
+    return {"elu": nn.ELU(), "selu": nn.SELU(), "relu": nn.ReLU(), "crelu": nn.ReLU(), "lrelu": nn.LeakyReLU(),
+            "tanh": nn.Tanh(), "sigmoid": nn.Sigmoid()}.get(name)
+
+
+def _mlp(dims, act):
+    layers = []
+    for i in range(len(dims) - 1):
+        layers.append(nn.Linear(dims[i], dims[i + 1]))
+        if i < len(dims) - 2:
+            layers.append(act)
+    return nn.Sequential(*layers)
+
+
+def mlp_desc(seq):
+    """nn.Sequential of Linear/ELU -> lrl_mlp_desc (device pointers of W [out,in], b [out])."""
+    lin = [m for m in seq if isinstance(m, nn.Linear)]
+    d = _abi.LrlMlpDesc()
+    d.num_layers = len(lin)
+    d.dims[0] = lin[0].in_features
+    for i, m in enumerate(lin):
+        assert m.weight.is_contiguous() and m.weight.dtype == torch.float32
+        d.dims[i + 1] = m.out_features
+        d.weight[i] = m.weight.data_ptr()
+        d.bias[i] = m.bias.data_ptr()
+    return d
+
+
+class ActorCritic(nn.Module):
+    is_recurrent = False
+
+    def __init__(self, num_obs, num_privileged_obs, num_obs_history, num_actions, **kwargs):
+        super().__init__()
+        act = get_activation(AC_Args.activation)
+        enc_in = AC_Args.env_factor_encoder_branch_input_dims[0]
+        enc_lat = AC_Args.env_factor_encoder_branch_latent_dims[0]
+        self.env_factor_encoder = _mlp([enc_in] + AC_Args.env_factor_encoder_branch_hidden_dims[0] + [enc_lat], act)
+        self.add_module("encoder", self.env_factor_encoder)
+        self.adaptation_module = _mlp([num_obs_history] + AC_Args.adaptation_module_branch_hidden_dims[0] + [enc_lat],
+                                      act)
+        latent = sum(AC_Args.env_factor_encoder_branch_latent_dims)
+        self.actor_body = _mlp([latent + num_obs] + AC_Args.actor_hidden_dims + [num_actions], act)
+        self.critic_body = _mlp([latent + num_obs] + AC_Args.critic_hidden_dims + [1], act)
+        self.std = nn.Parameter(AC_Args.init_noise_std * torch.ones(num_actions))
+        self.num_obs, self.num_privileged_obs, self.num_actions = num_obs, num_privileged_obs, num_actions
+        self.distribution = None
+        self._descs = None
+
+    # ---- reference API (torch path; used by the update and for checkpoint-compatible inference) ----
+    def reset(self, dones=None):
+        pass
+
+    def forward(self):
+        raise NotImplementedError
+
+    @property
+    def action_mean(self):
+        return self.distribution.mean
+
+    @property
+    def action_std(self):
+        return self.distribution.stddev
+
+    @property
+    def entropy(self):
+        return self.distribution.entropy().sum(dim=-1)
+
+    def update_distribution(self, observations, privileged_observations):
+        latent = self.env_factor_encoder(privileged_observations)
+        mean = self.actor_body(torch.cat((observations, latent), dim=-1))
+        self.distribution = torch.distributions.Normal(mean, mean * 0.0 + self.std, validate_args=False)
+
+    def act(self, observations, privileged_observations, **kwargs):
+        self.update_distribution(observations, privileged_observations)
+        return self.distribution.sample()
+
+    def get_actions_log_prob(self, actions):
+        return self.distribution.log_prob(actions).sum(dim=-1)
+
+    def act_expert(self, ob, policy_info={}):
+        return self.act_teacher(ob["obs"], ob["privileged_obs"])
+
+    def act_inference(self, ob, policy_info={}):
+        if ob["privileged_obs"] is not None:
+            policy_info["gt_latents"] = self.env_factor_encoder(ob["privileged_obs"]).detach().cpu().numpy()
+        return self.act_student(ob["obs"], ob["obs_history"])
+
+    def act_student(self, observations, observation_history, policy_info={}):
+        latent = self.adaptation_module(observation_history)
+        policy_info["latents"] = latent.detach().cpu().numpy()
+        return self.actor_body(torch.cat((observations, latent), dim=-1))
+
+    def act_teacher(self, observations, privileged_info, policy_info={}):
+        latent = self.env_factor_encoder(privileged_info)
+        policy_info["latents"] = latent.detach().cpu().numpy()
+        return self.actor_body(torch.cat((observations, latent), dim=-1))
+
+    def evaluate(self, critic_observations, privileged_observations, **kwargs):
+        latent = self.env_factor_encoder(privileged_observations)
+        return self.critic_body(torch.cat((critic_observations, latent), dim=-1))
+
+    # ---- fused HIP rollout path ----
+    def _hip_descs(self):
+        ptrs = tuple(p.data_ptr() for p in self.parameters())
+        if self._descs is None or self._descs[0] != ptrs:
+            self._descs = (ptrs, mlp_desc(self.env_factor_encoder), mlp_desc(self.actor_body),
+                           mlp_desc(self.critic_body))
+        return self._descs[1:]
+
+    def act_fused(self, obs, priv, hist=None, eps=None, seed=0, counter=0, store=None, store_row=0):
+        """PPO.act teacher path in one launch.  Returns (actions, mu, values [N,1], logp [N])."""
+        n = obs.shape[0]
+        dev = obs.device
+        assert obs.is_contiguous() and priv.is_contiguous() and obs.dtype == torch.float32
+        actions = torch.empty(n, self.num_actions, device=dev)
+        mu = torch.empty(n, self.num_actions, device=dev)
+        values = torch.empty(n, 1, device=dev)
+        logp = torch.empty(n, device=dev)
+        enc, act, cri = self._hip_descs()
+        std = self.std.detach()
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+        st = C.byref(store) if store is not None else None
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _abi.check(_abi.lib().lrl_policy_act(C.byref(enc), C.byref(act), C.byref(cri), ptr(std), ptr(obs), ptr(priv),
+                                             ptr(hist), C.c_int32(n), C.c_int32(obs.shape[1]),
+                                             C.c_int32(priv.shape[1]), ptr(eps), C.c_uint64(seed),
+                                             C.c_uint64(counter), ptr(actions), ptr(mu), ptr(values), ptr(logp), st,
+                                             C.c_int32(store_row), stream))
+        return actions, mu, values, logp

@@ -1,0 +1,197 @@
+"""PPO (mini_gym_learn/ppo/ppo.py:15-178) on the MI355X path.
+
+Rollout: ``act`` is one fused HIP launch (encoder + actor + critic + Normal sample + log-prob +
+storage write); GAE is the HIP kernel of RolloutStorage.compute_returns.  Update: the reference's
+algorithm step for step — adaptive-KL learning rate, clipped surrogate, clipped value loss,
+entropy bonus, grad-norm clip 1.0, Adam; then the adaptation-module regression with a second Adam
+over all parameters (Q14) — on the same parameters with torch autograd.  With
+``torch.distributed`` initialised, gradients are averaged with one flat all-reduce per optimiser
+step and the KL mean / advantage statistics are all-reduced so every rank takes identical steps.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .actor_critic import ActorCritic
+from .rollout_storage import RolloutStorage
+
+
+class PPO_Args:
+    value_loss_coef = 1.0
+    use_clipped_value_loss = True
+    clip_param = 0.2
+    entropy_coef = 0.01
+    num_learning_epochs = 5
+    num_mini_batches = 4
+    learning_rate = 1.e-3
+    adaptation_module_learning_rate = 1.e-3
+    num_adaptation_module_substeps = 1
+    schedule = "adaptive"
+    gamma = 0.99
+    lam = 0.95
+    desired_kl = 0.01
+    max_grad_norm = 1.
+
+
+def _world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+class PPO:
+    actor_critic: ActorCritic
+
+    def __init__(self, actor_critic, device="cpu", fused=None, seed=0):
+        self.device = device
+        self.actor_critic = actor_critic.to(device)
+        self.storage = None
+        self.optimizer = torch.optim.Adam(self.actor_critic.parameters(), lr=PPO_Args.learning_rate)
+        self.adaptation_module_optimizer = torch.optim.Adam(self.actor_critic.parameters(),
+                                                            lr=PPO_Args.adaptation_module_learning_rate)
+        self.transition = RolloutStorage.Transition()
+        self.learning_rate = PPO_Args.learning_rate
+        self.fused = (torch.device(device).type == "cuda") if fused is None else fused
+        self.seed = seed
+        self._act_counter = 0
+        self._store = None
+        self.grad_allreduce = _world() > 1
+
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, privileged_obs_shape, obs_history_shape,
+                     action_shape):
+        self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, privileged_obs_shape,
+                                      obs_history_shape, action_shape, self.device)
+        self._store = self.storage.store_desc() if self.fused else None
+
+    def test_mode(self):
+        self.actor_critic.eval()
+
+    def train_mode(self):
+        self.actor_critic.train()
+
+    def act(self, obs, privileged_obs, obs_history, eps=None):
+        if self.fused:
+            self._act_counter += 1
+            a, mu, v, lp = self.actor_critic.act_fused(
+                obs.contiguous(), privileged_obs.contiguous(), obs_history.contiguous(), eps=eps, seed=self.seed,
+                counter=self._act_counter, store=self._store, store_row=self.storage.step)
+            t = self.transition
+            t.actions, t.values, t.actions_log_prob, t.action_mean = a, v, lp, mu
+            t.action_sigma = self.actor_critic.std.detach().expand_as(mu)
+            t.observations = t.critic_observations = obs
+            t.privileged_observations, t.observation_histories = privileged_obs, obs_history
+            return a
+        t = self.transition
+        t.actions = self.actor_critic.act(obs, privileged_obs).detach()
+        t.values = self.actor_critic.evaluate(obs, privileged_obs).detach()
+        t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
+        t.action_mean = self.actor_critic.action_mean.detach()
+        t.action_sigma = self.actor_critic.action_std.detach()
+        t.observations = t.critic_observations = obs
+        t.privileged_observations, t.observation_histories = privileged_obs, obs_history
+        return t.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        t = self.transition
+        t.rewards = rewards.clone()
+        t.dones = dones
+        t.env_bins = infos["env_bins"]
+        if "time_outs" in infos:  # bootstrapping on time outs (ppo.py:81-83)
+            t.rewards += PPO_Args.gamma * torch.squeeze(t.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        self.storage.add_transitions(t, fused=self.fused)
+        t.clear()
+        self.actor_critic.reset(dones)
+
+    def compute_returns(self, last_critic_obs, last_critic_privileged_obs):
+        if self.fused:
+            _, _, last_values, _ = self.actor_critic.act_fused(last_critic_obs.contiguous(),
+                                                               last_critic_privileged_obs.contiguous(),
+                                                               seed=self.seed, counter=0)
+        else:
+            last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
+        reduce = None
+        if _world() > 1:
+            def reduce(stats):
+                dist.all_reduce(stats)
+                return stats
+        self.storage.compute_returns(last_values, PPO_Args.gamma, PPO_Args.lam, reduce_stats=reduce)
+
+    def _allreduce_grads(self, params):
+        grads = [p.grad for p in params if p.grad is not None]
+        if not grads:
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat)
+        flat /= _world()
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
+
+    def update(self):
+        mean_value_loss = torch.zeros((), device=self.device)
+        mean_surrogate_loss = torch.zeros((), device=self.device)
+        mean_adaptation_module_loss = torch.zeros((), device=self.device)
+        ac = self.actor_critic
+        params = list(ac.parameters())
+        gen = self.storage.mini_batch_generator(PPO_Args.num_mini_batches, PPO_Args.num_learning_epochs)
+        for (obs_b, critic_obs_b, priv_b, hist_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+             old_sigma_b, masks_b, env_bins_b) in gen:
+            ac.act(obs_b, priv_b, masks=masks_b)
+            logp_b = ac.get_actions_log_prob(actions_b)
+            value_b = ac.evaluate(critic_obs_b, priv_b, masks=masks_b)
+            mu_b, sigma_b, entropy_b = ac.action_mean, ac.action_std, ac.entropy
+            if PPO_Args.desired_kl is not None and PPO_Args.schedule == "adaptive":
+                with torch.inference_mode():
+                    kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.e-5) + (
+                        torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) / (2.0 * torch.square(sigma_b))
+                        - 0.5, axis=-1)
+                    kl_mean = torch.mean(kl)
+                    if _world() > 1:
+                        kl_mean = kl_mean.clone()
+                        dist.all_reduce(kl_mean)
+                        kl_mean /= _world()
+                    kl_mean = kl_mean.item()
+                    if kl_mean > PPO_Args.desired_kl * 2.0:
+                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+                    elif kl_mean < PPO_Args.desired_kl / 2.0 and kl_mean > 0.0:
+                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+                    for g in self.optimizer.param_groups:
+                        g["lr"] = self.learning_rate
+            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+            surrogate = -torch.squeeze(adv_b) * ratio
+            surrogate_clipped = -torch.squeeze(adv_b) * torch.clamp(ratio, 1.0 - PPO_Args.clip_param,
+                                                                   1.0 + PPO_Args.clip_param)
+            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+            if PPO_Args.use_clipped_value_loss:
+                value_clipped = target_values_b + (value_b - target_values_b).clamp(-PPO_Args.clip_param,
+                                                                                    PPO_Args.clip_param)
+                value_loss = torch.max((value_b - returns_b).pow(2), (value_clipped - returns_b).pow(2)).mean()
+            else:
+                value_loss = (returns_b - value_b).pow(2).mean()
+            loss = surrogate_loss + PPO_Args.value_loss_coef * value_loss - PPO_Args.entropy_coef * entropy_b.mean()
+            self.optimizer.zero_grad()
+            loss.backward()
+            if self.grad_allreduce:
+                self._allreduce_grads(params)
+            nn.utils.clip_grad_norm_(params, PPO_Args.max_grad_norm)
+            self.optimizer.step()
+            mean_value_loss += value_loss.detach()
+            mean_surrogate_loss += surrogate_loss.detach()
+            for _ in range(PPO_Args.num_adaptation_module_substeps):
+                adaptation_pred = ac.adaptation_module(hist_b)
+                with torch.no_grad():
+                    adaptation_target = ac.env_factor_encoder(priv_b)
+                adaptation_loss = F.mse_loss(adaptation_pred, adaptation_target)
+                self.adaptation_module_optimizer.zero_grad()
+                adaptation_loss.backward()
+                if self.grad_allreduce:
+                    self._allreduce_grads(params)
+                self.adaptation_module_optimizer.step()
+                mean_adaptation_module_loss += adaptation_loss.detach()
+        num_updates = PPO_Args.num_learning_epochs * PPO_Args.num_mini_batches
+        out = torch.stack([mean_value_loss / num_updates, mean_surrogate_loss / num_updates,
+                           mean_adaptation_module_loss / (num_updates * PPO_Args.num_adaptation_module_substeps)])
+        self.storage.clear()
+        mv, ms, ma = out.tolist()
+        return mv, ms, ma

@@ -1,0 +1,143 @@
+"""On-policy runner (mini_gym_learn/ppo/__init__.py:47-298): rollout -> GAE -> update.
+
+Same constructor (``Runner(env, device)``), ``RunnerArgs`` and ``learn(num_learning_iterations,
+init_at_random_ep_len, eval_freq, eval_expert)`` signature and iteration order as the reference.
+ml_logger is replaced by a small local logger (metrics in memory + a JSON-lines file when a run
+directory is configured); checkpoints keep the reference's state-dict layout and file names
+(``checkpoints/ac_weights_{it:06d}.pt`` / ``ac_weights_last.pt``) plus the TorchScript exports of
+``adaptation_module`` and ``actor_body``.
+"""
+import copy
+import json
+import os
+import time
+from collections import defaultdict
+
+import torch
+
+from .actor_critic import ActorCritic
+from .ppo import PPO
+
+
+class RunnerArgs:
+    algorithm_class_name = "PPO"
+    num_steps_per_env = 24
+    max_iterations = 1500
+    save_interval = 400
+    save_video_interval = 100
+    log_freq = 10
+    resume = False
+    load_run = -1
+    checkpoint = -1
+    resume_path = None
+
+
+class Logger:
+    """The subset of ml_logger the runner uses."""
+
+    def __init__(self, root=None):
+        self.root = root
+        self.prefix = root or "memory"
+        self.metrics = defaultdict(list)
+        self.summaries = []
+        self._t0 = time.time()
+        self._split = time.time()
+
+    def store_metrics(self, **kw):
+        for k, v in kw.items():
+            self.metrics[k].append(float(v) if not isinstance(v, float) else v)
+
+    def since(self, _="start"):
+        return time.time() - self._t0
+
+    def split(self, _="epoch"):
+        t, self._split = time.time() - self._split, time.time()
+        return t
+
+    def log_metrics_summary(self, key_values=None):
+        s = {k: sum(v) / len(v) for k, v in self.metrics.items() if v}
+        s.update(key_values or {})
+        self.summaries.append(s)
+        self.metrics.clear()
+        if self.root:
+            os.makedirs(self.root, exist_ok=True)
+            with open(os.path.join(self.root, "metrics.jsonl"), "a") as f:
+                f.write(json.dumps(s) + "\n")
+
+    def torch_save(self, obj, path):
+        if self.root:
+            full = os.path.join(self.root, path)
+            os.makedirs(os.path.dirname(full), exist_ok=True)
+            torch.save(obj, full)
+
+
+class Runner:
+    def __init__(self, env, device="cpu", seed=0, logger=None):
+        self.device = device
+        self.env = env
+        ac = ActorCritic(self.env.num_obs, self.env.num_privileged_obs, self.env.num_obs_history,
+                         self.env.num_actions).to(self.device)
+        self.alg = PPO(ac, device=self.device, seed=seed)
+        self.num_steps_per_env = RunnerArgs.num_steps_per_env
+        self.alg.init_storage(self.env.num_train_envs, self.num_steps_per_env, [self.env.num_obs],
+                              [self.env.num_privileged_obs], [self.env.num_obs_history], [self.env.num_actions])
+        self.tot_timesteps = 0
+        self.tot_time = 0
+        self.current_learning_iteration = 0
+        self.last_recording_it = 0
+        self.logger = logger or Logger()
+        self.env.reset()
+
+    def learn(self, num_learning_iterations, init_at_random_ep_len=False, eval_freq=100, eval_expert=False):
+        lg = self.logger
+        if init_at_random_ep_len:  # lands on the wrapper, not the env, as in the reference (Q5)
+            self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
+                                                             high=int(self.env.max_episode_length))
+        n_train = self.env.num_train_envs
+        obs_dict = self.env.get_observations()
+        obs, priv, hist = obs_dict["obs"], obs_dict["privileged_obs"], obs_dict["obs_history"]
+        self.alg.actor_critic.train()
+        tot_iter = self.current_learning_iteration + num_learning_iterations
+        for it in range(self.current_learning_iteration, tot_iter):
+            with torch.inference_mode():
+                for _ in range(self.num_steps_per_env):
+                    actions = self.alg.act(obs[:n_train], priv[:n_train], hist[:n_train])
+                    obs_dict, rewards, dones, infos = self.env.step(actions)
+                    obs, priv, hist = obs_dict["obs"], obs_dict["privileged_obs"], obs_dict["obs_history"]
+                    self.alg.process_env_step(rewards[:n_train], dones[:n_train], infos)
+                self.alg.compute_returns(obs[:n_train], priv[:n_train])
+                if it % eval_freq == 0:
+                    self.env.reset_evaluation_envs()
+            mv, ms, ma = self.alg.update()
+            lg.store_metrics(time_elapsed=lg.since("start"), time_iter=lg.split("epoch"), adaptation_loss=ma,
+                             mean_value_loss=mv, mean_surrogate_loss=ms)
+            self.tot_timesteps += self.num_steps_per_env * self.env.num_envs
+            if (it + 1) % RunnerArgs.log_freq == 0:
+                lg.log_metrics_summary(key_values={"timesteps": self.tot_timesteps, "iterations": it})
+            if RunnerArgs.save_interval and it % RunnerArgs.save_interval == 0:
+                self.save(it)
+        self.current_learning_iteration += num_learning_iterations
+
+    def save(self, it):
+        lg = self.logger
+        if not lg.root:
+            return
+        sd = self.alg.actor_critic.state_dict()
+        lg.torch_save(sd, f"checkpoints/ac_weights_{it:06d}.pt")
+        lg.torch_save(sd, "checkpoints/ac_weights_last.pt")
+        path = os.path.join(lg.root, "checkpoints")
+        ac = self.alg.actor_critic
+        torch.jit.script(copy.deepcopy(ac.adaptation_module).to("cpu")).save(os.path.join(path, "adaptation_module_latest.jit"))
+        torch.jit.script(copy.deepcopy(ac.actor_body).to("cpu")).save(os.path.join(path, "body_latest.jit"))
+
+    def get_inference_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_inference
+
+    def get_expert_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_expert
