@@ -17,6 +17,8 @@ static int fail(int code, const char* fmt, ...) {
   va_end(ap);
   return code;
 }
+extern "C" int lrl_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
 #define HIPCHECK(x)                                                                     \
   do {                                                                                  \
     hipError_t e_ = (x);                                                                \
@@ -263,12 +265,12 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
 
 int32_t lrl_sim_destroy(lrl_sim* s) {
   if (!s) return 0;
-  hipSetDevice(s->device);
-  hipFree(s->arena);
-  hipFree(s->dk);
-  hipFree(s->d_body_leg);
-  hipFree(s->d_body_link);
-  hipFree(s->d_foot_xyz);
+  (void)hipSetDevice(s->device);
+  (void)hipFree(s->arena);
+  (void)hipFree(s->dk);
+  (void)hipFree(s->d_body_leg);
+  (void)hipFree(s->d_body_link);
+  (void)hipFree(s->d_foot_xyz);
   delete s;
   return 0;
 }

@@ -11,6 +11,8 @@
 
 #include "../../include/lrl.h"
 
+extern "C" int lrl_set_error(int code, const char* msg);
+
 namespace lrl {
 
 constexpr int GAE_BLOCK = 256;
@@ -96,28 +98,30 @@ static int gae_partial(const float* rewards, const uint8_t* dones, const float* 
                        double* stats, hipStream_t st) {
   if (T <= 0 || N <= 0 || !rewards || !dones || !values || !last_values || !returns || !advantages || !workspace ||
       !stats)
-    return LRL_E_INVALID;
+    return lrl_set_error(LRL_E_INVALID, "lrl_gae: null argument or empty shape");
   const int blocks = (N + lrl::GAE_BLOCK - 1) / lrl::GAE_BLOCK;
-  if (blocks > 1000) return LRL_E_INVALID;  // workspace: 2 doubles per block
+  if (blocks > 1000) return lrl_set_error(LRL_E_INVALID, "lrl_gae: N > 256000 (workspace holds 1000 partials)");
   double* part = reinterpret_cast<double*>(workspace);
   hipLaunchKernelGGL(lrl::gae_kernel, dim3(blocks), dim3(lrl::GAE_BLOCK), 0, st, rewards, dones, values, last_values,
                      T, N, gamma, lam, returns, advantages, part);
   hipLaunchKernelGGL(lrl::gae_fold_kernel, dim3(1), dim3(64), 0, st, part, blocks, (int64_t)T * N, stats);
-  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, hipGetErrorString(e));
 }
 
 static int adv_normalize(float* adv, int64_t total, const double* stats, hipStream_t st) {
-  if (!adv || !stats || total < 2) return LRL_E_INVALID;
+  if (!adv || !stats || total < 2) return lrl_set_error(LRL_E_INVALID, "lrl_adv_normalize: bad arguments");
   int nb = (int)((total + lrl::GAE_BLOCK - 1) / lrl::GAE_BLOCK);
   if (nb > 1024) nb = 1024;
   hipLaunchKernelGGL(lrl::adv_normalize_kernel, dim3(nb), dim3(lrl::GAE_BLOCK), 0, st, adv, total, stats);
-  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, hipGetErrorString(e));
 }
 
 extern "C" int32_t lrl_gae(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
                            int32_t T, int32_t N, float gamma, float lam, float* returns, float* advantages,
                            float* workspace, void* stream) {
-  if (!workspace) return LRL_E_INVALID;
+  if (!workspace) return lrl_set_error(LRL_E_INVALID, "lrl_gae: null workspace");
   double* stats = reinterpret_cast<double*>(workspace + 4000);
   int rc = gae_partial(rewards, dones, values, last_values, T, N, gamma, lam, returns, advantages, workspace, stats,
                        (hipStream_t)stream);

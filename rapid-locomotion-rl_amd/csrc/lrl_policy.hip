@@ -23,6 +23,8 @@
 #include "../../include/lrl.h"
 #include "../../include/lrl_philox.h"
 
+extern "C" int lrl_set_error(int code, const char* msg);
+
 namespace lrl {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -174,13 +176,23 @@ __global__ __launch_bounds__(PTHREADS) void policy_act_kernel(lrl_mlp_desc enc, 
       size_t g = row0 + i / np;
       if (g < (size_t)n) store.priv[(b + row0) * np + i] = priv[(size_t)row0 * np + i];
     }
-    if (hist && store.hist) {
+    if (hist && store.hist) {  // the tile's history rows are one contiguous span in both buffers
       const int hd = store.hist_dim;
       const int rows = min(PROWS, n - row0);
-      const float4* src = reinterpret_cast<const float4*>(hist + (size_t)row0 * hd);
-      float4* dst = reinterpret_cast<float4*>(store.hist + (b + row0) * hd);
-      const int n4 = rows * hd / 4;
-      for (int i = threadIdx.x; i < n4; i += PTHREADS) dst[i] = src[i];
+      const float* src = hist + (size_t)row0 * hd;
+      float* dst = store.hist + (b + row0) * hd;
+      const int cnt = rows * hd;
+      if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int i = threadIdx.x; i < cnt / 4; i += PTHREADS) d4[i] = s4[i];
+      } else if ((((uintptr_t)src | (uintptr_t)dst) & 7) == 0 && (cnt & 1) == 0) {
+        const float2* s2 = reinterpret_cast<const float2*>(src);
+        float2* d2 = reinterpret_cast<float2*>(dst);
+        for (int i = threadIdx.x; i < cnt / 2; i += PTHREADS) d2[i] = s2[i];
+      } else {
+        for (int i = threadIdx.x; i < cnt; i += PTHREADS) dst[i] = src[i];
+      }
     }
   }
 }
@@ -196,22 +208,27 @@ extern "C" int32_t lrl_policy_act(const lrl_mlp_desc* encoder, const lrl_mlp_des
                                   int32_t num_obs, int32_t num_priv, const float* eps, uint64_t seed, uint64_t counter,
                                   float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
                                   int32_t store_row, void* stream) {
-  if (!encoder || !actor || !critic || !std_ || !obs || !priv || !actions || n <= 0) return LRL_E_INVALID;
+  if (!encoder || !actor || !critic || !std_ || !obs || !priv || !actions || n <= 0)
+    return lrl_set_error(LRL_E_INVALID, "lrl_policy_act: null argument or n <= 0");
   const int nl = encoder->dims[encoder->num_layers];
-  if (num_obs + nl > 64 || num_priv > 32 || actor->dims[actor->num_layers] > 16) return LRL_E_INVALID;
+  if (num_obs + nl > 64 || num_priv > 32 || actor->dims[actor->num_layers] > 16)
+    return lrl_set_error(LRL_E_INVALID, "lrl_policy_act: obs+latent > 64, priv > 32 or actions > 16");
   if (actor->dims[0] != num_obs + nl || critic->dims[0] != num_obs + nl || encoder->dims[0] != num_priv)
-    return LRL_E_INVALID;
+    return lrl_set_error(LRL_E_INVALID, "lrl_policy_act: layer input widths do not match obs/priv/latent");
   for (const lrl_mlp_desc* d : {encoder, actor, critic}) {
-    if (d->num_layers < 1 || d->num_layers > 7) return LRL_E_INVALID;
+    if (d->num_layers < 1 || d->num_layers > 7) return lrl_set_error(LRL_E_INVALID, "lrl_policy_act: 1..7 layers");
     for (int l = 0; l <= d->num_layers; ++l)
-      if (d->dims[l] <= 0 || d->dims[l] > lrl::MAXW) return LRL_E_INVALID;
+      if (d->dims[l] <= 0 || d->dims[l] > lrl::MAXW)
+        return lrl_set_error(LRL_E_INVALID, "lrl_policy_act: layer width must be 1..512");
   }
-  if (store && (store->hist_dim % 4)) return LRL_E_INVALID;
+  if (store && (!store->obs || !store->priv || !store->actions || !store->values || !store->logp || !store->mu ||
+                !store->sigma || store->hist_dim < 0))
+    return lrl_set_error(LRL_E_INVALID, "lrl_policy_act: incomplete rollout store");
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)lrl::policy_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             policy_lds_bytes()) != hipSuccess)
-      return LRL_E_HIP;
+      return lrl_set_error(LRL_E_HIP, "lrl_policy_act: cannot raise the LDS limit");
     attr = true;
   }
   lrl_rollout_store st{};
@@ -220,5 +237,6 @@ extern "C" int32_t lrl_policy_act(const lrl_mlp_desc* encoder, const lrl_mlp_des
   hipLaunchKernelGGL(lrl::policy_act_kernel, dim3(blocks), dim3(lrl::PTHREADS), policy_lds_bytes(), (hipStream_t)stream,
                      *encoder, *actor, *critic, std_, obs, priv, hist, n, num_obs, num_priv, eps, seed, counter,
                      actions, mu, values, logp, st, store_row, store ? 1 : 0);
-  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, hipGetErrorString(e));
 }

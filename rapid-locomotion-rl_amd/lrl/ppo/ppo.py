@@ -51,7 +51,8 @@ class PPO:
         self.transition = RolloutStorage.Transition()
         self.learning_rate = PPO_Args.learning_rate
         self.fused = (torch.device(device).type == "cuda") if fused is None else fused
-        self.seed = seed
+        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.seed = seed + 1000003 * rank  # per-rank policy-noise stream (counter RNG keyed by local row)
         self._act_counter = 0
         self._store = None
         self.grad_allreduce = _world() > 1
