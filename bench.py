@@ -26,6 +26,19 @@ B_ENV = 1325            # algorithmic HBM bytes per env-step;
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary (profiles/r*_pmc.json,
+    written by scripts/gpu_profile.sh + scripts/pmc_summary.py from separate rocprofv3 --pmc passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    for path in reversed(files):
+        with open(path) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        if k:
+            return k["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(seconds=12.0):
     """The CPU oracle (oracle/lrl_oracle.c: dense fp64 dynamics + fp32 bookkeeping), one core, on a
     bounded sample of the same workload: 256 Mini Cheetah envs stepping with random actions."""
@@ -124,6 +137,7 @@ def main():
     value = steps_total / elapsed
     if rank == 0:
         achieved = B_ENV * ENVS_PER_GPU / (k_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic("lrl::env_step_kernel")
         out = {
             "metric": "env-steps/sec, 4096 Mini Cheetah envs, 1/2/4/8 MI355X; PPO iters/sec",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -137,8 +151,9 @@ def main():
             "env_step_kernel_ms": round(k_ms, 4),
             "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel", "achieved": round(achieved, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": None,
-                         "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch; the kernel is "
+                         "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
+                         "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (the fused history "
+                                 f"shift adds 4872 B/env-step = {4872 * ENVS_PER_GPU} B per launch); the kernel is "
                                  "latency/VALU-bound (one env per lane), see DESIGN.md"},
             "reference_context": {"upstream_example_run_env_steps_per_s": 41176, "upstream_ppo_iters_per_s": 0.429,
                                   "hardware": "unspecified NVIDIA GPU, 4000 envs (BASELINE.md §1)"},

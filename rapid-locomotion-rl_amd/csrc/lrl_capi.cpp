@@ -107,6 +107,7 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
     for (int c = 0; c < 3; ++c) k->sph_pos[s][c] = m->sphere_pos[s][c];
     k->sph_rad[s] = m->sphere_radius[s];
     k->sph_link[s] = leg < 0 ? -1 : (link > 2 ? 2 : link);
+    k->sph_leg[s] = leg;
     if (leg < 0) k->base_sph_end = s + 1;
   }
   for (int l = 0; l < 4; ++l) {
@@ -210,7 +211,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   HIPCHECK(hipMemcpy(s->d_body_leg, model->body_leg, sizeof(int32_t) * LRL_MAX_BODIES, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(s->d_body_link, model->body_link, sizeof(int32_t) * LRL_MAX_BODIES, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(s->d_foot_xyz, model->foot_xyz, sizeof(float) * 12, hipMemcpyHostToDevice));
-  int lds_contacts = (4 * 45 + model->num_spheres * 13) * 64 * 4;  // leg blocks + contact rows
+  int lds_contacts = (4 * 51 + model->num_spheres * 13) * 64 * 4;  // leg blocks + contact rows
   int lds_tiles = (NO + LRL_NUM_PRIV) * 64 * 4;
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
   if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);

@@ -140,7 +140,9 @@ __device__ __forceinline__ float sv_get(const SV& s, int r) {
 // the accesses are bank-conflict free).  Field map inside a leg (LEGF floats):
 //   0..8  joint axes a_j (base frame)   9..17 joint origins o_j   18..35 K = D^-1 B^T (3x6)
 //   36..41 D^-1 (00 11 22 01 02 12)   42..44 per-joint bias / solve scratch
-#define LEGF 45  // + 42..44: joint bias C_l, then y_l = D^-1 (tau - C)_l
+//   45..47 leg joint rates at the start of the contact solve   48..50 Y = sum of D^-1 p_l over the
+//   impulses applied to this leg (lazy propagation: qd_l = qd0_l + Y_l - K_l (v_b - v_b0))
+#define LEGF 51
 #define LI(r, c) ((r) * ((r) + 1) / 2 + (c))
 
 struct Lds {
@@ -184,22 +186,38 @@ __device__ __forceinline__ void chol6(float* L) {
     }
   }
 }
-__device__ __forceinline__ void fwd6(const float* L, float* b) {
+// S^-1 = L^-T L^-1 from the Cholesky factor, packed lower (in place).  One inversion per sub-step
+// keeps every later solve a dense 6x6 multiply: short dependency chains, no divisions.
+__device__ __forceinline__ void chol_to_inverse6(float* L) {
+  float Li[21];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) Li[LI(j, j)] = 1.f / L[LI(j, j)];
+#pragma unroll
+  for (int i = 1; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = j; k < i; ++k) s += L[LI(i, k)] * Li[LI(k, j)];
+      Li[LI(i, j)] = -s * Li[LI(i, i)];
+    }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = i; k < 6; ++k) s += Li[LI(k, i)] * Li[LI(k, j)];
+      L[LI(i, j)] = s;
+    }
+}
+__device__ __forceinline__ void sym6mul(const float* S, const float* x, float* y) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    float s = b[i];
+    float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < i; ++k) s -= L[LI(i, k)] * b[k];
-    b[i] = s / L[LI(i, i)];
-  }
-}
-__device__ __forceinline__ void bwd6(const float* L, float* b) {
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    float s = b[i];
-#pragma unroll
-    for (int k = i + 1; k < 6; ++k) s -= L[LI(k, i)] * b[k];
-    b[i] = s / L[LI(i, i)];
+    for (int j = 0; j < 6; ++j) s += S[i >= j ? LI(i, j) : LI(j, i)] * x[j];
+    y[i] = s;
   }
 }
 __device__ __forceinline__ V3 sym3mul(float d0, float d1, float d2, float d3, float d4, float d5, V3 v) {
@@ -221,130 +239,124 @@ __device__ __forceinline__ void sym3inv(const float* D, float* Di) {
   Di[2] = (a * d - b * b) * id;
 }
 
-// M^-1 applied to a generalized impulse that is nonzero in the base part pb and in leg `lsel` (pl):
-//   x_b = S^-1 (pb - K_L^T pl),  x_l = -K_l x_b (+ D_L^-1 pl for l == L).  Accumulates into nu.
-__device__ __forceinline__ void apply_minv_add(const Lds& M, const float* Lc, float* pb, int lsel, V3 pl, float* nu) {
-  if (lsel >= 0) {
+// c_j = a_j x (x - o_j) for the joints carrying the point (j <= link)
+__device__ __forceinline__ void leg_dirs(const Lds& M, int lsel, int link, V3 x, V3* c) {
 #pragma unroll
-    for (int r = 0; r < 6; ++r) pb[r] -= M.Kx(lsel, 0, r) * pl.x + M.Kx(lsel, 1, r) * pl.y + M.Kx(lsel, 2, r) * pl.z;
-  }
-  fwd6(Lc, pb);
-  bwd6(Lc, pb);
-#pragma unroll
-  for (int r = 0; r < 6; ++r) nu[r] += pb[r];
-  V3 y = lsel >= 0 ? di_mul(M, lsel, pl) : v3(0.f, 0.f, 0.f);
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float kx = 0.f;
-#pragma unroll
-      for (int r = 0; r < 6; ++r) kx += M.Kx(l, j, r) * pb[r];
-      float yj = (l == lsel) ? (j == 0 ? y.x : j == 1 ? y.y : y.z) : 0.f;
-      nu[6 + 3 * l + j] += yj - kx;
-    }
-  }
+  for (int j = 0; j < 3; ++j) c[j] = (j <= link) ? cross(M.a(lsel, j), x - M.o(lsel, j)) : v3(0.f, 0.f, 0.f);
 }
 
-// point velocity (base frame) of body point x on leg lsel / link (lsel < 0: base)
-__device__ __forceinline__ V3 point_vel(const Lds& M, const float* nu, V3 x, int lsel, int link) {
-  V3 u = cross(v3(nu[0], nu[1], nu[2]), x) + v3(nu[3], nu[4], nu[5]);
-  if (lsel >= 0) {
+// current joint rates of leg L under lazy propagation
+__device__ __forceinline__ V3 leg_qd(const Lds& M, int L, const float* vb, const float* vb0) {
+  float d[6];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      float qd = 0.f;
+  for (int r = 0; r < 6; ++r) d[r] = vb[r] - vb0[r];
+  float q[3];
 #pragma unroll
-      for (int l = 0; l < 4; ++l)
-        if (l == lsel) qd = nu[6 + 3 * l + j];
-      if (j <= link) u = u + qd * cross(M.a(lsel, j), x - M.o(lsel, j));
-    }
+  for (int j = 0; j < 3; ++j) {
+    float k = 0.f;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) k += M.Kx(L, j, r) * d[r];
+    q[j] = M.leg(L, 45 + j) + M.leg(L, 48 + j) - k;
   }
-  return u;
+  return v3(q[0], q[1], q[2]);
+}
+
+// Apply a world-frame contact impulse dl (t1, t2, n) = (x, y, z) at base-frame point x:
+//   generalized impulse p = J^T (R^T dl);  dv_b = S^-1 (p_b - K_L^T p_L);  Y_L += D_L^-1 p_L
+__device__ __forceinline__ void apply_impulse(const Lds& M, const float* Si, const M3& R, V3 x, int lsel, int link,
+                                              V3 dl, float* vb) {
+  const V3 fb = mulT(R, dl);
+  const V3 tq = cross(x, fb);
+  float r[6] = {tq.x, tq.y, tq.z, fb.x, fb.y, fb.z};
+  if (lsel >= 0) {
+    V3 c[3];
+    leg_dirs(M, lsel, link, x, c);
+    const V3 pl = v3(dot(c[0], fb), dot(c[1], fb), dot(c[2], fb));
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r[k] -= M.Kx(lsel, 0, k) * pl.x + M.Kx(lsel, 1, k) * pl.y + M.Kx(lsel, 2, k) * pl.z;
+    const V3 y = di_mul(M, lsel, pl);
+    M.leg(lsel, 48) += y.x;
+    M.leg(lsel, 49) += y.y;
+    M.leg(lsel, 50) += y.z;
+  }
+  float dv[6];
+  sym6mul(Si, r, dv);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) vb[k] += dv[k];
 }
 
 // One contact sphere's 3x3 Delassus block W = G S^-1 G^T + J_l D^-1 J_l^T (n, t1, t2 rows)
-__device__ __forceinline__ void contact_setup(const Lds& M, const float* Lc, const M3& R, int s, int lsel, int link) {
-  V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
+__device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, const M3& R, int s, int lsel, int link) {
+  const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
   V3 c[3] = {v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f)};
-  if (lsel >= 0) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (j <= link) c[j] = cross(M.a(lsel, j), x - M.o(lsel, j));
-  }
-  float z[3][6];
+  if (lsel >= 0) leg_dirs(M, lsel, link, x, c);
+  float g[3][6];
   V3 h[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    V3 nd = d == 0 ? v3(R.m[6], R.m[7], R.m[8]) : d == 1 ? v3(R.m[0], R.m[1], R.m[2]) : v3(R.m[3], R.m[4], R.m[5]);
-    V3 xn = cross(x, nd);
-    float g[6] = {xn.x, xn.y, xn.z, nd.x, nd.y, nd.z};
+    const V3 nd = d == 0 ? v3(R.m[6], R.m[7], R.m[8]) : d == 1 ? v3(R.m[0], R.m[1], R.m[2]) : v3(R.m[3], R.m[4], R.m[5]);
+    const V3 xn = cross(x, nd);
+    g[d][0] = xn.x; g[d][1] = xn.y; g[d][2] = xn.z; g[d][3] = nd.x; g[d][4] = nd.y; g[d][5] = nd.z;
     h[d] = v3(dot(c[0], nd), dot(c[1], nd), dot(c[2], nd));
     if (lsel >= 0) {
 #pragma unroll
       for (int r = 0; r < 6; ++r)
-        g[r] -= M.Kx(lsel, 0, r) * h[d].x + M.Kx(lsel, 1, r) * h[d].y + M.Kx(lsel, 2, r) * h[d].z;
+        g[d][r] -= M.Kx(lsel, 0, r) * h[d].x + M.Kx(lsel, 1, r) * h[d].y + M.Kx(lsel, 2, r) * h[d].z;
     }
-    fwd6(Lc, g);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) z[d][r] = g[r];
   }
   float W[3][3];
 #pragma unroll
-  for (int d = 0; d < 3; ++d)
+  for (int e = 0; e < 3; ++e) {
+    float z[6];
+    sym6mul(Si, g[e], z);
 #pragma unroll
-    for (int e = d; e < 3; ++e) {
+    for (int d = 0; d <= e; ++d) {
       float w = 0.f;
 #pragma unroll
-      for (int r = 0; r < 6; ++r) w += z[d][r] * z[e][r];
+      for (int r = 0; r < 6; ++r) w += g[d][r] * z[r];
       if (lsel >= 0) w += dot(h[d], di_mul(M, lsel, h[e]));
       W[d][e] = w;
       W[e][d] = w;
     }
-  float id = 1.f / (W[1][1] * W[2][2] - W[1][2] * W[2][1]);
-  M.sph(s, 3) = W[0][0];
+  }
+  const float id = 1.f / (W[1][1] * W[2][2] - W[1][2] * W[2][1]);
+  M.sph(s, 3) = 1.f / W[0][0];
   M.sph(s, 4) = W[1][0];
   M.sph(s, 5) = W[2][0];
   M.sph(s, 6) = W[2][2] * id;  // (W_tt)^-1: 11, 12, 22
   M.sph(s, 7) = -W[1][2] * id;
   M.sph(s, 8) = W[1][1] * id;
-  M.sph(s, 10) = 0.f;
-  M.sph(s, 11) = 0.f;
-  M.sph(s, 12) = 0.f;
 }
 
 // One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone)
-__device__ __forceinline__ void contact_pgs(const Lds& M, const float* Lc, const M3& R, int s, int lsel, int link,
-                                            float mu, float* nu) {
-  V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
-  V3 uw = mul(R, point_vel(M, nu, x, lsel, link));  // world: (t1, t2, n) = (x, y, z)
-  float Wnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
-  float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
-  float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
-  float ln = fmaxf(ln0 - (uw.z - b) / Wnn, 0.f);
-  float dn = ln - ln0;
-  float ut1 = uw.x + Wt1n * dn, ut2 = uw.y + Wt2n * dn;
+__device__ __forceinline__ void contact_pgs(const Lds& M, const float* Si, const M3& R, int s, int lsel, int link,
+                                            float mu, float* vb, const float* vb0) {
+  const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
+  V3 u = cross(v3(vb[0], vb[1], vb[2]), x) + v3(vb[3], vb[4], vb[5]);
+  if (lsel >= 0) {
+    const V3 qd = leg_qd(M, lsel, vb, vb0);
+    V3 c[3];
+    leg_dirs(M, lsel, link, x, c);
+    u = u + qd.x * c[0] + qd.y * c[1] + qd.z * c[2];
+  }
+  const V3 uw = mul(R, u);  // world: (t1, t2, n) = (x, y, z)
+  const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
+  const float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
+  const float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
+  const float ln = fmaxf(ln0 - (uw.z - b) * iWnn, 0.f);
+  const float dn = ln - ln0;
+  const float ut1 = uw.x + Wt1n * dn, ut2 = uw.y + Wt2n * dn;
   float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
-  float lim = mu * ln, nt = sqrtf(lt1 * lt1 + lt2 * lt2);
-  if (nt > lim) {
-    float sc = nt > 0.f ? lim / nt : 0.f;
+  const float lim = mu * ln, nt2 = lt1 * lt1 + lt2 * lt2;
+  if (nt2 > lim * lim) {
+    const float sc = nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f;
     lt1 *= sc;
     lt2 *= sc;
   }
   M.sph(s, 10) = ln;
   M.sph(s, 11) = lt1;
   M.sph(s, 12) = lt2;
-  V3 fb = mulT(R, v3(lt1 - lt10, lt2 - lt20, dn));
-  V3 tq = cross(x, fb);
-  float pb[6] = {tq.x, tq.y, tq.z, fb.x, fb.y, fb.z};
-  V3 pl = v3(0.f, 0.f, 0.f);
-  if (lsel >= 0) {
-    float cj[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (j <= link) cj[j] = dot(cross(M.a(lsel, j), x - M.o(lsel, j)), fb);
-    pl = v3(cj[0], cj[1], cj[2]);
-  }
-  apply_minv_add(M, Lc, pb, lsel, pl, nu);
+  apply_impulse(M, Si, R, x, lsel, link, v3(lt1 - lt10, lt2 - lt20, dn), vb);
 }
 
 struct Body {  // per-lane env state during the step
@@ -352,19 +364,13 @@ struct Body {  // per-lane env state during the step
   float q[12], qd[12];
 };
 
-__device__ __forceinline__ int sphere_leg(const KParams* __restrict__ K, int s) {
-  int l = -1;
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (s >= K->leg_sph_begin[k] && s < K->leg_sph_end[k]) l = k;
-  return l;
-}
 
 // ------------------------------------------------------------------------------------------------
 // One physics sub-step.  Contact impulses of the sub-step stay in the LDS rows (fields 10..12).
 // ------------------------------------------------------------------------------------------------
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau, float mb, const float* Ib, V3 cb,
                         float mu, float rest, const Lds& M, uint64_t& active) {
+  const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
   const lrl_env_params& P = K->p;
   const float dt = P.sim_dt;
   const M3 R = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
@@ -401,7 +407,14 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.sph(s, 0) = x.x;
       M.sph(s, 1) = x.y;
       M.sph(s, 2) = x.z;
-      float u0 = dot(Rz, point_vel(M, nu, x, lsel, link));
+      V3 u = cross(wb, x) + vb;
+      if (lsel >= 0) {
+        V3 c[3];
+        leg_dirs(M, lsel, link, x, c);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) u = u + pick12(st.qd, 3 * lsel + j) * c[j];
+      }
+      const float u0 = dot(Rz, u);
       float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
       if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
       M.sph(s, 9) = tgt;
@@ -486,6 +499,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   Sch[LI(5, 0)] += A.h.y;  Sch[LI(5, 1)] -= A.h.x;
   Sch[LI(3, 3)] += A.m; Sch[LI(4, 4)] += A.m; Sch[LI(5, 5)] += A.m;
   chol6(Sch);
+  chol_to_inverse6(Sch);  // Sch now holds S^-1
   // free acceleration: M acc = [0; tau] - C
   {
     float pb[6] = {-Cb.a.x, -Cb.a.y, -Cb.a.z, -Cb.l.x, -Cb.l.y, -Cb.l.z};
@@ -499,10 +513,12 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.leg(l, 43) = y.y;
       M.leg(l, 44) = y.z;
     }
-    fwd6(Sch, pb);
-    bwd6(Sch, pb);
+    float xb[6];
+    sym6mul(Sch, pb, xb);
 #pragma unroll
-    for (int r = 0; r < 6; ++r) nu[r] += dt * pb[r];
+    for (int r = 0; r < 6; ++r) nu[r] += dt * xb[r];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) pb[r] = xb[r];
 #pragma unroll
     for (int l = 0; l < 4; ++l)
 #pragma unroll
@@ -513,15 +529,51 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         nu[6 + 3 * l + j] += dt * (M.leg(l, 42 + j) - kx);
       }
   }
-  // contact rows and projected Gauss-Seidel; spheres visited in model order (base, legs 0..3) and
-  // only when active in some lane of the wave
+  // contact solve.  Start state: v_b0 = free base velocity, qd0 = free joint rates (LDS), Y = 0.
+  float vb0[6], vbc[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) vb0[r] = vbc[r] = nu[r];
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      M.leg(l, 45 + j) = nu[6 + 3 * l + j];
+      M.leg(l, 48 + j) = 0.f;
+    }
+  // Delassus rows of the active spheres (only spheres active in some lane of the wave are visited)
   for (int s = 0; s < K->num_spheres; ++s)
     if (__any((int)((active >> s) & 1ull)))
-      if ((active >> s) & 1ull) contact_setup(M, Sch, R, s, sphere_leg(K, s), K->sph_link[s]);
+      if ((active >> s) & 1ull) contact_setup(M, Sch, R, s, K->sph_leg[s], K->sph_link[s]);
+  // warm start: spheres in contact in the previous sub-step keep their impulse (world frame)
+  for (int s = 0; s < K->num_spheres; ++s) {
+    const bool act = (active >> s) & 1ull, warm = act && ((prev_active >> s) & 1ull);
+    if (__any((int)act)) {
+      if (act && !warm) {
+        M.sph(s, 10) = 0.f;
+        M.sph(s, 11) = 0.f;
+        M.sph(s, 12) = 0.f;
+      }
+      if (__any((int)warm))
+        if (warm)
+          apply_impulse(M, Sch, R, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), K->sph_leg[s], K->sph_link[s],
+                        v3(M.sph(s, 11), M.sph(s, 12), M.sph(s, 10)), vbc);
+    }
+  }
+  // projected Gauss-Seidel, sphere order = model order (base, legs 0..3)
   for (int it = 0; it < P.solver_iterations; ++it)
     for (int s = 0; s < K->num_spheres; ++s)
       if (__any((int)((active >> s) & 1ull)))
-        if ((active >> s) & 1ull) contact_pgs(M, Sch, R, s, sphere_leg(K, s), K->sph_link[s], mu, nu);
+        if ((active >> s) & 1ull) contact_pgs(M, Sch, R, s, K->sph_leg[s], K->sph_link[s], mu, vbc, vb0);
+  // materialise the lazily propagated joint rates
+#pragma unroll
+  for (int r = 0; r < 6; ++r) nu[r] = vbc[r];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const V3 q = leg_qd(M, l, vbc, vb0);
+    nu[6 + 3 * l] = q.x;
+    nu[6 + 3 * l + 1] = q.y;
+    nu[6 + 3 * l + 2] = q.z;
+  }
   // semi-implicit integration
 #pragma unroll
   for (int j = 0; j < 12; ++j) {

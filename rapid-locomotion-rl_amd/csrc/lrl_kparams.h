@@ -23,6 +23,7 @@ struct KParams {
   float sph_pos[LRL_MAX_SPHERES][3];
   float sph_rad[LRL_MAX_SPHERES];
   int32_t sph_link[LRL_MAX_SPHERES];  // 0..2 dynamic link inside the leg, -1 base
+  int32_t sph_leg[LRL_MAX_SPHERES];   // 0..3, -1 base
   int32_t base_sph_end;               // spheres [0, base_sph_end) are on the base
   int32_t leg_sph_begin[LRL_NUM_LEGS], leg_sph_end[LRL_NUM_LEGS];
   int32_t body_sph_begin[LRL_MAX_BODIES], body_sph_end[LRL_MAX_BODIES];

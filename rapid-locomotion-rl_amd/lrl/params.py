@@ -151,7 +151,7 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         contact_offset=physx.contact_offset, max_depenetration_velocity=physx.max_depenetration_velocity,
         bounce_threshold_velocity=physx.bounce_threshold_velocity, ground_friction=cfg.terrain.static_friction,
         ground_restitution=cfg.terrain.restitution,
-        solver_iterations=solver_iterations or 2 * physx.num_position_iterations, baumgarte=baumgarte,
+        solver_iterations=solver_iterations or physx.num_position_iterations, baumgarte=baumgarte,
         control_type=0, action_scale=cfg.control.action_scale, hip_scale_reduction=cfg.control.hip_scale_reduction,
         clip_actions=cfg.normalization.clip_actions, p_gains=p_gains, d_gains=d_gains, default_dof_pos=default,
         torque_limits=robot["dof_effort"], soft_dof_pos_lower=soft_lo.tolist(), soft_dof_pos_upper=soft_hi.tolist(),

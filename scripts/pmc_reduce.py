@@ -1,0 +1,16 @@
+"""Reduce a rocprofv3 counter_collection.csv to per-kernel (dispatches, mean, min, max) of one counter."""
+import csv
+import sys
+from collections import defaultdict
+
+path, counter = sys.argv[1], sys.argv[2]
+vals = defaultdict(list)
+with open(path) as f:
+    for row in csv.DictReader(f):
+        if row.get("Counter_Name") != counter:
+            continue
+        vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+w = csv.writer(sys.stdout)
+w.writerow(["kernel", "counter", "dispatches", "mean", "min", "max"])
+for k, v in sorted(vals.items(), key=lambda kv: -sum(kv[1])):
+    w.writerow([k[:160], counter, len(v), sum(v) / len(v), min(v), max(v)])
