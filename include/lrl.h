@@ -25,6 +25,9 @@
  *   lrl_gae                ~ RolloutStorage.compute_returns (rollout_storage.py:76-90)
  *   lrl_policy_act         ~ PPO.act teacher path (ppo.py:62-74 -> actor_critic.py:137-147,170-173)
  *                            fused with RolloutStorage.add_transitions (rollout_storage.py:57-71)
+ *   lrl_ppo_*              ~ PPO.update (ppo.py:94-178): minibatch forward/backward of the PPO loss,
+ *                            adaptive-KL LR + clip_grad_norm_ + Adam, the adaptation-module MSE step
+ *   lrl_gemm_f32           ~ the torch.nn.Linear products those are built from (test entry point)
  *
  * Conventions: every function returns 0 on success or a negative LRL_E* code, with a message
  * available from lrl_last_error() (thread-local).  All data pointers passed to compute entry points
@@ -281,6 +284,80 @@ int32_t lrl_policy_act(const lrl_mlp_desc* encoder, const lrl_mlp_desc* actor, c
                        int32_t num_obs, int32_t num_priv, const float* eps, uint64_t seed, uint64_t counter,
                        float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
                        int32_t store_row, void* stream);
+
+/* ---------------- PPO update (ppo.py:94-178) ----------------
+ * All ActorCritic parameters live in ONE flat fp32 buffer (the nn.Module's tensors are views of it);
+ * gradients and the Adam moments (exp_avg / exp_avg_sq) are flat buffers of the same layout.  Actor and
+ * critic layers are stored pairwise adjacent ([actor W; critic W]) so each pair runs as one grouped
+ * GEMM.  Offsets are in floats, 16-B aligned. */
+typedef struct lrl_ppo_net {
+  int32_t num_obs, num_priv, num_hist, num_actions; /* 42, 18, 630, 12 */
+  int32_t enc_h0, enc_h1, latent;                   /* env_factor_encoder 18 -> 256 -> 128 -> 18 */
+  int32_t ac_h0, ac_h1, ac_h2;                      /* actor_body / critic_body hidden 512, 256, 128 */
+  int32_t ad_h0, ad_h1;                             /* adaptation_module 630 -> 256 -> 32 -> 18 */
+  int64_t w1, b1, w2, b2, w3, b3;                   /* [actor; critic] layer pairs */
+  int64_t w4a, b4a, w4c, b4c;                       /* actor / critic heads */
+  int64_t e1w, e1b, e2w, e2b, e3w, e3b;             /* env_factor_encoder */
+  int64_t d1w, d1b, d2w, d2b, d3w, d3b;             /* adaptation_module */
+  int64_t std_off;                                  /* std [num_actions] */
+  int64_t main_begin, main_end;   /* parameters of the PPO optimiser step (encoder, actor, critic, std) */
+  int64_t adapt_begin, adapt_end; /* parameters of the adaptation step */
+  int64_t kl_slot;                /* grads[kl_slot] = minibatch KL mean (all-reduced with the grads) */
+  int64_t total;                  /* buffer length */
+} lrl_ppo_net;
+
+/* One minibatch: the flattened rollout storage ([T*N, .]) and the minibatch's row indices (the int64
+ * slice of torch.randperm that mini_batch_generator uses, rollout_storage.py:103-120). */
+typedef struct lrl_ppo_batch {
+  const float *obs, *priv, *hist, *actions, *values, *returns, *logp, *adv, *mu, *sigma;
+  const int64_t* rows;
+  int32_t batch;
+} lrl_ppo_batch;
+
+typedef struct lrl_ppo_hparams { /* PPO_Args (ppo.py:15-34) + torch.optim.Adam defaults */
+  float clip_param, entropy_coef, value_loss_coef, max_grad_norm, desired_kl;
+  int32_t use_clipped_value_loss, adaptive_schedule;
+  float beta1, beta2, eps;
+} lrl_ppo_hparams;
+
+/* Device-resident control block (caller allocates, zero-initialises and sets lr). */
+typedef struct lrl_ppo_ctrl {
+  double lr;            /* PPO optimiser learning rate (adaptive-KL schedule, ppo.py:113-124) */
+  double loss_sum[3];   /* running sums of value, surrogate and adaptation losses (ppo.py:149-171) */
+  float mb[4];          /* this minibatch: value loss, surrogate loss, adaptation loss, kl */
+  float clip_scale, step_size, total_norm, pad;
+} lrl_ppo_ctrl;
+
+/* Workspace bytes for minibatches of `batch` rows. */
+int64_t lrl_ppo_workspace_bytes(const lrl_ppo_net* net, int32_t batch);
+/* Forward + backward of the PPO loss (ppo.py:98-147): writes grads[main_begin:main_end) and
+ * grads[kl_slot]; ctrl->mb[0..1] = value / surrogate loss. */
+int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float* params, float* grads,
+                                 const lrl_ppo_batch* batch, const lrl_ppo_hparams* hp, void* workspace,
+                                 lrl_ppo_ctrl* ctrl, void* stream);
+/* Adaptive LR from the KL (x grad_scale), clip_grad_norm_(max_grad_norm) over grads x grad_scale
+ * (grad_scale = 1/world after a SUM all-reduce), Adam step `step` (1-based) over the main region. */
+int32_t lrl_ppo_optimizer_step(const lrl_ppo_net* net, float* params, const float* grads, float* exp_avg,
+                               float* exp_avg_sq, int64_t step, float grad_scale, const lrl_ppo_hparams* hp,
+                               void* workspace, lrl_ppo_ctrl* ctrl, void* stream);
+/* Adaptation-module regression (ppo.py:157-171): forward/backward -> grads[adapt_begin:adapt_end),
+ * ctrl->mb[2] = MSE. */
+int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, const float* params, float* grads,
+                                            const lrl_ppo_batch* batch, void* workspace, lrl_ppo_ctrl* ctrl,
+                                            void* stream);
+/* Adam step of the adaptation optimiser (fixed lr) over the adaptation region. */
+int32_t lrl_ppo_adaptation_step(const lrl_ppo_net* net, float* params, const float* grads, float* exp_avg,
+                                float* exp_avg_sq, int64_t step, double lr, float grad_scale,
+                                const lrl_ppo_hparams* hp, lrl_ppo_ctrl* ctrl, void* stream);
+
+/* Test entry point of the GEMM the update is built from: C = op(A) op(B) with
+ * layout 0 (NT: C[m][n] = sum_k A[m][k] B[n][k]), 2 (NN: sum_k A[m][k] B[k][n]),
+ * 3 (TN: sum_k A[k][m] B[k][n], split over k, partials reduced in place);
+ * epi 0 store, 1 +bias[n], 2 elu(+bias[n]), 3 *elu'(aux[m][n]).  rows (optional) gathers A's rows
+ * (NT/NN) or B's rows (TN). */
+int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda,
+                     const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, const float* aux,
+                     int64_t ld_aux, const int64_t* rows, float* workspace, int64_t workspace_floats, void* stream);
 
 #ifdef __cplusplus
 }

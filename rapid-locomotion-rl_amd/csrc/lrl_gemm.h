@@ -1,0 +1,54 @@
+// lrl_gemm.h — LDS-tiled fp32 MFMA GEMM for the PPO minibatch update (gfx950).
+//
+// C(m, n) = sum_k A(m, k) B(k, n) on v_mfma_f32_32x32x2_f32 (exact fp32, k-ordered FMA chain), with
+// the three operand layouts an MLP's forward / backward-data / weight-gradient products need:
+//   forward       Y[b][o]  = X[b][i] W[o][i]        A k-contiguous, B k-contiguous   (+bias, ELU)
+//   backward-data dX[b][i] = dY[b][o] W[o][i]       A k-contiguous, B n-contiguous   (* ELU'(X))
+//   weight grad   dW[o][i] = dY[b][o] X[b][i]       A m-contiguous, B n-contiguous   (split over b)
+// The batch dimension of a k-contiguous A (the rows of X) and of an n-contiguous B (the rows of X in
+// the weight gradient) may be gathered through an int64 row list — the minibatch indices of
+// RolloutStorage.mini_batch_generator (rollout_storage.py:100-137) — so the minibatch is never copied.
+//
+// A workgroup (4 waves, 2x2) owns a BM x BN tile (BM, BN in {64, 128}); tiles of BK = 16 stage through
+// LDS k-major ([k][m] / [k][n]) so each MFMA operand is one conflict-free ds_read_b32 per lane; the
+// next tile is prefetched into registers while the current one is consumed (one barrier per tile).
+#pragma once
+#include <stdint.h>
+
+namespace lrl {
+
+enum GemmEpi : int {
+  EPI_STORE = 0,     // C = acc
+  EPI_BIAS = 1,      // C = acc + bias[n]
+  EPI_BIAS_ELU = 2,  // C = elu(acc + bias[n])
+  EPI_DELU = 3,      // C = acc * elu'(aux[m][n])  (aux = ELU output of the layer input: elu' = aux > 0 ? 1 : aux + 1)
+  EPI_PARTIAL = 4,   // split-k partial: C + split * part_stride (+ bias-gradient partial of A's columns)
+};
+
+struct GemmP {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  const float* aux;
+  const int64_t* a_rows;  // k-contiguous A: row list for m (nullptr = identity)
+  const int64_t* b_rows;  // n-contiguous B: row list for k (nullptr = identity)
+  float* bias_part;       // EPI_PARTIAL: [splits][groups][M] partial sums over k of A(m, k), or nullptr
+  int M, N, K;
+  int splits, kps;        // k range of split s: [s*kps, min(K, (s+1)*kps))
+  int64_t lda, ldb, ldc, ld_aux;
+  int64_t ga, gb, gc, gbias, gaux;  // per-group element offsets (blockIdx.z = group * splits + split)
+  int64_t part_stride;              // EPI_PARTIAL: elements between split slices of C ([split][group][M][N])
+};
+
+// layout: bit0 = A m-contiguous, bit1 = B n-contiguous
+enum GemmLayout : int { GEMM_NT = 0, GEMM_NN = 2, GEMM_TN = 3 };
+
+// Enqueue C = op(A, B) for `groups` independent problems of the same shape.  Returns 0 or a negative
+// lrl error code (bad shape / unsupported layout).
+int gemm_launch(const GemmP& p, int layout, int epi, int groups, void* stream);
+
+// How a weight-gradient product (reduction over K rows, `groups` problems) is split: the split count.
+int gemm_pick_splits(int M, int N, int K, int groups);
+
+}  // namespace lrl

@@ -1,0 +1,717 @@
+// lrl_ppo.hip — PPO.update (mini_gym_learn/ppo/ppo.py:94-178) for gfx950.
+//
+// Per minibatch (B rows gathered through the randperm slice, never copied):
+//   phase 1  lrl_ppo_forward_backward      encoder / actor / critic forward (grouped fp32-MFMA GEMMs,
+//            bias+ELU fused), one "head" kernel for the distribution, losses (clipped surrogate,
+//            clipped value loss, entropy), KL and the loss gradient, then the backward pass
+//            (backward-data GEMMs with ELU' fused, split-k weight-gradient GEMMs) and one segmented
+//            reduction that lands every gradient in the flat grad buffer;
+//   phase 2  lrl_ppo_optimizer_step        adaptive-KL learning rate, clip_grad_norm_, Adam — all on the
+//            device (the learning rate lives in lrl_ppo_ctrl), so a single-GPU update never syncs the host;
+//   phase 3  lrl_ppo_adaptation_forward_backward   target = encoder(priv) with the updated weights,
+//            adaptation_module(history) forward, MSE and backward;
+//   phase 4  lrl_ppo_adaptation_step       Adam on the adaptation module (Q14: the second optimiser only
+//            ever sees adaptation-module gradients).
+// Between phases 1/2 and 3/4 a multi-GPU caller all-reduces grads[main_begin:kl_slot+1) /
+// grads[adapt_begin:adapt_end) (one flat RCCL all-reduce each) and passes grad_scale = 1/world.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/lrl.h"
+#include "lrl_gemm.h"
+
+extern "C" int lrl_set_error(int code, const char* msg);
+
+namespace lrl {
+
+constexpr float LOG_SQRT_2PI = 0.91893853320467274178f;  // math.log(math.sqrt(2 * math.pi))
+constexpr int HEAD_ROWS = 64;                             // rows per head workgroup
+constexpr int HEAD_THREADS = 256;
+constexpr int HEAD_W = 128;                               // actor / critic last hidden width (ac_h2)
+constexpr int MAX_ACT = 16;
+constexpr int MAX_LAT = 32;
+
+__device__ __forceinline__ float delu(float h) { return h > 0.f ? 1.f : h + 1.f; }  // elu'(y) from h = elu(y)
+
+// ---------------------------------------------------------------------------------------------------
+// gather obs rows into the actor/critic input X = [obs | latent | 0-pad] ([B][64])
+__global__ void ppo_prep_kernel(const float* __restrict__ obs, const int64_t* __restrict__ rows, int B, int no,
+                                int xs, float* __restrict__ X) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * xs) return;
+  const int b = (int)(i / xs), c = (int)(i - (int64_t)b * xs);
+  X[i] = c < no ? obs[rows[b] * no + c] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// PPO head: mu = H3a W4a^T + b4a, v = H3c W4c^T + b4c, Normal(mu, std) log-prob / entropy, clipped
+// surrogate, clipped value loss, KL(old || new) (ppo.py:98-147, actor_critic.py:126-135); gradient of
+// loss = surrogate + c_v value - c_e entropy w.r.t. mu, v and std; dH3 = (dmu W4a | dv W4c) * elu'(H3);
+// per-workgroup partials: dW4a, db4a, dW4c, db4c, dstd, sum kl, sum surrogate, sum value loss.
+struct HeadArgs {
+  const float* h3;      // [B][2*HW]: actor | critic
+  float* dh3;           // [B][2*HW]
+  const float *w4a, *b4a, *w4c, *b4c, *stdv;
+  const float *actions, *old_mu, *old_sigma, *tv, *ret, *adv, *old_logp;
+  const int64_t* rows;
+  int B, na;
+  float clip, ent_coef, vcoef;
+  int clipped_value;
+  float* part;          // [gridDim.x][part_len]
+  int part_len;
+};
+
+// partial layout
+__host__ __device__ constexpr int hp_w4a(int) { return 0; }
+__host__ __device__ constexpr int hp_b4a(int na) { return na * HEAD_W; }
+__host__ __device__ constexpr int hp_w4c(int na) { return na * HEAD_W + na; }
+__host__ __device__ constexpr int hp_b4c(int na) { return na * HEAD_W + na + HEAD_W; }
+__host__ __device__ constexpr int hp_std(int na) { return na * HEAD_W + na + HEAD_W + 1; }
+__host__ __device__ constexpr int hp_kl(int na) { return na * HEAD_W + na + HEAD_W + 1 + na; }
+__host__ __device__ constexpr int hp_len(int na) { return hp_kl(na) + 3; }  // kl, surrogate, value
+
+__global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
+  constexpr int HP = 2 * HEAD_W + 1;  // odd pitch: row-per-lane reads conflict-free
+  __shared__ float H[HEAD_ROWS][HP];
+  __shared__ float W4[MAX_ACT + 1][HEAD_W];
+  __shared__ float MU[HEAD_ROWS][MAX_ACT + 1];
+  __shared__ float VP[HEAD_ROWS][4];
+  __shared__ float DMU[HEAD_ROWS][MAX_ACT + 1];  // dmu_j, [na] = dv
+  __shared__ float DS[HEAD_ROWS][MAX_ACT];       // per-row d loss / d std_j
+  __shared__ float SC[HEAD_ROWS][3];             // kl, surrogate, value loss per row
+  const int t = threadIdx.x, na = a.na;
+  const int r0 = blockIdx.x * HEAD_ROWS;
+  const int nrows = min(HEAD_ROWS, a.B - r0);
+  for (int i = t; i < HEAD_ROWS * 2 * HEAD_W; i += HEAD_THREADS) {
+    const int r = i / (2 * HEAD_W), c = i - r * (2 * HEAD_W);
+    H[r][c] = r < nrows ? a.h3[(int64_t)(r0 + r) * (2 * HEAD_W) + c] : 0.f;
+  }
+  for (int i = t; i < (na + 1) * HEAD_W; i += HEAD_THREADS) {
+    const int j = i / HEAD_W, k = i - j * HEAD_W;
+    W4[j][k] = j < na ? a.w4a[j * HEAD_W + k] : a.w4c[k];
+  }
+  __syncthreads();
+  // forward: thread (r, q) computes actions q, q+4, q+8, ... and a quarter of the value dot
+  {
+    const int r = t & 63, q = t >> 6;
+    for (int j = q; j < na; j += 4) {
+      float s = 0.f;
+      for (int k = 0; k < HEAD_W; ++k) s = fmaf(H[r][k], W4[j][k], s);
+      MU[r][j] = s + a.b4a[j];
+    }
+    float s = 0.f;
+    for (int k = q * (HEAD_W / 4); k < (q + 1) * (HEAD_W / 4); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
+    VP[r][q] = s;
+  }
+  __syncthreads();
+  const float invB = 1.f / (float)a.B;
+  if (t < HEAD_ROWS) {
+    const int r = t;
+    float dsig[MAX_ACT];
+    float kl = 0.f, surr_loss = 0.f, vloss = 0.f, dv = 0.f;
+    for (int j = 0; j < na; ++j) { DMU[r][j] = 0.f; dsig[j] = 0.f; }
+    if (r < nrows) {
+      const int64_t g = a.rows[r0 + r];
+      const float v = ((VP[r][0] + VP[r][1]) + (VP[r][2] + VP[r][3])) + a.b4c[0];
+      float logp = 0.f;
+      float dj[MAX_ACT];
+      for (int j = 0; j < na; ++j) {
+        const float s = a.stdv[j], mu = MU[r][j];
+        const float var = s * s;
+        const float d = a.actions[g * na + j] - mu;
+        dj[j] = d;
+        logp += -(d * d) / (2.f * var) - logf(s) - LOG_SQRT_2PI;
+        // KL(old || new), ppo.py:111-114 (inference mode)
+        const float so = a.old_sigma[g * na + j], dm = a.old_mu[g * na + j] - mu;
+        kl += logf(s / so + 1.e-5f) + (so * so + dm * dm) / (2.f * (s * s)) - 0.5f;
+      }
+      const float adv = a.adv[g];
+      const float ratio = expf(logp - a.old_logp[g]);
+      const float surr = -adv * ratio;
+      const float rc = fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip);
+      const float surr_c = -adv * rc;
+      surr_loss = fmaxf(surr, surr_c);
+      // torch.max backward: the larger side takes the gradient, ties split it in half
+      const float ga = surr > surr_c ? invB : (surr == surr_c ? 0.5f * invB : 0.f);
+      const float gb = surr_c > surr ? invB : (surr == surr_c ? 0.5f * invB : 0.f);
+      const bool in_rng = ratio >= 1.f - a.clip && ratio <= 1.f + a.clip;
+      const float dratio = -adv * ga + (in_rng ? -adv * gb : 0.f);
+      const float dlogp = dratio * ratio;
+      for (int j = 0; j < na; ++j) {
+        const float s = a.stdv[j], var = s * s, d = dj[j];
+        DMU[r][j] = dlogp * (d / var);
+        dsig[j] = dlogp * (d * d / (var * s) - 1.f / s) - a.ent_coef * invB / s;
+      }
+      // value loss (ppo.py:133-143)
+      const float tv = a.tv[g], ret = a.ret[g];
+      const float gv = a.vcoef * invB;
+      if (a.clipped_value) {
+        const float dvt = v - tv;
+        const float vc = tv + fminf(fmaxf(dvt, -a.clip), a.clip);
+        const float l1 = (v - ret) * (v - ret), l2 = (vc - ret) * (vc - ret);
+        vloss = fmaxf(l1, l2);
+        const float g1 = l1 > l2 ? gv : (l1 == l2 ? 0.5f * gv : 0.f);
+        const float g2 = l2 > l1 ? gv : (l1 == l2 ? 0.5f * gv : 0.f);
+        const bool vin = dvt >= -a.clip && dvt <= a.clip;
+        dv = g1 * 2.f * (v - ret) + (vin ? g2 * 2.f * (vc - ret) : 0.f);
+      } else {
+        vloss = (ret - v) * (ret - v);
+        dv = gv * 2.f * (v - ret);
+      }
+    }
+    DMU[r][na] = dv;
+    for (int j = 0; j < na; ++j) DS[r][j] = dsig[j];
+    SC[r][0] = kl;
+    SC[r][1] = surr_loss;
+    SC[r][2] = vloss;
+  }
+  __syncthreads();
+  // backward into H3 and the head weight-gradient partials: thread = column of [actor | critic]
+  float* P = a.part + (int64_t)blockIdx.x * a.part_len;
+  {
+    const int k = t;  // 0..255
+    const bool actor = k < HEAD_W;
+    const int kk = actor ? k : k - HEAD_W;
+    float accw[MAX_ACT];
+    for (int j = 0; j < MAX_ACT; ++j) accw[j] = 0.f;
+    float accc = 0.f;
+    for (int r = 0; r < nrows; ++r) {
+      const float h = H[r][k];
+      float g;
+      if (actor) {
+        float s = 0.f;
+        for (int j = 0; j < na; ++j) {
+          s = fmaf(DMU[r][j], W4[j][kk], s);
+          accw[j] = fmaf(DMU[r][j], h, accw[j]);
+        }
+        g = s;
+      } else {
+        g = DMU[r][na] * W4[na][kk];
+        accc = fmaf(DMU[r][na], h, accc);
+      }
+      a.dh3[(int64_t)(r0 + r) * (2 * HEAD_W) + k] = g * delu(h);
+    }
+    if (actor) {
+      for (int j = 0; j < na; ++j) P[hp_w4a(na) + j * HEAD_W + kk] = accw[j];
+    } else {
+      P[hp_w4c(na) + kk] = accc;
+    }
+  }
+  if (t < na) {
+    float sb = 0.f, ss = 0.f;
+    for (int r = 0; r < nrows; ++r) {
+      sb += DMU[r][t];
+      ss += DS[r][t];
+    }
+    P[hp_b4a(na) + t] = sb;
+    P[hp_std(na) + t] = ss;
+  } else if (t == na) {
+    float sb = 0.f;
+    for (int r = 0; r < nrows; ++r) sb += DMU[r][na];
+    P[hp_b4c(na)] = sb;
+  } else if (t >= 32 && t < 35) {
+    const int c = t - 32;
+    float s = 0.f;
+    for (int r = 0; r < nrows; ++r) s += SC[r][c];
+    P[hp_kl(na) + c] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Adaptation head: pred = HD2 W_D3^T + b, MSE against the encoder target (F.mse_loss, mean over B*L),
+// dHD2 = dpred W_D3 * elu'(HD2); partials dW_D3 [L][H], db_D3 [L], sum of squared errors.
+struct AdaptHeadArgs {
+  const float* hd2;  // [B][ldh]
+  int ldh;
+  const float* tgt;  // [B][ldt]
+  int ldt;
+  float* dhd2;       // [B][ldh]
+  const float *w, *b;
+  int B, H, L;       // hidden (32), latent (18)
+  float* part;
+  int part_len;      // L*H + L + 1
+};
+
+__global__ __launch_bounds__(HEAD_THREADS) void adapt_head_kernel(AdaptHeadArgs a) {
+  __shared__ float HS[HEAD_ROWS][MAX_LAT + 1];
+  __shared__ float DP[HEAD_ROWS][MAX_LAT + 1];
+  __shared__ float WS[MAX_LAT][MAX_LAT + 1];
+  __shared__ float ERR[HEAD_ROWS];
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.x * HEAD_ROWS;
+  const int nrows = min(HEAD_ROWS, a.B - r0);
+  for (int i = t; i < HEAD_ROWS * a.H; i += HEAD_THREADS) {
+    const int r = i / a.H, c = i - r * a.H;
+    HS[r][c] = r < nrows ? a.hd2[(int64_t)(r0 + r) * a.ldh + c] : 0.f;
+  }
+  for (int i = t; i < a.L * a.H; i += HEAD_THREADS) WS[i / a.H][i % a.H] = a.w[i];
+  __syncthreads();
+  const float scale = 2.f / ((float)a.B * (float)a.L);
+  if (t < HEAD_ROWS) {
+    const int r = t;
+    float e = 0.f;
+    for (int j = 0; j < a.L; ++j) {
+      float d = 0.f;
+      if (r < nrows) {
+        float s = 0.f;
+        for (int k = 0; k < a.H; ++k) s = fmaf(HS[r][k], WS[j][k], s);
+        const float pred = s + a.b[j];
+        d = pred - a.tgt[(int64_t)(r0 + r) * a.ldt + j];
+      }
+      e += d * d;
+      DP[r][j] = scale * d;
+    }
+    ERR[r] = e;
+  }
+  __syncthreads();
+  float* P = a.part + (int64_t)blockIdx.x * a.part_len;
+  // dHD2 (thread = (row, k) pairs)
+  for (int i = t; i < nrows * a.H; i += HEAD_THREADS) {
+    const int r = i / a.H, k = i - r * a.H;
+    float s = 0.f;
+    for (int j = 0; j < a.L; ++j) s = fmaf(DP[r][j], WS[j][k], s);
+    a.dhd2[(int64_t)(r0 + r) * a.ldh + k] = s * delu(HS[r][k]);
+  }
+  // dW_D3 partial (thread = (j, k))
+  for (int i = t; i < a.L * a.H; i += HEAD_THREADS) {
+    const int j = i / a.H, k = i - j * a.H;
+    float s = 0.f;
+    for (int r = 0; r < nrows; ++r) s = fmaf(DP[r][j], HS[r][k], s);
+    P[i] = s;
+  }
+  if (t < a.L) {
+    float s = 0.f;
+    for (int r = 0; r < nrows; ++r) s += DP[r][t];
+    P[a.L * a.H + t] = s;
+  } else if (t == 64) {
+    float s = 0.f;
+    for (int r = 0; r < nrows; ++r) s += ERR[r];
+    P[a.L * a.H + a.L] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Segmented reduction of partial slices: dst[i] = scale * sum_p src[p * stride + i] (fixed order).
+struct Seg {
+  const float* src;
+  float* dst;
+  int64_t len, stride;
+  int parts;
+  float scale;
+};
+constexpr int MAX_SEGS = 24;
+struct SegList {
+  Seg s[MAX_SEGS];
+  int n;
+};
+
+__global__ void seg_reduce_kernel(SegList L) {
+  const Seg& sg = L.s[blockIdx.y];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.len; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    const float* p = sg.src + i;
+    for (int q = 0; q < sg.parts; ++q) acc += p[(int64_t)q * sg.stride];
+    sg.dst[i] = acc * sg.scale;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// clip_grad_norm_ (torch.nn.utils.clip_grad_norm_): sum of squares partials, fp64
+constexpr int NORM_BLOCKS = 256;
+__global__ void sumsq_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = g[i];
+    s += x * x;
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// adaptive learning rate (ppo.py:110-124), clip coefficient, Adam step size, loss bookkeeping
+__global__ void ppo_finalize_kernel(const double* __restrict__ part, int nparts, const float* __restrict__ kl_slot,
+                                    float grad_scale, float max_norm, float desired_kl, int adaptive, double bc1,
+                                    float inv_B, lrl_ppo_ctrl* ctrl) {
+  __shared__ double red[64];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double tot = 0.0;
+  for (int i = 0; i < 64; ++i) tot += red[i];
+  const float total_norm = (float)sqrt(tot) * grad_scale;
+  float clip = max_norm / (total_norm + 1e-6f);
+  clip = fminf(clip, 1.f);
+  double lr = ctrl->lr;
+  const float kl = kl_slot[0] * grad_scale;
+  if (adaptive) {
+    const double k = (double)kl;
+    if (k > (double)desired_kl * 2.0) lr = fmax(1e-5, lr / 1.5);
+    else if (k < (double)desired_kl / 2.0 && k > 0.0) lr = fmin(1e-2, lr * 1.5);
+  }
+  ctrl->lr = lr;
+  ctrl->mb[3] = kl;
+  ctrl->clip_scale = clip;
+  ctrl->total_norm = total_norm;
+  ctrl->step_size = (float)(lr / bc1);
+  ctrl->loss_sum[0] += (double)ctrl->mb[0];
+  ctrl->loss_sum[1] += (double)ctrl->mb[1];
+}
+
+// torch.optim.Adam (foreach, no weight decay / amsgrad):
+//   m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2; p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float grad_scale, const lrl_ppo_ctrl* __restrict__ ctrl,
+                            float step_size_host, float one_minus_b1, float b2, float one_minus_b2, float bc2_sqrt,
+                            float eps, lrl_ppo_ctrl* acc_ctrl) {
+  const float clip = ctrl ? ctrl->clip_scale : 1.f;
+  const float step = ctrl ? ctrl->step_size : step_size_host;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * grad_scale;
+    gi = gi * clip;
+    float mi = m[i];
+    mi = mi + one_minus_b1 * (gi - mi);
+    float vi = v[i] * b2;
+    vi = vi + one_minus_b2 * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] + (-step) * (mi / denom);
+  }
+  if (acc_ctrl && blockIdx.x == 0 && threadIdx.x == 0) acc_ctrl->loss_sum[2] += (double)acc_ctrl->mb[2];
+}
+
+// ---------------------------------------------------------------------------------------------------
+// host side: workspace plan
+struct Plan {
+  int B;
+  float *xa, *he1, *he2, *h1, *h2, *h3, *dh3, *dh2, *dh1, *dlat, *dhe2, *dhe1;
+  float *tgt, *hd1, *hd2, *dhd2, *dhd1;
+  float* part;     // partial area (reused by phases 1 and 3)
+  int64_t part_floats;
+  int64_t bytes;
+};
+
+constexpr int XS = 64;      // X row pitch (obs + latent <= 64)
+constexpr int LATS = 32;    // latent-wide buffers pitch
+constexpr int HD2S = 32;    // adaptation hidden-2 pitch
+
+static int64_t tn_part_floats(int M, int N, int K, int groups) {
+  const int s = gemm_pick_splits(M, N, K, groups);
+  return (int64_t)s * groups * ((int64_t)M * N + M);
+}
+
+static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
+  Plan p;
+  p.B = B;
+  int64_t off = 0;
+  auto take = [&](int64_t floats) {
+    float* r = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += ((floats * 4 + 255) / 256) * 256;
+    return r;
+  };
+  const int64_t Bl = B;
+  p.xa = take(Bl * XS);
+  p.he1 = take(Bl * n.enc_h0);
+  p.he2 = take(Bl * n.enc_h1);
+  p.h1 = take(Bl * 2 * n.ac_h0);
+  p.h2 = take(Bl * 2 * n.ac_h1);
+  p.h3 = take(Bl * 2 * n.ac_h2);
+  p.dh3 = take(Bl * 2 * n.ac_h2);
+  p.dh2 = take(Bl * 2 * n.ac_h1);
+  p.dh1 = take(Bl * 2 * n.ac_h0);
+  p.dlat = take(Bl * LATS);
+  p.dhe2 = take(Bl * n.enc_h1);
+  p.dhe1 = take(Bl * n.enc_h0);
+  p.tgt = take(Bl * LATS);
+  p.hd1 = take(Bl * n.ad_h0);
+  p.hd2 = take(Bl * HD2S);
+  p.dhd2 = take(Bl * HD2S);
+  p.dhd1 = take(Bl * n.ad_h0);
+  const int hb = (B + HEAD_ROWS - 1) / HEAD_ROWS;
+  int64_t ph1 = tn_part_floats(n.ac_h2, n.ac_h1, B, 2) + tn_part_floats(n.ac_h1, n.ac_h0, B, 2) +
+                tn_part_floats(2 * n.ac_h0, n.num_obs + n.latent, B, 1) + tn_part_floats(n.latent, n.enc_h1, B, 1) +
+                tn_part_floats(n.enc_h1, n.enc_h0, B, 1) + tn_part_floats(n.enc_h0, n.num_priv, B, 1) +
+                (int64_t)hb * hp_len(n.num_actions) + 64 * 8;
+  int64_t ph3 = tn_part_floats(n.ad_h1, n.ad_h0, B, 1) + tn_part_floats(n.ad_h0, n.num_hist, B, 1) +
+                (int64_t)hb * (n.latent * n.ad_h1 + n.latent + 1) + 64 * 4;
+  p.part_floats = std::max(ph1, ph3);
+  p.part = take(p.part_floats);
+  p.bytes = off;
+  return p;
+}
+
+static int check_net(const lrl_ppo_net* n) {
+  if (!n) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: null net");
+  if (n->ac_h2 != HEAD_W) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: last actor/critic hidden width must be 128");
+  if (n->num_actions > MAX_ACT || n->num_actions < 1) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: num_actions > 16");
+  if (n->latent > MAX_LAT || n->ad_h1 > MAX_LAT) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: latent/adaptation widths > 32");
+  if (n->num_obs + n->latent > XS) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: obs + latent > 64");
+  return 0;
+}
+
+// one GEMM helper per layout
+struct G {
+  hipStream_t st;
+  float* part_end;  // end of the partial area: a product that would not fit is refused before launch
+  int rc = 0;
+  void nt(const float* A, int64_t lda, const int64_t* rows, const float* W, int64_t ldw, float* C, int64_t ldc,
+          const float* bias, int M, int N, int K, bool elu, int groups = 1, int64_t ga = 0, int64_t gw = 0,
+          int64_t gc = 0, int64_t gbias = 0) {
+    if (rc) return;
+    GemmP p{};
+    p.A = A; p.lda = lda; p.a_rows = rows; p.B = W; p.ldb = ldw; p.C = C; p.ldc = ldc; p.bias = bias;
+    p.M = M; p.N = N; p.K = K; p.splits = 1;
+    p.ga = ga; p.gb = gw; p.gc = gc; p.gbias = gbias;
+    rc = gemm_launch(p, GEMM_NT, elu ? EPI_BIAS_ELU : EPI_BIAS, groups, st);
+  }
+  // dX = dY W (* elu'(aux) if aux)
+  void nn(const float* dY, int64_t ldy, const float* W, int64_t ldw, float* dX, int64_t ldx, const float* aux,
+          int64_t ldaux, int M, int N, int K, int groups = 1, int64_t gy = 0, int64_t gw = 0, int64_t gx = 0,
+          int64_t gaux = 0) {
+    if (rc) return;
+    GemmP p{};
+    p.A = dY; p.lda = ldy; p.B = W; p.ldb = ldw; p.C = dX; p.ldc = ldx; p.aux = aux; p.ld_aux = ldaux;
+    p.M = M; p.N = N; p.K = K; p.splits = 1;
+    p.ga = gy; p.gb = gw; p.gc = gx; p.gaux = gaux;
+    rc = gemm_launch(p, GEMM_NN, aux ? EPI_DELU : EPI_STORE, groups, st);
+  }
+  // partial dW[o][i] = sum_b dY[b][o] X[rows(b)][i]; returns the segments (weights then biases)
+  void tn(const float* dY, int64_t ldy, const float* X, int64_t ldx, const int64_t* rows, int M, int N, int K,
+          int groups, int64_t gy, int64_t gx, float*& part, float* dw, float* db, SegList& L) {
+    if (rc) return;
+    const int splits = gemm_pick_splits(M, N, K, groups);
+    if (part + (int64_t)splits * groups * ((int64_t)M * N + M) > part_end) { rc = LRL_E_INVALID; return; }
+    GemmP p{};
+    p.A = dY; p.lda = ldy; p.B = X; p.ldb = ldx; p.b_rows = rows;
+    p.M = M; p.N = N; p.K = K; p.splits = splits; p.kps = (K + splits - 1) / splits;
+    p.ga = gy; p.gb = gx; p.gc = (int64_t)M * N; p.ldc = N;
+    p.part_stride = (int64_t)groups * M * N;
+    p.C = part;
+    p.bias_part = part + (int64_t)splits * groups * M * N;
+    rc = gemm_launch(p, GEMM_TN, EPI_PARTIAL, groups, st);
+    if (rc) return;
+    if (L.n + 2 > MAX_SEGS) { rc = LRL_E_INVALID; return; }
+    L.s[L.n++] = Seg{part, dw, (int64_t)groups * M * N, (int64_t)groups * M * N, splits, 1.f};
+    L.s[L.n++] = Seg{p.bias_part, db, (int64_t)groups * M, (int64_t)groups * M, splits, 1.f};
+    part = p.bias_part + (int64_t)splits * groups * M;
+    part = reinterpret_cast<float*>(((reinterpret_cast<uintptr_t>(part) + 255) / 256) * 256);
+  }
+};
+
+static void launch_seg(const SegList& L, hipStream_t st) {
+  int64_t mx = 1;
+  for (int i = 0; i < L.n; ++i) mx = std::max(mx, L.s[i].len);
+  const int bx = (int)std::min<int64_t>((mx + 255) / 256, 1024);
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3(bx, L.n), dim3(256), 0, st, L);
+}
+
+}  // namespace lrl
+
+using namespace lrl;
+
+extern "C" int64_t lrl_ppo_workspace_bytes(const lrl_ppo_net* net, int32_t batch) {
+  if (check_net(net) || batch <= 0) return -1;
+  return make_plan(*net, batch, nullptr).bytes;
+}
+
+extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float* params, float* grads,
+                                            const lrl_ppo_batch* bt, const lrl_ppo_hparams* hp, void* workspace,
+                                            lrl_ppo_ctrl* ctrl, void* stream) {
+  if (int rc = check_net(net)) return rc;
+  if (!bt || !hp || !params || !grads || !workspace || !ctrl || bt->batch <= 0)
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_forward_backward: null argument");
+  const lrl_ppo_net& n = *net;
+  const int B = bt->batch;
+  Plan P = make_plan(n, B, static_cast<char*>(workspace));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  G g{st, P.part + P.part_floats};
+  const float* w = params;
+  const int nx = n.num_obs + n.latent;
+  // ---- forward ----
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)B * XS + 255) / 256)), dim3(256), 0, st, bt->obs,
+                     bt->rows, B, n.num_obs, XS, P.xa);
+  g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
+  g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
+  g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.xa + n.num_obs, XS, w + n.e3b, B, n.latent, n.enc_h1, false);
+  g.nt(P.xa, XS, nullptr, w + n.w1, nx, P.h1, 2 * n.ac_h0, w + n.b1, B, 2 * n.ac_h0, nx, true);
+  g.nt(P.h1, 2 * n.ac_h0, nullptr, w + n.w2, n.ac_h0, P.h2, 2 * n.ac_h1, w + n.b2, B, n.ac_h1, n.ac_h0, true, 2,
+       n.ac_h0, (int64_t)n.ac_h1 * n.ac_h0, n.ac_h1, n.ac_h1);
+  g.nt(P.h2, 2 * n.ac_h1, nullptr, w + n.w3, n.ac_h1, P.h3, 2 * n.ac_h2, w + n.b3, B, n.ac_h2, n.ac_h1, true, 2,
+       n.ac_h1, (int64_t)n.ac_h2 * n.ac_h1, n.ac_h2, n.ac_h2);
+  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_forward_backward: forward GEMM launch failed");
+  // ---- head ----
+  SegList L{};
+  float* part = P.part;
+  const int hb = (B + HEAD_ROWS - 1) / HEAD_ROWS;
+  const int na = n.num_actions;
+  HeadArgs ha{};
+  ha.h3 = P.h3; ha.dh3 = P.dh3;
+  ha.w4a = w + n.w4a; ha.b4a = w + n.b4a; ha.w4c = w + n.w4c; ha.b4c = w + n.b4c; ha.stdv = w + n.std_off;
+  ha.actions = bt->actions; ha.old_mu = bt->mu; ha.old_sigma = bt->sigma; ha.tv = bt->values; ha.ret = bt->returns;
+  ha.adv = bt->adv; ha.old_logp = bt->logp; ha.rows = bt->rows;
+  ha.B = B; ha.na = na; ha.clip = hp->clip_param; ha.ent_coef = hp->entropy_coef; ha.vcoef = hp->value_loss_coef;
+  ha.clipped_value = hp->use_clipped_value_loss;
+  ha.part = part; ha.part_len = hp_len(na);
+  hipLaunchKernelGGL(ppo_head_kernel, dim3(hb), dim3(HEAD_THREADS), 0, st, ha);
+  {
+    const int64_t pl = hp_len(na);
+    const float invB = 1.f / (float)B;
+    L.s[L.n++] = Seg{part + hp_w4a(na), grads + n.w4a, (int64_t)na * HEAD_W, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + hp_b4a(na), grads + n.b4a, na, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + hp_w4c(na), grads + n.w4c, HEAD_W, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + hp_b4c(na), grads + n.b4c, 1, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + hp_std(na), grads + n.std_off, na, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + hp_kl(na), grads + n.kl_slot, 1, pl, hb, invB};
+    L.s[L.n++] = Seg{part + hp_kl(na) + 1, &ctrl->mb[1], 1, pl, hb, invB};
+    L.s[L.n++] = Seg{part + hp_kl(na) + 2, &ctrl->mb[0], 1, pl, hb, invB};
+    part += ((hb * pl + 63) / 64) * 64;
+  }
+  // ---- backward ----
+  const int h0 = n.ac_h0, h1 = n.ac_h1, h2 = n.ac_h2;
+  g.tn(P.dh3, 2 * h2, P.h2, 2 * h1, nullptr, h2, h1, B, 2, h2, h1, part, grads + n.w3, grads + n.b3, L);
+  g.nn(P.dh3, 2 * h2, w + n.w3, h1, P.dh2, 2 * h1, P.h2, 2 * h1, B, h1, h2, 2, h2, (int64_t)h2 * h1, h1, h1);
+  g.tn(P.dh2, 2 * h1, P.h1, 2 * h0, nullptr, h1, h0, B, 2, h1, h0, part, grads + n.w2, grads + n.b2, L);
+  g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
+  g.tn(P.dh1, 2 * h0, P.xa, XS, nullptr, 2 * h0, nx, B, 1, 0, 0, part, grads + n.w1, grads + n.b1, L);
+  // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
+  g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
+  g.tn(P.dlat, LATS, P.he2, n.enc_h1, nullptr, n.latent, n.enc_h1, B, 1, 0, 0, part, grads + n.e3w, grads + n.e3b, L);
+  g.nn(P.dlat, LATS, w + n.e3w, n.enc_h1, P.dhe2, n.enc_h1, P.he2, n.enc_h1, B, n.enc_h1, n.latent);
+  g.tn(P.dhe2, n.enc_h1, P.he1, n.enc_h0, nullptr, n.enc_h1, n.enc_h0, B, 1, 0, 0, part, grads + n.e2w, grads + n.e2b, L);
+  g.nn(P.dhe2, n.enc_h1, w + n.e2w, n.enc_h0, P.dhe1, n.enc_h0, P.he1, n.enc_h0, B, n.enc_h0, n.enc_h1);
+  g.tn(P.dhe1, n.enc_h0, bt->priv, n.num_priv, bt->rows, n.enc_h0, n.num_priv, B, 1, 0, 0, part, grads + n.e1w,
+       grads + n.e1b, L);
+  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_forward_backward: backward GEMM launch failed");
+  launch_seg(L, st);
+  return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_forward_backward: launch failed");
+}
+
+extern "C" int32_t lrl_ppo_optimizer_step(const lrl_ppo_net* net, float* params, const float* grads, float* exp_avg,
+                                          float* exp_avg_sq, int64_t step, float grad_scale,
+                                          const lrl_ppo_hparams* hp, void* workspace, lrl_ppo_ctrl* ctrl,
+                                          void* stream) {
+  if (int rc = check_net(net)) return rc;
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !hp || !workspace || !ctrl || step < 1)
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_optimizer_step: bad argument");
+  const lrl_ppo_net& n = *net;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // norm partials: the first 2 KB of the workspace (phase-1 scratch, dead once its reduction ran)
+  double* norm_part = static_cast<double*>(workspace);
+  const int64_t len = n.main_end - n.main_begin;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(NORM_BLOCKS), dim3(256), 0, st, grads + n.main_begin, len, norm_part);
+  const double bc1 = 1.0 - pow((double)hp->beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)hp->beta2, (double)step);
+  hipLaunchKernelGGL(ppo_finalize_kernel, dim3(1), dim3(64), 0, st, norm_part, NORM_BLOCKS,
+                     grads + n.kl_slot, grad_scale, hp->max_grad_norm, hp->desired_kl, hp->adaptive_schedule, bc1,
+                     0.f, ctrl);
+  const int blocks = (int)std::min<int64_t>((len + 255) / 256, 2048);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, params + n.main_begin, grads + n.main_begin,
+                     exp_avg + n.main_begin, exp_avg_sq + n.main_begin, len, grad_scale, ctrl, 0.f,
+                     (float)(1.0 - (double)hp->beta1), hp->beta2, (float)(1.0 - (double)hp->beta2), (float)sqrt(bc2),
+                     hp->eps, (lrl_ppo_ctrl*)nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_optimizer_step: launch failed");
+}
+
+extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, const float* params, float* grads,
+                                                       const lrl_ppo_batch* bt, void* workspace, lrl_ppo_ctrl* ctrl,
+                                                       void* stream) {
+  if (int rc = check_net(net)) return rc;
+  if (!bt || !params || !grads || !workspace || !ctrl || bt->batch <= 0)
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_adaptation_forward_backward: null argument");
+  const lrl_ppo_net& n = *net;
+  const int B = bt->batch;
+  Plan P = make_plan(n, B, static_cast<char*>(workspace));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  G g{st, P.part + P.part_floats};
+  const float* w = params;
+  // target = env_factor_encoder(priv) with the just-updated weights (torch.no_grad, ppo.py:159-160)
+  g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
+  g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
+  g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.tgt, LATS, w + n.e3b, B, n.latent, n.enc_h1, false);
+  // prediction = adaptation_module(obs_history)
+  g.nt(bt->hist, n.num_hist, bt->rows, w + n.d1w, n.num_hist, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, n.num_hist, true);
+  g.nt(P.hd1, n.ad_h0, nullptr, w + n.d2w, n.ad_h0, P.hd2, HD2S, w + n.d2b, B, n.ad_h1, n.ad_h0, true);
+  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_adaptation: forward GEMM launch failed");
+  SegList L{};
+  float* part = P.part;
+  const int hb = (B + HEAD_ROWS - 1) / HEAD_ROWS;
+  AdaptHeadArgs aa{};
+  aa.hd2 = P.hd2; aa.ldh = HD2S; aa.tgt = P.tgt; aa.ldt = LATS; aa.dhd2 = P.dhd2; aa.w = w + n.d3w; aa.b = w + n.d3b;
+  aa.B = B; aa.H = n.ad_h1; aa.L = n.latent; aa.part = part; aa.part_len = n.latent * n.ad_h1 + n.latent + 1;
+  hipLaunchKernelGGL(adapt_head_kernel, dim3(hb), dim3(HEAD_THREADS), 0, st, aa);
+  {
+    const int64_t pl = aa.part_len;
+    L.s[L.n++] = Seg{part, grads + n.d3w, (int64_t)n.latent * n.ad_h1, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + n.latent * n.ad_h1, grads + n.d3b, n.latent, pl, hb, 1.f};
+    L.s[L.n++] = Seg{part + n.latent * n.ad_h1 + n.latent, &ctrl->mb[2], 1, pl, hb,
+                     1.f / ((float)B * (float)n.latent)};
+    part += ((hb * pl + 63) / 64) * 64;
+  }
+  g.tn(P.dhd2, HD2S, P.hd1, n.ad_h0, nullptr, n.ad_h1, n.ad_h0, B, 1, 0, 0, part, grads + n.d2w, grads + n.d2b, L);
+  g.nn(P.dhd2, HD2S, w + n.d2w, n.ad_h0, P.dhd1, n.ad_h0, P.hd1, n.ad_h0, B, n.ad_h0, n.ad_h1);
+  g.tn(P.dhd1, n.ad_h0, bt->hist, n.num_hist, bt->rows, n.ad_h0, n.num_hist, B, 1, 0, 0, part, grads + n.d1w,
+       grads + n.d1b, L);
+  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_adaptation: backward GEMM launch failed");
+  launch_seg(L, st);
+  return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_adaptation: launch failed");
+}
+
+extern "C" int32_t lrl_ppo_adaptation_step(const lrl_ppo_net* net, float* params, const float* grads, float* exp_avg,
+                                           float* exp_avg_sq, int64_t step, double lr, float grad_scale,
+                                           const lrl_ppo_hparams* hp, lrl_ppo_ctrl* ctrl, void* stream) {
+  if (int rc = check_net(net)) return rc;
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !hp || step < 1)
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_adaptation_step: bad argument");
+  const lrl_ppo_net& n = *net;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const double bc1 = 1.0 - pow((double)hp->beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)hp->beta2, (double)step);
+  const int64_t len = n.adapt_end - n.adapt_begin;
+  const int blocks = (int)std::min<int64_t>((len + 255) / 256, 2048);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, params + n.adapt_begin, grads + n.adapt_begin,
+                     exp_avg + n.adapt_begin, exp_avg_sq + n.adapt_begin, len, grad_scale,
+                     (const lrl_ppo_ctrl*)nullptr, (float)(lr / bc1), (float)(1.0 - (double)hp->beta1), hp->beta2,
+                     (float)(1.0 - (double)hp->beta2), (float)sqrt(bc2), hp->eps, ctrl);
+  return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_adaptation_step: launch failed");
+}
+
+// ---- GEMM test entry point ----
+extern "C" int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t N, int32_t K, const float* A,
+                                int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias,
+                                const float* aux, int64_t ld_aux, const int64_t* rows, float* workspace,
+                                int64_t workspace_floats, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  GemmP p{};
+  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.C = C; p.ldc = ldc; p.bias = bias; p.aux = aux; p.ld_aux = ld_aux;
+  p.M = M; p.N = N; p.K = K; p.splits = 1;
+  if (layout == GEMM_TN) {
+    // split-k into the workspace, then reduce into C (C must be [M][N] contiguous: ldc == N)
+    if (ldc != N) return lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: TN needs ldc == N");
+    const int splits = gemm_pick_splits(M, N, K, 1);
+    if ((int64_t)splits * ((int64_t)M * N + M) > workspace_floats)
+      return lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: workspace too small");
+    p.b_rows = rows; p.splits = splits; p.kps = (K + splits - 1) / splits;
+    p.C = workspace; p.gc = (int64_t)M * N; p.part_stride = (int64_t)M * N;
+    p.bias_part = workspace + (int64_t)splits * M * N;
+    int rc = gemm_launch(p, GEMM_TN, EPI_PARTIAL, 1, st);
+    if (rc) return lrl_set_error(rc, "lrl_gemm_f32: launch failed");
+    SegList L{};
+    L.s[L.n++] = Seg{workspace, C, (int64_t)M * N, (int64_t)M * N, splits, 1.f};
+    if (bias) L.s[L.n++] = Seg{p.bias_part, const_cast<float*>(bias), M, M, splits, 1.f};  // bias = db output
+    launch_seg(L, st);
+    return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_gemm_f32: launch failed");
+  }
+  p.a_rows = rows;
+  int rc = gemm_launch(p, layout, epi, 1, st);
+  return rc ? lrl_set_error(rc, "lrl_gemm_f32: bad layout/epilogue or launch failure") : 0;
+}

@@ -84,6 +84,31 @@ class LrlRolloutStore(C.Structure):
                 ("hist_dim", i32)]
 
 
+i64 = C.c_int64
+
+
+class LrlPpoNet(C.Structure):
+    _fields_ = [(k, i32) for k in ("num_obs", "num_priv", "num_hist", "num_actions", "enc_h0", "enc_h1", "latent",
+                                    "ac_h0", "ac_h1", "ac_h2", "ad_h0", "ad_h1")] + \
+               [(k, i64) for k in ("w1", "b1", "w2", "b2", "w3", "b3", "w4a", "b4a", "w4c", "b4c", "e1w", "e1b", "e2w",
+                                    "e2b", "e3w", "e3b", "d1w", "d1b", "d2w", "d2b", "d3w", "d3b", "std_off",
+                                    "main_begin", "main_end", "adapt_begin", "adapt_end", "kl_slot", "total")]
+
+
+class LrlPpoBatch(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("obs", "priv", "hist", "actions", "values", "returns", "logp", "adv", "mu",
+                                          "sigma", "rows")] + [("batch", i32)]
+
+
+class LrlPpoHparams(C.Structure):
+    _fields_ = [("clip_param", f32), ("entropy_coef", f32), ("value_loss_coef", f32), ("max_grad_norm", f32),
+                ("desired_kl", f32), ("use_clipped_value_loss", i32), ("adaptive_schedule", i32), ("beta1", f32),
+                ("beta2", f32), ("eps", f32)]
+
+
+PPO_CTRL_BYTES = 64  # sizeof(lrl_ppo_ctrl): double lr, double loss_sum[3], float mb[4], float x4
+
+
 def fill(struct, **kw):
     """Assign python values (scalars / nested lists) into a ctypes struct."""
     for k, v in kw.items():
@@ -118,8 +143,11 @@ def lib():
                      "lrl_sim_set_root_state_indexed", "lrl_sim_set_dof_state_indexed", "lrl_sim_inject_uniforms",
                      "lrl_sim_refresh_rigid_body_state", "lrl_sim_shift_history", "lrl_sim_randomize", "lrl_gae",
                      "lrl_policy_act", "lrl_abi_version", "lrl_device_count", "lrl_gae_partial", "lrl_adv_normalize",
-                     "lrl_sim_reset_idx_ex", "lrl_sim_set_step_counter"]:
+                     "lrl_sim_reset_idx_ex", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
+                     "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
+                     "lrl_gemm_f32"]:
             getattr(L, name).restype = C.c_int32
+        L.lrl_ppo_workspace_bytes.restype = C.c_int64
         _lib = L
     return _lib
 

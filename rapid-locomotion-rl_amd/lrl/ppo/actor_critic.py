@@ -127,6 +127,73 @@ class ActorCritic(nn.Module):
         latent = self.env_factor_encoder(privileged_observations)
         return self.critic_body(torch.cat((critic_observations, latent), dim=-1))
 
+    # ---- flat parameter buffer (lrl_ppo_net layout) ----
+    def flatten_parameters(self):
+        """Move every parameter into ONE flat fp32 buffer on its current device (the tensors become views,
+        so state_dict / load_state_dict / the optimiser see the same storage).  Layout: the PPO step's
+        parameters [actor/critic layer pairs adjacent, heads, encoder, std], one KL slot, then the
+        adaptation module; returns the lrl_ppo_net descriptor (offsets in floats)."""
+        net = getattr(self, "_net", None)
+        if net is not None and self.std.data_ptr() == self._flat.data_ptr() + 4 * net.std_off:
+            return net
+        A = [m for m in self.actor_body if isinstance(m, nn.Linear)]
+        Cb = [m for m in self.critic_body if isinstance(m, nn.Linear)]
+        E = [m for m in self.env_factor_encoder if isinstance(m, nn.Linear)]
+        D = [m for m in self.adaptation_module if isinstance(m, nn.Linear)]
+        if len(A) != 4 or len(Cb) != 4 or len(E) != 3 or len(D) != 3:
+            raise ValueError("lrl_ppo expects 4-layer actor/critic and 3-layer encoder/adaptation MLPs")
+        if not isinstance(self.actor_body[1], nn.ELU):
+            raise ValueError("lrl_ppo implements the ELU activation only")
+        net = _abi.LrlPpoNet()
+        order, off = [], 0
+
+        def put(name, *tensors, align=64):
+            nonlocal off
+            off = (off + align - 1) // align * align
+            start = off
+            for t in tensors:
+                order.append((t, off))
+                off += t.numel()
+            if name:
+                setattr(net, name, start)
+            return start
+
+        net.main_begin = 0
+        for i, nm in enumerate(("1", "2", "3")):
+            put("w" + nm, A[i].weight, Cb[i].weight)
+            put("b" + nm, A[i].bias, Cb[i].bias)
+        put("w4a", A[3].weight); put("b4a", A[3].bias); put("w4c", Cb[3].weight); put("b4c", Cb[3].bias)
+        put("e1w", E[0].weight); put("e1b", E[0].bias); put("e2w", E[1].weight); put("e2b", E[1].bias)
+        put("e3w", E[2].weight); put("e3b", E[2].bias)
+        put("std_off", self.std)
+        net.main_end = off
+        net.kl_slot = off
+        off += 1
+        off = (off + 63) // 64 * 64
+        net.adapt_begin = off
+        put("d1w", D[0].weight); put("d1b", D[0].bias); put("d2w", D[1].weight); put("d2b", D[1].bias)
+        put("d3w", D[2].weight); put("d3b", D[2].bias)
+        net.adapt_end = off
+        net.total = (off + 63) // 64 * 64
+        dev = self.std.device
+        flat = torch.zeros(net.total, device=dev)
+        with torch.no_grad():
+            for t, o in order:
+                flat[o:o + t.numel()].copy_(t.detach().reshape(-1))
+            for t, o in order:
+                t.data = flat[o:o + t.numel()].view_as(t)
+        net.num_obs, net.num_priv = self.num_obs, self.num_privileged_obs
+        net.num_hist, net.num_actions = D[0].in_features, self.num_actions
+        net.enc_h0, net.enc_h1, net.latent = E[0].out_features, E[1].out_features, E[2].out_features
+        net.ac_h0, net.ac_h1, net.ac_h2 = A[0].out_features, A[1].out_features, A[2].out_features
+        net.ad_h0, net.ad_h1 = D[0].out_features, D[1].out_features
+        if A[0].in_features != self.num_obs + net.latent or [m.out_features for m in Cb[:3]] != \
+                [net.ac_h0, net.ac_h1, net.ac_h2]:
+            raise ValueError("actor and critic must share hidden sizes and take [obs, latent]")
+        self._flat, self._net = flat, net
+        self._descs = None
+        return net
+
     # ---- fused HIP rollout path ----
     def _hip_descs(self):
         ptrs = tuple(p.data_ptr() for p in self.parameters())

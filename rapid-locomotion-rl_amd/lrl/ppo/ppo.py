@@ -4,15 +4,24 @@ Rollout: ``act`` is one fused HIP launch (encoder + actor + critic + Normal samp
 storage write); GAE is the HIP kernel of RolloutStorage.compute_returns.  Update: the reference's
 algorithm step for step — adaptive-KL learning rate, clipped surrogate, clipped value loss,
 entropy bonus, grad-norm clip 1.0, Adam; then the adaptation-module regression with a second Adam
-over all parameters (Q14) — on the same parameters with torch autograd.  With
-``torch.distributed`` initialised, gradients are averaged with one flat all-reduce per optimiser
-step and the KL mean / advantage statistics are all-reduced so every rank takes identical steps.
+(Q14: it only ever sees adaptation-module gradients).
+
+On the GPU (``fused``) the update runs natively (``lrl_ppo_*`` in liblrl.so, csrc/lrl_ppo.hip):
+parameters, gradients and Adam moments are flat device buffers, each minibatch is four launch
+sequences (PPO forward/backward, adaptive LR + clip + Adam, adaptation forward/backward, Adam) and
+the learning rate stays on the device, so a single-GPU update synchronises with the host once, at
+its end.  With ``torch.distributed`` initialised, the flat gradient (+ the KL mean riding in the same
+buffer) is all-reduced once per optimiser step and the advantage statistics once per iteration, so
+every rank takes identical steps.  ``fused=False`` keeps the torch-autograd restatement (CPU tests).
 """
+import ctypes as C
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import _abi
 from .actor_critic import ActorCritic
 from .rollout_storage import RolloutStorage
 
@@ -56,6 +65,11 @@ class PPO:
         self._act_counter = 0
         self._store = None
         self.grad_allreduce = _world() > 1
+        self._native = None  # flat grads / Adam moments / ctrl / workspace of the native update
+        self.record_lr = False  # native path: keep the per-minibatch learning rates (self.lr_trace)
+        self.lr_trace = []
+        if self.fused:
+            self.actor_critic.flatten_parameters()
 
     def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, privileged_obs_shape, obs_history_shape,
                      action_shape):
@@ -129,7 +143,103 @@ class PPO:
             g.copy_(flat[off:off + n].view_as(g))
             off += n
 
+    # ---- native update (csrc/lrl_ppo.hip) ----
+    def _native_state(self, batch):
+        ac = self.actor_critic
+        net = ac.flatten_parameters()
+        st = self._native
+        if st is None or st["net_ptr"] != ac._flat.data_ptr():
+            dev = ac._flat.device
+            st = dict(net=net, net_ptr=ac._flat.data_ptr(), grads=torch.zeros(net.total, device=dev),
+                      exp_avg=torch.zeros(net.total, device=dev), exp_avg_sq=torch.zeros(net.total, device=dev),
+                      ctrl=torch.zeros(_abi.PPO_CTRL_BYTES // 8, dtype=torch.float64, device=dev),
+                      steps=[0, 0], ws=None, ws_batch=0)
+            hp = _abi.LrlPpoHparams()
+            _abi.fill(hp, clip_param=PPO_Args.clip_param, entropy_coef=PPO_Args.entropy_coef,
+                      value_loss_coef=PPO_Args.value_loss_coef, max_grad_norm=PPO_Args.max_grad_norm,
+                      desired_kl=PPO_Args.desired_kl if PPO_Args.desired_kl is not None else 0.0,
+                      use_clipped_value_loss=int(PPO_Args.use_clipped_value_loss),
+                      adaptive_schedule=int(PPO_Args.desired_kl is not None and PPO_Args.schedule == "adaptive"),
+                      beta1=0.9, beta2=0.999, eps=1e-8)
+            st["hp"] = hp
+            self._native = st
+        if st["ws_batch"] != batch:
+            nbytes = _abi.lib().lrl_ppo_workspace_bytes(C.byref(net), C.c_int32(batch))
+            if nbytes < 0:
+                raise RuntimeError("lrl_ppo_workspace_bytes rejected the network")
+            st["ws"] = torch.empty(nbytes, dtype=torch.uint8, device=ac._flat.device)
+            st["ws_batch"] = batch
+        return st
+
+    def _update_native(self):
+        s = self.storage
+        T, N = s.num_transitions_per_env, s.num_envs
+        nmb = PPO_Args.num_mini_batches
+        mb = (T * N) // nmb
+        st = self._native_state(mb)
+        net, hp = st["net"], st["hp"]
+        world = _world()
+        L = _abi.lib()
+        ptr = lambda t: C.c_void_p(t.data_ptr())
+        stream = C.c_void_p(torch.cuda.current_stream(st["grads"].device).cuda_stream)
+        indices = torch.randperm(nmb * mb, requires_grad=False, device=self.device)
+        trace = []
+        flat = lambda t: t.flatten(0, 1)
+        bufs = dict(obs=flat(s.observations), priv=flat(s.privileged_observations),
+                    hist=flat(s.observation_histories), actions=flat(s.actions), values=flat(s.values),
+                    returns=flat(s.returns), logp=flat(s.actions_log_prob), adv=flat(s.advantages), mu=flat(s.mu),
+                    sigma=flat(s.sigma))
+        for v in bufs.values():
+            assert v.is_contiguous() and v.dtype == torch.float32
+        batch = _abi.LrlPpoBatch()
+        for k, v in bufs.items():
+            setattr(batch, k, v.data_ptr())
+        batch.batch = mb
+        ctrl = st["ctrl"]
+        ctrl[0] = self.learning_rate
+        ctrl[1:4] = 0.0
+        params, grads, m, v, ws = self.actor_critic._flat, st["grads"], st["exp_avg"], st["exp_avg_sq"], st["ws"]
+        main = grads[net.main_begin:net.kl_slot + 1]
+        adapt = grads[net.adapt_begin:net.adapt_end]
+        scale = 1.0 / world
+        for epoch in range(PPO_Args.num_learning_epochs):
+            for i in range(nmb):
+                rows = indices[i * mb:(i + 1) * mb]
+                batch.rows = rows.data_ptr()
+                _abi.check(L.lrl_ppo_forward_backward(C.byref(net), ptr(params), ptr(grads), C.byref(batch),
+                                                      C.byref(hp), ptr(ws), ptr(ctrl), stream))
+                if world > 1:
+                    dist.all_reduce(main)
+                st["steps"][0] += 1
+                _abi.check(L.lrl_ppo_optimizer_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
+                                                    C.c_int64(st["steps"][0]), C.c_float(scale), C.byref(hp),
+                                                    ptr(ws), ptr(ctrl), stream))
+                if self.record_lr:
+                    trace.append(ctrl[0].clone())
+                for _ in range(PPO_Args.num_adaptation_module_substeps):
+                    _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), ptr(params), ptr(grads),
+                                                                     C.byref(batch), ptr(ws), ptr(ctrl), stream))
+                    if world > 1:
+                        dist.all_reduce(adapt)
+                    st["steps"][1] += 1
+                    _abi.check(L.lrl_ppo_adaptation_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
+                                                         C.c_int64(st["steps"][1]),
+                                                         C.c_double(PPO_Args.adaptation_module_learning_rate),
+                                                         C.c_float(scale), C.byref(hp), ptr(ctrl), stream))
+        num_updates = PPO_Args.num_learning_epochs * nmb
+        lr, vsum, ssum, asum = ctrl[:4].tolist()
+        if self.record_lr:
+            self.lr_trace = torch.stack(trace).tolist()
+        self.learning_rate = lr
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+        self.storage.clear()
+        return (vsum / num_updates, ssum / num_updates,
+                asum / (num_updates * PPO_Args.num_adaptation_module_substeps))
+
     def update(self):
+        if self.fused:
+            return self._update_native()
         mean_value_loss = torch.zeros((), device=self.device)
         mean_surrogate_loss = torch.zeros((), device=self.device)
         mean_adaptation_module_loss = torch.zeros((), device=self.device)

@@ -34,7 +34,9 @@ def test_struct_layout_matches_header():
 #include <stddef.h>
 #include "lrl.h"
 int main(){printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_model), sizeof(lrl_env_params), sizeof(lrl_tensor),
- offsetof(lrl_env_params, noise_vec), offsetof(lrl_env_params, max_episode_length), sizeof(lrl_mlp_desc));return 0;}
+ offsetof(lrl_env_params, noise_vec), offsetof(lrl_env_params, max_episode_length), sizeof(lrl_mlp_desc));
+printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_ppo_net), offsetof(lrl_ppo_net, total), sizeof(lrl_ppo_batch),
+ offsetof(lrl_ppo_batch, batch), sizeof(lrl_ppo_hparams), sizeof(lrl_ppo_ctrl));return 0;}
 """
     exe = "/tmp/lrl_layout_check"
     src = exe + ".c"
@@ -43,7 +45,9 @@ int main(){printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_model), sizeof(lrl_env
     out = [int(x) for x in subprocess.check_output([exe]).split()]
     assert out == [C.sizeof(_abi.LrlModel), C.sizeof(_abi.LrlEnvParams), C.sizeof(_abi.LrlTensor),
                    _abi.LrlEnvParams.noise_vec.offset, _abi.LrlEnvParams.max_episode_length.offset,
-                   C.sizeof(_abi.LrlMlpDesc)]
+                   C.sizeof(_abi.LrlMlpDesc), C.sizeof(_abi.LrlPpoNet), _abi.LrlPpoNet.total.offset,
+                   C.sizeof(_abi.LrlPpoBatch), _abi.LrlPpoBatch.batch.offset, C.sizeof(_abi.LrlPpoHparams),
+                   _abi.PPO_CTRL_BYTES]
 
 
 def test_product_fails_loudly_without_gpu():

@@ -1,0 +1,88 @@
+"""fp32 MFMA GEMM of the native PPO update (csrc/lrl_gemm.hip, through lrl_gemm_f32) against a plain
+torch fp32 reference of the same op: the three layouts an MLP's forward / backward-data / weight-gradient
+need, every epilogue, gathered rows, ragged and unaligned shapes."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from lrl import _abi
+
+pytestmark = pytest.mark.gpu
+dev = "cuda:0"
+
+
+def _p(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _gemm(layout, epi, M, N, K, A, lda, B, ldb, Cm, ldc, bias=None, aux=None, ld_aux=0, rows=None, ws=None):
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    nws = ws.numel() if ws is not None else 0
+    _abi.check(_abi.lib().lrl_gemm_f32(C.c_int32(layout), C.c_int32(epi), C.c_int32(M), C.c_int32(N), C.c_int32(K),
+                                       _p(A), C.c_int64(lda), _p(B), C.c_int64(ldb), _p(Cm), C.c_int64(ldc), _p(bias),
+                                       _p(aux), C.c_int64(ld_aux), _p(rows), _p(ws), C.c_int64(nws), stream))
+    torch.cuda.synchronize()
+
+
+def _tol(ref, k):
+    # fp32 accumulation-order difference: ~ sqrt(K) ulps of the magnitude of the products' sum
+    return 2e-6 * np.sqrt(k) * (ref.abs().max().item() + 1.0)
+
+
+@pytest.mark.parametrize("M,N,K,gather,epi", [(300, 200, 60, False, 2), (1000, 1024, 60, True, 2),
+                                               (777, 256, 18, True, 2), (513, 18, 128, False, 1),
+                                               (640, 256, 630, True, 2), (64, 64, 16, False, 0)])
+def test_forward_nt(M, N, K, gather, epi):
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N)
+    src_rows = M + 37
+    X = torch.randn(src_rows, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) / np.sqrt(K)
+    b = torch.randn(N, device=dev, generator=g)
+    rows = torch.randperm(src_rows, device=dev)[:M].contiguous() if gather else None
+    Xm = X[rows] if gather else X[:M]
+    ref = Xm @ W.T
+    if epi >= 1:
+        ref = ref + b
+    if epi == 2:
+        ref = torch.nn.functional.elu(ref)
+    out = torch.full((M, N), float("nan"), device=dev)
+    _gemm(0, epi, M, N, K, X, K, W, K, out, N, bias=b if epi else None, rows=rows)
+    assert torch.isfinite(out).all()
+    assert (out - ref).abs().max().item() <= _tol(ref, K)
+
+
+@pytest.mark.parametrize("M,N,K,delu", [(300, 256, 128, True), (1000, 18, 1024, False), (513, 512, 256, True),
+                                         (96, 128, 18, True)])
+def test_backward_data_nn(M, N, K, delu):
+    g = torch.Generator(device=dev).manual_seed(M + 3 * N + K)
+    dY = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(K, N, device=dev, generator=g) / np.sqrt(K)  # W[out][in] with out = reduction
+    H = torch.nn.functional.elu(torch.randn(M, N, device=dev, generator=g))
+    ref = dY @ W
+    if delu:
+        ref = ref * torch.where(H > 0, torch.ones_like(H), H + 1)
+    out = torch.empty(M, N, device=dev)
+    _gemm(2, 3 if delu else 0, M, N, K, dY, K, W, N, out, N, aux=H if delu else None, ld_aux=N)
+    assert (out - ref).abs().max().item() <= _tol(ref, K)
+
+
+@pytest.mark.parametrize("M,N,K,gather", [(256, 512, 24576, False), (128, 256, 6000, False), (18, 128, 4097, False),
+                                          (256, 630, 24576, True), (1024, 60, 3000, False), (12, 128, 96, False)])
+def test_weight_grad_tn(M, N, K, gather):
+    """dW[o][i] = sum_b dY[b][o] X[b][i] (split over b, partials reduced), db[o] = sum_b dY[b][o]."""
+    g = torch.Generator(device=dev).manual_seed(M * N + K)
+    dY = torch.randn(K, M, device=dev, generator=g)
+    src = K + 11
+    X = torch.randn(src, N, device=dev, generator=g)
+    rows = torch.randperm(src, device=dev)[:K].contiguous() if gather else None
+    Xk = X[rows] if gather else X[:K]
+    ref = dY.T.double() @ Xk.double()
+    out = torch.empty(M, N, device=dev)
+    db = torch.empty(M, device=dev)
+    ws = torch.empty(64 * (M * N + M) * 2, device=dev)
+    _gemm(3, 4, M, N, K, dY, M, X, N, out, N, bias=db, rows=rows, ws=ws)
+    err = (out.double() - ref).abs().max().item()
+    assert err <= 4e-6 * np.sqrt(K) * (ref.abs().max().item() + 1.0), err
+    assert (db.double() - dY.double().sum(0)).abs().max().item() <= 1e-5 * np.sqrt(K) * 10

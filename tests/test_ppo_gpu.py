@@ -107,13 +107,7 @@ def test_ppo_rollout_gae_update_match_reference():
     np.testing.assert_allclose(alg.storage.returns.cpu().numpy(), g["returns"], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(alg.storage.advantages.cpu().numpy(), g["advantages"], rtol=1e-4, atol=1e-4)
     np.testing.assert_array_equal(alg.storage.observation_histories.cpu().numpy(), g["hist_seq"][:T])
-    lrs = []
-    orig_step = alg.optimizer.step
-
-    def step_rec(*a, **k):
-        lrs.append(alg.learning_rate)
-        return orig_step(*a, **k)
-    alg.optimizer.step = step_rec
+    alg.record_lr = True
     perm = torch.as_tensor(g["perm"], device="cuda:0")
     orig = torch.randperm
     torch.randperm = lambda n, **kw: perm
@@ -121,6 +115,7 @@ def test_ppo_rollout_gae_update_match_reference():
         mv, ms, ma = alg.update()
     finally:
         torch.randperm = orig
+    lrs = alg.lr_trace  # learning rate used by each of the 20 PPO optimiser steps (device-side schedule)
     np.testing.assert_allclose(lrs, g["lrs"], rtol=1e-9)
     np.testing.assert_allclose([mv, ms, ma], [g["mean_value_loss"], g["mean_surrogate_loss"],
                                               g["mean_adaptation_loss"]], rtol=2e-3, atol=1e-5)
@@ -131,3 +126,136 @@ def test_ppo_rollout_gae_update_match_reference():
     heads = np.stack([np.pad(params[k].detach().cpu().numpy().ravel()[:16], (0, max(0, 16 - params[k].numel())))
                       for k in names])
     np.testing.assert_allclose(heads, g["param_head"], rtol=2e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,T", [(512, 24), (4096, 24)])
+def test_native_update_matches_torch_autograd(N, T):
+    """The native update (csrc/lrl_ppo.hip: GEMMs + head kernels + device-side LR/clip/Adam) against the
+    torch-autograd restatement (fused=False) on the same rollout storage and permutation, at the
+    benchmark's minibatch size (4096 envs x 24 steps / 4 = 24,576 rows) and a smaller one."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.ppo import PPO
+    torch.manual_seed(0)
+    algs = []
+    for fused in (True, False):
+        ac = ActorCritic(42, 18, 630, 12)
+        init_params(ac)
+        alg = PPO(ac.cuda(), device="cuda:0", fused=fused)
+        alg.init_storage(N, T, [42], [18], [630], [12])
+        algs.append(alg)
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    st0 = algs[0].storage
+    with torch.no_grad():
+        for name in ("observations", "privileged_observations", "observation_histories", "actions", "mu"):
+            getattr(st0, name).copy_(torch.randn(getattr(st0, name).shape, device="cuda:0", generator=g))
+        st0.sigma.fill_(1.0)
+        st0.values.copy_(torch.randn(st0.values.shape, device="cuda:0", generator=g))
+        st0.returns.copy_(st0.values + 0.3 * torch.randn(st0.values.shape, device="cuda:0", generator=g))
+        a = torch.randn(st0.advantages.shape, device="cuda:0", generator=g)
+        st0.advantages.copy_((a - a.mean()) / a.std())
+        # old log-probs near the current policy's so the ratio straddles the clip range
+        st0.actions_log_prob.copy_(-11.0 + torch.randn(st0.values.shape, device="cuda:0", generator=g))
+        for name in ("observations", "privileged_observations", "observation_histories", "actions", "mu", "sigma",
+                     "values", "returns", "advantages", "actions_log_prob"):
+            getattr(algs[1].storage, name).copy_(getattr(st0, name))
+    perm = torch.randperm(N * T, device="cuda:0")
+    orig = torch.randperm
+    torch.randperm = lambda n, **kw: perm
+    try:
+        out = [alg.update() for alg in algs]
+    finally:
+        torch.randperm = orig
+    assert algs[0].learning_rate == algs[1].learning_rate
+    np.testing.assert_allclose(out[0], out[1], rtol=2e-3, atol=1e-5)
+    p0 = dict(algs[0].actor_critic.named_parameters())
+    for k, v in algs[1].actor_critic.named_parameters():
+        d = (p0[k].detach() - v.detach()).abs().max().item()
+        assert d <= 2e-3 * (v.detach().abs().max().item() + 1e-2), (k, d)
+
+
+def _random_storage(alg, N, T, seed=1):
+    st = alg.storage
+    g = torch.Generator(device="cuda:0").manual_seed(seed)
+    with torch.no_grad():
+        for name in ("observations", "privileged_observations", "observation_histories", "actions", "mu"):
+            getattr(st, name).copy_(torch.randn(getattr(st, name).shape, device="cuda:0", generator=g))
+        st.sigma.fill_(1.0)
+        st.values.copy_(torch.randn(st.values.shape, device="cuda:0", generator=g))
+        st.returns.copy_(st.values + 0.3 * torch.randn(st.values.shape, device="cuda:0", generator=g))
+        a = torch.randn(st.advantages.shape, device="cuda:0", generator=g)
+        st.advantages.copy_((a - a.mean()) / a.std())
+        st.actions_log_prob.copy_(-11.0 + torch.randn(st.values.shape, device="cuda:0", generator=g))
+
+
+def test_native_minibatch_gradients_match_autograd():
+    """One minibatch of lrl_ppo_forward_backward / lrl_ppo_adaptation_forward_backward against torch
+    autograd of the reference's loss (ppo.py:98-147, 157-166): every parameter's gradient, the KL mean,
+    the losses."""
+    import ctypes as C
+    import torch.nn.functional as F
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.ppo import PPO, PPO_Args
+    N, T = 256, 24
+    ac = ActorCritic(42, 18, 630, 12)
+    init_params(ac)
+    alg = PPO(ac.cuda(), device="cuda:0", fused=True)
+    alg.init_storage(N, T, [42], [18], [630], [12])
+    _random_storage(alg, N, T)
+    mb = N * T // 4
+    rows = torch.randperm(N * T, device="cuda:0")[:mb].contiguous()
+    nst = alg._native_state(mb)
+    net, hp, grads, ctrl, ws = nst["net"], nst["hp"], nst["grads"], nst["ctrl"], nst["ws"]
+    s = alg.storage
+    fl = lambda t: t.flatten(0, 1)
+    batch = _abi.LrlPpoBatch()
+    for k, t in dict(obs=s.observations, priv=s.privileged_observations, hist=s.observation_histories,
+                     actions=s.actions, values=s.values, returns=s.returns, logp=s.actions_log_prob,
+                     adv=s.advantages, mu=s.mu, sigma=s.sigma).items():
+        setattr(batch, k, fl(t).data_ptr())
+    batch.rows, batch.batch = rows.data_ptr(), mb
+    p = lambda t: C.c_void_p(t.data_ptr())
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L = _abi.lib()
+    _abi.check(L.lrl_ppo_forward_backward(C.byref(net), p(ac._flat), p(grads), C.byref(batch), C.byref(hp), p(ws),
+                                          p(ctrl), stream))
+    _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), p(ac._flat), p(grads), C.byref(batch), p(ws),
+                                                     p(ctrl), stream))
+    torch.cuda.synchronize()
+    mbf = ctrl.view(torch.float32)[8:12].tolist()  # value, surrogate, adaptation, (kl in grads)
+    kl_native = grads[net.kl_slot].item()
+    # torch autograd on the same minibatch
+    obs, priv, hist = fl(s.observations)[rows], fl(s.privileged_observations)[rows], fl(s.observation_histories)[rows]
+    act, tv, ret = fl(s.actions)[rows], fl(s.values)[rows], fl(s.returns)[rows]
+    oldlp, adv, omu, osig = fl(s.actions_log_prob)[rows], fl(s.advantages)[rows], fl(s.mu)[rows], fl(s.sigma)[rows]
+    ac.zero_grad(set_to_none=True)
+    ac.act(obs, priv)
+    logp = ac.get_actions_log_prob(act)
+    value = ac.evaluate(obs, priv)
+    mu, sigma, ent = ac.action_mean, ac.action_std, ac.entropy
+    with torch.no_grad():
+        kl = torch.sum(torch.log(sigma / osig + 1.e-5) + (torch.square(osig) + torch.square(omu - mu)) /
+                       (2.0 * torch.square(sigma)) - 0.5, axis=-1).mean().item()
+    ratio = torch.exp(logp - torch.squeeze(oldlp))
+    surr = torch.max(-torch.squeeze(adv) * ratio,
+                     -torch.squeeze(adv) * torch.clamp(ratio, 1 - PPO_Args.clip_param, 1 + PPO_Args.clip_param)).mean()
+    vc = tv + (value - tv).clamp(-PPO_Args.clip_param, PPO_Args.clip_param)
+    vl = torch.max((value - ret).pow(2), (vc - ret).pow(2)).mean()
+    loss = surr + vl - PPO_Args.entropy_coef * ent.mean()
+    loss.backward()
+    pred = ac.adaptation_module(hist)
+    with torch.no_grad():
+        target = ac.env_factor_encoder(priv)
+    al = F.mse_loss(pred, target)
+    al.backward()
+    np.testing.assert_allclose(kl_native, kl, rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(mbf[:3], [vl.item(), surr.item(), al.item()], rtol=1e-4, atol=1e-7)
+    fg = grads.cpu()
+    bad = []
+    for name, prm in ac.named_parameters():
+        off = (prm.data_ptr() - ac._flat.data_ptr()) // 4
+        got = fg[off:off + prm.numel()].view_as(prm)
+        ref = prm.grad.cpu()
+        err = (got - ref).abs().max().item()
+        if err > 1e-4 * (ref.abs().max().item() + 1e-6) + 1e-7:
+            bad.append(f"{name}: err {err:.3g} ref max {ref.abs().max().item():.3g} got max {got.abs().max().item():.3g}")
+    assert not bad, "\n".join(bad)
