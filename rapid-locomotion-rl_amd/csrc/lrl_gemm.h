@@ -9,7 +9,7 @@
 // the weight gradient) may be gathered through an int64 row list — the minibatch indices of
 // RolloutStorage.mini_batch_generator (rollout_storage.py:100-137) — so the minibatch is never copied.
 //
-// A workgroup (4 waves, 2x2) owns a BM x BN tile (BM, BN in {64, 128}); tiles of BK = 16 stage through
+// A workgroup (4 waves) owns a BM x BN tile (128/64 wide, 32 for thin layers); slices of BK = 32 stage through
 // LDS k-major ([k][m] / [k][n]) so each MFMA operand is one conflict-free ds_read_b32 per lane; the
 // next tile is prefetched into registers while the current one is consumed (one barrier per tile).
 #pragma once
@@ -36,6 +36,7 @@ struct GemmP {
   float* bias_part;       // EPI_PARTIAL: [splits][groups][M] partial sums over k of A(m, k), or nullptr
   int M, N, K;
   int splits, kps;        // k range of split s: [s*kps, min(K, (s+1)*kps))
+  int avec, bvec;         // staging access width (4/2/1 floats), set by gemm_launch from the alignment
   int64_t lda, ldb, ldc, ld_aux;
   int64_t ga, gb, gc, gbias, gaux;  // per-group element offsets (blockIdx.z = group * splits + split)
   int64_t part_stride;              // EPI_PARTIAL: elements between split slices of C ([split][group][M][N])

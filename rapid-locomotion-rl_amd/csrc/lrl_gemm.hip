@@ -10,48 +10,71 @@ namespace lrl {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int GBK = 16;
+#ifndef LRL_GBK
+#define LRL_GBK 16
+#endif
+constexpr int GBK = LRL_GBK;  // k-slice per LDS stage
+constexpr int KQ = GBK / 4;   // float4 items per k-contiguous row slice
 constexpr int GTHREADS = 256;
 
 template <int BM, int BN, int LAYOUT>
 struct GemmTile {
   static constexpr bool AMC = (LAYOUT & 1) != 0;
   static constexpr bool BNC = (LAYOUT & 2) != 0;
-  // k-major LDS images; padding keeps the transposing stores of k-contiguous operands conflict-free
-  // (row pitch = 2 mod 8 words) and the float4 stores of m/n-contiguous operands 16-B aligned.
-  static constexpr int PA = AMC ? 4 : 2;
-  static constexpr int PB = BNC ? 4 : 2;
-  static constexpr int NA = BM * GBK / 4 / GTHREADS;  // float4 loads per thread per tile
-  static constexpr int NB = BN * GBK / 4 / GTHREADS;
+  // k-major LDS images.  Transposing stores of k-contiguous operands: row pitch = 1 mod 8 words keeps the
+  // 32 lanes of a half-wave (4 rows x 8 k-quads) on distinct banks; float4 stores of m/n-contiguous
+  // operands need a 16-B aligned pitch.
+  static constexpr int PK = GBK == 32 ? 1 : 2;
+  static constexpr int PA = AMC ? 4 : PK;
+  static constexpr int PB = BNC ? 4 : PK;
+  static constexpr int IA = BM * GBK / 4, IB = BN * GBK / 4;  // float4 items per tile
+  static constexpr int NA = (IA + GTHREADS - 1) / GTHREADS;   // per thread
+  static constexpr int NB = (IB + GTHREADS - 1) / GTHREADS;
+  // 4 waves: WM x WN wave grid, each wave TM x TN MFMA tiles of 32x32
+  static constexpr int WN = (BM >= 64 && BN >= 64) ? 2 : (BM == 32 ? 4 : 1);
+  static constexpr int WM = 4 / WN;
+  static constexpr int TM = BM / (32 * WM);
+  static constexpr int TN = BN / (32 * WN);
+  static_assert(TM >= 1 && TN >= 1, "tile shape");
 };
 
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
 
+// load 4 consecutive floats (all in range) with the widest access the operand's alignment allows
+__device__ __forceinline__ float4 load4(const float* __restrict__ src, int vec) {
+  if (vec == 4) return *reinterpret_cast<const float4*>(src);
+  if (vec == 2) {
+    const float2 a = reinterpret_cast<const float2*>(src)[0], b = reinterpret_cast<const float2*>(src)[1];
+    return make_float4(a.x, a.y, b.x, b.y);
+  }
+  return make_float4(src[0], src[1], src[2], src[3]);
+}
+
 // ---- global -> register staging of one BK slice ----
-// k-contiguous operand X(r, k) = P[row(r) * ld + k], tile rows r0.., k0..: thread item i covers
-// (r = i / 4, k = 4 (i % 4) .. +3).  m/n-contiguous operand X(r, k) = P[krow(k) * ld + r]: item i covers
-// (k = i / (R/4), r = 4 (i % (R/4)) .. +3).
-template <int R, int NI, bool RCONTIG, bool VEC>
+// k-contiguous operand X(r, k) = P[row(r) * ld + k]: item i covers (r = i / KQ, k = 4 (i % KQ) .. +3).
+// r-contiguous operand X(r, k) = P[krow(k) * ld + r]: item i covers (k = i / (R/4), r = 4 (i % (R/4)) .. +3).
+template <int R, int NI, bool RCONTIG>
 __device__ __forceinline__ void stage_load(float4 (&reg)[NI], const float* __restrict__ P, int64_t ld,
-                                           const int64_t* __restrict__ rows, int r0, int R_lim, int k0,
+                                           const int64_t* __restrict__ rows, int vec, int r0, int R_lim, int k0,
                                            int k_lim) {
+  constexpr int ITEMS = R * GBK / 4;
 #pragma unroll
   for (int u = 0; u < NI; ++u) {
     const int i = threadIdx.x + u * GTHREADS;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (!RCONTIG) {
-      const int r = i >> 2, k = k0 + 4 * (i & 3);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ITEMS % GTHREADS != 0 && i >= ITEMS) {
+    } else if (!RCONTIG) {
+      const int r = i / KQ, k = k0 + 4 * (i % KQ);
       const int gr = r0 + r;
       if (gr < R_lim) {
         const int64_t row = rows ? rows[gr] : (int64_t)gr;
         const float* src = P + row * ld + k;
-        if (VEC && k + 3 < k_lim) {
-          const float4 t = *reinterpret_cast<const float4*>(src);
-          v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        if (k + 3 < k_lim) {
+          v = load4(src, vec);
         } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (k + c < k_lim) v[c] = src[c];
+          if (k + 0 < k_lim) v.x = src[0];
+          if (k + 1 < k_lim) v.y = src[1];
+          if (k + 2 < k_lim) v.z = src[2];
         }
       }
     } else {
@@ -60,27 +83,28 @@ __device__ __forceinline__ void stage_load(float4 (&reg)[NI], const float* __res
       if (k < k_lim) {
         const int64_t row = rows ? rows[k] : (int64_t)k;
         const float* src = P + row * ld + gr;
-        if (VEC && gr + 3 < R_lim) {
-          const float4 t = *reinterpret_cast<const float4*>(src);
-          v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        if (gr + 3 < R_lim) {
+          v = load4(src, vec);
         } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (gr + c < R_lim) v[c] = src[c];
+          if (gr + 0 < R_lim) v.x = src[0];
+          if (gr + 1 < R_lim) v.y = src[1];
+          if (gr + 2 < R_lim) v.z = src[2];
         }
       }
     }
-    reg[u] = make_float4(v[0], v[1], v[2], v[3]);
+    reg[u] = v;
   }
 }
 
 template <int R, int PAD, int NI, bool RCONTIG>
 __device__ __forceinline__ void stage_store(float (*S)[R + PAD], const float4 (&reg)[NI]) {
+  constexpr int ITEMS = R * GBK / 4;
 #pragma unroll
   for (int u = 0; u < NI; ++u) {
     const int i = threadIdx.x + u * GTHREADS;
-    if (!RCONTIG) {
-      const int r = i >> 2, k = 4 * (i & 3);
+    if (ITEMS % GTHREADS != 0 && i >= ITEMS) {
+    } else if (!RCONTIG) {
+      const int r = i / KQ, k = 4 * (i % KQ);
       S[k + 0][r] = reg[u].x;
       S[k + 1][r] = reg[u].y;
       S[k + 2][r] = reg[u].z;
@@ -92,7 +116,7 @@ __device__ __forceinline__ void stage_store(float (*S)[R + PAD], const float4 (&
   }
 }
 
-template <int BM, int BN, int LAYOUT, bool AV, bool BV, int EPI>
+template <int BM, int BN, int LAYOUT, int EPI>
 __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   using T = GemmTile<BM, BN, LAYOUT>;
   __shared__ __attribute__((aligned(16))) float As[2][GBK][BM + T::PA];
@@ -105,8 +129,10 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   const int kend = min(p.K, kbeg + p.kps);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 31, h = lane >> 5;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  constexpr int TM = T::TM, TN = T::TN;
+  const int wm = (w / T::WN) * (BM / T::WM), wn = (w % T::WN) * (BN / T::WN);
+  const int64_t* a_rows = T::AMC ? nullptr : p.a_rows;
+  const int64_t* b_rows = T::BNC ? p.b_rows : nullptr;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -123,8 +149,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   float4 ra[T::NA], rb[T::NB];
   int k0 = kbeg;
   if (k0 < kend) {
-    stage_load<BM, T::NA, T::AMC, AV>(ra, A, p.lda, T::AMC ? nullptr : p.a_rows, m0, p.M, k0, kend);
-    stage_load<BN, T::NB, T::BNC, BV>(rb, B, p.ldb, T::BNC ? p.b_rows : nullptr, n0, p.N, k0, kend);
+    stage_load<BM, T::NA, T::AMC>(ra, A, p.lda, a_rows, p.avec, m0, p.M, k0, kend);
+    stage_load<BN, T::NB, T::BNC>(rb, B, p.ldb, b_rows, p.bvec, n0, p.N, k0, kend);
     stage_store<BM, T::PA, T::NA, T::AMC>(As[0], ra);
     stage_store<BN, T::PB, T::NB, T::BNC>(Bs[0], rb);
   }
@@ -133,8 +159,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   for (; k0 < kend; k0 += GBK) {
     const int kn = k0 + GBK;
     if (kn < kend) {
-      stage_load<BM, T::NA, T::AMC, AV>(ra, A, p.lda, T::AMC ? nullptr : p.a_rows, m0, p.M, kn, kend);
-      stage_load<BN, T::NB, T::BNC, BV>(rb, B, p.ldb, T::BNC ? p.b_rows : nullptr, n0, p.N, kn, kend);
+      stage_load<BM, T::NA, T::AMC>(ra, A, p.lda, a_rows, p.avec, m0, p.M, kn, kend);
+      stage_load<BN, T::NB, T::BNC>(rb, B, p.ldb, b_rows, p.bvec, n0, p.N, kn, kend);
     }
     if (do_bsum && threadIdx.x < BM) {
 #pragma unroll
@@ -194,48 +220,58 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
     p.bias_part[((int64_t)s * (gridDim.z / p.splits) + g) * p.M + m0 + threadIdx.x] = bsum;
 }
 
-template <int BM, int BN, int LAYOUT, int EPI>
-static void launch_t(const GemmP& p, bool av, bool bv, dim3 grid, hipStream_t st) {
-  if (av && bv)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, LAYOUT, true, true, EPI>), grid, dim3(GTHREADS), 0, st, p);
-  else if (av)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, LAYOUT, true, false, EPI>), grid, dim3(GTHREADS), 0, st, p);
-  else if (bv)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, LAYOUT, false, true, EPI>), grid, dim3(GTHREADS), 0, st, p);
-  else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, LAYOUT, false, false, EPI>), grid, dim3(GTHREADS), 0, st, p);
-}
-
 template <int BM, int BN>
-static int launch_bm(const GemmP& p, int layout, int epi, bool av, bool bv, dim3 grid, hipStream_t st) {
+static int launch_bm(const GemmP& p, int layout, int epi, dim3 grid, hipStream_t st) {
+#define LRL_GEMM_LAUNCH(L, E) hipLaunchKernelGGL((gemm_kernel<BM, BN, L, E>), grid, dim3(GTHREADS), 0, st, p)
   switch (layout) {
     case GEMM_NT:
       switch (epi) {
-        case EPI_STORE: launch_t<BM, BN, GEMM_NT, EPI_STORE>(p, av, bv, grid, st); return 0;
-        case EPI_BIAS: launch_t<BM, BN, GEMM_NT, EPI_BIAS>(p, av, bv, grid, st); return 0;
-        case EPI_BIAS_ELU: launch_t<BM, BN, GEMM_NT, EPI_BIAS_ELU>(p, av, bv, grid, st); return 0;
+        case EPI_STORE: LRL_GEMM_LAUNCH(GEMM_NT, EPI_STORE); return 0;
+        case EPI_BIAS: LRL_GEMM_LAUNCH(GEMM_NT, EPI_BIAS); return 0;
+        case EPI_BIAS_ELU: LRL_GEMM_LAUNCH(GEMM_NT, EPI_BIAS_ELU); return 0;
       }
       break;
     case GEMM_NN:
       switch (epi) {
-        case EPI_STORE: launch_t<BM, BN, GEMM_NN, EPI_STORE>(p, av, bv, grid, st); return 0;
-        case EPI_DELU: launch_t<BM, BN, GEMM_NN, EPI_DELU>(p, av, bv, grid, st); return 0;
+        case EPI_STORE: LRL_GEMM_LAUNCH(GEMM_NN, EPI_STORE); return 0;
+        case EPI_DELU: LRL_GEMM_LAUNCH(GEMM_NN, EPI_DELU); return 0;
+        case EPI_PARTIAL: LRL_GEMM_LAUNCH(GEMM_NN, EPI_PARTIAL); return 0;
       }
       break;
     case GEMM_TN:
       if (epi == EPI_PARTIAL) {
-        launch_t<BM, BN, GEMM_TN, EPI_PARTIAL>(p, av, bv, grid, st);
+        LRL_GEMM_LAUNCH(GEMM_TN, EPI_PARTIAL);
         return 0;
       }
       break;
   }
+#undef LRL_GEMM_LAUNCH
   return LRL_E_INVALID;
 }
 
-static bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+// widest staging access allowed by the pitch / base / group offset alignment of an operand
+static int vec_width(const float* ptr, int64_t ld, int64_t goff) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+  if ((a & 15) == 0 && ld % 4 == 0 && goff % 4 == 0) return 4;
+  if ((a & 7) == 0 && ld % 2 == 0 && goff % 2 == 0) return 2;
+  return 1;
+}
+
+// tile shape: 128 where the dimension is long, narrower for the thin layers; at least 4 32x32 tiles
+// Measured on MI355X (scripts/gemm_bench.py): 64x64 tiles (4 workgroups/CU, one 32x32 MFMA tile per
+// wave) beat 128x128 for the batch-major forward / backward-data products; the split-k weight
+// gradients prefer 128x128.
+static void pick_tile(int M, int N, bool wgrad, int& bm, int& bn) {
+  const int mx = wgrad ? 128 : 64;
+  bm = M > 64 && mx > 64 ? 128 : (M > 32 ? 64 : 32);
+  bn = N > 64 && mx > 64 ? 128 : (N > 32 ? 64 : 32);
+  if (bm == 32 && bn < 128) bn = 128;
+  if (bn == 32 && bm < 128) bm = 128;
+}
 
 int gemm_pick_splits(int M, int N, int K, int groups) {
-  const int bm = M > 64 ? 128 : 64, bn = N > 64 ? 128 : 64;
+  int bm, bn;
+  pick_tile(M, N, true, bm, bn);
   const int tiles = groups * ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   int splits = 1;
   // aim for >= 512 workgroups, keep >= 256 rows per split and <= 128 splits
@@ -249,21 +285,19 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   if (p.splits <= 0) p.splits = 1;
   if (p.kps <= 0) p.kps = (p.K + p.splits - 1) / p.splits;
   p.kps = (p.kps + GBK - 1) / GBK * GBK;
-  const bool amc = layout & 1, bnc = layout & 2;
-  // float4 staging needs the contiguous dimension's pitch and base 16-B aligned (group offsets too)
-  const bool av = (p.lda % 4 == 0) && aligned16(p.A) && (p.ga % 4 == 0);
-  const bool bv = (p.ldb % 4 == 0) && aligned16(p.B) && (p.gb % 4 == 0);
-  (void)amc;
-  (void)bnc;
-  const int bm = p.M > 64 ? 128 : 64;
-  const int bn = p.N > 64 ? 128 : 64;
+  p.avec = vec_width(p.A, p.lda, p.ga);
+  p.bvec = vec_width(p.B, p.ldb, p.gb);
+  int bm, bn;
+  pick_tile(p.M, p.N, layout == GEMM_TN, bm, bn);
   dim3 grid((p.M + bm - 1) / bm, (p.N + bn - 1) / bn, groups * p.splits);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  int rc;
-  if (bm == 128 && bn == 128) rc = launch_bm<128, 128>(p, layout, epi, av, bv, grid, st);
-  else if (bm == 128) rc = launch_bm<128, 64>(p, layout, epi, av, bv, grid, st);
-  else if (bn == 128) rc = launch_bm<64, 128>(p, layout, epi, av, bv, grid, st);
-  else rc = launch_bm<64, 64>(p, layout, epi, av, bv, grid, st);
+  int rc = LRL_E_INVALID;
+  if (bm == 128 && bn == 128) rc = launch_bm<128, 128>(p, layout, epi, grid, st);
+  else if (bm == 128 && bn == 64) rc = launch_bm<128, 64>(p, layout, epi, grid, st);
+  else if (bm == 64 && bn == 128) rc = launch_bm<64, 128>(p, layout, epi, grid, st);
+  else if (bm == 64 && bn == 64) rc = launch_bm<64, 64>(p, layout, epi, grid, st);
+  else if (bm == 128 && bn == 32) rc = launch_bm<128, 32>(p, layout, epi, grid, st);
+  else if (bm == 32 && bn == 128) rc = launch_bm<32, 128>(p, layout, epi, grid, st);
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
 }

@@ -87,9 +87,21 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
   const int t = threadIdx.x, na = a.na;
   const int r0 = blockIdx.x * HEAD_ROWS;
   const int nrows = min(HEAD_ROWS, a.B - r0);
-  for (int i = t; i < HEAD_ROWS * 2 * HEAD_W; i += HEAD_THREADS) {
-    const int r = i / (2 * HEAD_W), c = i - r * (2 * HEAD_W);
-    H[r][c] = r < nrows ? a.h3[(int64_t)(r0 + r) * (2 * HEAD_W) + c] : 0.f;
+  {
+    // 16 float4 loads in flight per thread, then scattered into the odd-pitch LDS tile
+    constexpr int NV = HEAD_ROWS * 2 * HEAD_W / 4 / HEAD_THREADS;
+    float4 v[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i = t + u * HEAD_THREADS, r = i / (HEAD_W / 2), c = 4 * (i % (HEAD_W / 2));
+      v[u] = r < nrows ? *reinterpret_cast<const float4*>(a.h3 + (int64_t)(r0 + r) * (2 * HEAD_W) + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i = t + u * HEAD_THREADS, r = i / (HEAD_W / 2), c = 4 * (i % (HEAD_W / 2));
+      H[r][c] = v[u].x; H[r][c + 1] = v[u].y; H[r][c + 2] = v[u].z; H[r][c + 3] = v[u].w;
+    }
   }
   for (int i = t; i < (na + 1) * HEAD_W; i += HEAD_THREADS) {
     const int j = i / HEAD_W, k = i - j * HEAD_W;
@@ -111,24 +123,30 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
   __syncthreads();
   const float invB = 1.f / (float)a.B;
   if (t < HEAD_ROWS) {
+    // one lane per row; per-action loops are unrolled to MAX_ACT with guards so the arrays stay in VGPRs
     const int r = t;
-    float dsig[MAX_ACT];
     float kl = 0.f, surr_loss = 0.f, vloss = 0.f, dv = 0.f;
-    for (int j = 0; j < na; ++j) { DMU[r][j] = 0.f; dsig[j] = 0.f; }
+    float dmu[MAX_ACT], dsig[MAX_ACT];
+#pragma unroll
+    for (int j = 0; j < MAX_ACT; ++j) { dmu[j] = 0.f; dsig[j] = 0.f; }
     if (r < nrows) {
       const int64_t g = a.rows[r0 + r];
       const float v = ((VP[r][0] + VP[r][1]) + (VP[r][2] + VP[r][3])) + a.b4c[0];
       float logp = 0.f;
       float dj[MAX_ACT];
-      for (int j = 0; j < na; ++j) {
-        const float s = a.stdv[j], mu = MU[r][j];
-        const float var = s * s;
-        const float d = a.actions[g * na + j] - mu;
-        dj[j] = d;
-        logp += -(d * d) / (2.f * var) - logf(s) - LOG_SQRT_2PI;
-        // KL(old || new), ppo.py:111-114 (inference mode)
-        const float so = a.old_sigma[g * na + j], dm = a.old_mu[g * na + j] - mu;
-        kl += logf(s / so + 1.e-5f) + (so * so + dm * dm) / (2.f * (s * s)) - 0.5f;
+#pragma unroll
+      for (int j = 0; j < MAX_ACT; ++j) {
+        dj[j] = 0.f;
+        if (j < na) {
+          const float s = a.stdv[j], mu = MU[r][j];
+          const float var = s * s;
+          const float d = a.actions[g * na + j] - mu;
+          dj[j] = d;
+          logp += -(d * d) / (2.f * var) - logf(s) - LOG_SQRT_2PI;
+          // KL(old || new), ppo.py:111-114 (inference mode)
+          const float so = a.old_sigma[g * na + j], dm = a.old_mu[g * na + j] - mu;
+          kl += logf(s / so + 1.e-5f) + (so * so + dm * dm) / (2.f * (s * s)) - 0.5f;
+        }
       }
       const float adv = a.adv[g];
       const float ratio = expf(logp - a.old_logp[g]);
@@ -142,10 +160,13 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
       const bool in_rng = ratio >= 1.f - a.clip && ratio <= 1.f + a.clip;
       const float dratio = -adv * ga + (in_rng ? -adv * gb : 0.f);
       const float dlogp = dratio * ratio;
-      for (int j = 0; j < na; ++j) {
-        const float s = a.stdv[j], var = s * s, d = dj[j];
-        DMU[r][j] = dlogp * (d / var);
-        dsig[j] = dlogp * (d * d / (var * s) - 1.f / s) - a.ent_coef * invB / s;
+#pragma unroll
+      for (int j = 0; j < MAX_ACT; ++j) {
+        if (j < na) {
+          const float s = a.stdv[j], var = s * s, d = dj[j];
+          dmu[j] = dlogp * (d / var);
+          dsig[j] = dlogp * (d * d / (var * s) - 1.f / s) - a.ent_coef * invB / s;
+        }
       }
       // value loss (ppo.py:133-143)
       const float tv = a.tv[g], ret = a.ret[g];
@@ -164,8 +185,12 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
         dv = gv * 2.f * (v - ret);
       }
     }
-    DMU[r][na] = dv;
-    for (int j = 0; j < na; ++j) DS[r][j] = dsig[j];
+#pragma unroll
+    for (int j = 0; j < MAX_ACT; ++j) {
+      DMU[r][j] = dmu[j];
+      DS[r][j] = dsig[j];
+    }
+    DMU[r][MAX_ACT] = dv;
     SC[r][0] = kl;
     SC[r][1] = surr_loss;
     SC[r][2] = vloss;
@@ -175,30 +200,37 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
   float* P = a.part + (int64_t)blockIdx.x * a.part_len;
   {
     const int k = t;  // 0..255
-    const bool actor = k < HEAD_W;
-    const int kk = actor ? k : k - HEAD_W;
-    float accw[MAX_ACT];
-    for (int j = 0; j < MAX_ACT; ++j) accw[j] = 0.f;
-    float accc = 0.f;
-    for (int r = 0; r < nrows; ++r) {
-      const float h = H[r][k];
-      float g;
-      if (actor) {
-        float s = 0.f;
-        for (int j = 0; j < na; ++j) {
-          s = fmaf(DMU[r][j], W4[j][kk], s);
-          accw[j] = fmaf(DMU[r][j], h, accw[j]);
-        }
-        g = s;
-      } else {
-        g = DMU[r][na] * W4[na][kk];
-        accc = fmaf(DMU[r][na], h, accc);
+    if (k < HEAD_W) {
+      float wk[MAX_ACT], accw[MAX_ACT];
+#pragma unroll
+      for (int j = 0; j < MAX_ACT; ++j) {
+        wk[j] = j < na ? W4[j][k] : 0.f;
+        accw[j] = 0.f;
       }
-      a.dh3[(int64_t)(r0 + r) * (2 * HEAD_W) + k] = g * delu(h);
-    }
-    if (actor) {
-      for (int j = 0; j < na; ++j) P[hp_w4a(na) + j * HEAD_W + kk] = accw[j];
+      for (int r = 0; r < nrows; ++r) {
+        const float h = H[r][k];
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < MAX_ACT; ++j) {
+          const float dm = DMU[r][j];  // zero for j >= na
+          s = fmaf(dm, wk[j], s);
+          accw[j] = fmaf(dm, h, accw[j]);
+        }
+        a.dh3[(int64_t)(r0 + r) * (2 * HEAD_W) + k] = s * delu(h);
+      }
+#pragma unroll
+      for (int j = 0; j < MAX_ACT; ++j)
+        if (j < na) P[hp_w4a(na) + j * HEAD_W + k] = accw[j];
     } else {
+      const int kk = k - HEAD_W;
+      const float wk = W4[na][kk];
+      float accc = 0.f;
+      for (int r = 0; r < nrows; ++r) {
+        const float h = H[r][k];
+        const float d = DMU[r][MAX_ACT];
+        accc = fmaf(d, h, accc);
+        a.dh3[(int64_t)(r0 + r) * (2 * HEAD_W) + k] = (d * wk) * delu(h);
+      }
       P[hp_w4c(na) + kk] = accc;
     }
   }
@@ -210,9 +242,9 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
     }
     P[hp_b4a(na) + t] = sb;
     P[hp_std(na) + t] = ss;
-  } else if (t == na) {
+  } else if (t == 16) {
     float sb = 0.f;
-    for (int r = 0; r < nrows; ++r) sb += DMU[r][na];
+    for (int r = 0; r < nrows; ++r) sb += DMU[r][MAX_ACT];
     P[hp_b4c(na)] = sb;
   } else if (t >= 32 && t < 35) {
     const int c = t - 32;
@@ -313,9 +345,18 @@ struct SegList {
 __global__ void seg_reduce_kernel(SegList L) {
   const Seg& sg = L.s[blockIdx.y];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.len; i += (int64_t)gridDim.x * blockDim.x) {
+    // 8 independent loads in flight per step, summed in part order (deterministic)
     float acc = 0.f;
     const float* p = sg.src + i;
-    for (int q = 0; q < sg.parts; ++q) acc += p[(int64_t)q * sg.stride];
+    int q = 0;
+    for (; q + 8 <= sg.parts; q += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(q + u) * sg.stride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; q < sg.parts; ++q) acc += p[(int64_t)q * sg.stride];
     sg.dst[i] = acc * sg.scale;
   }
 }
@@ -441,7 +482,7 @@ static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
   int64_t ph1 = tn_part_floats(n.ac_h2, n.ac_h1, B, 2) + tn_part_floats(n.ac_h1, n.ac_h0, B, 2) +
                 tn_part_floats(2 * n.ac_h0, n.num_obs + n.latent, B, 1) + tn_part_floats(n.latent, n.enc_h1, B, 1) +
                 tn_part_floats(n.enc_h1, n.enc_h0, B, 1) + tn_part_floats(n.enc_h0, n.num_priv, B, 1) +
-                (int64_t)hb * hp_len(n.num_actions) + 64 * 8;
+                (int64_t)hb * hp_len(n.num_actions) + 64 * 8 + 16 * Bl * LATS;  // + split-k d latent
   int64_t ph3 = tn_part_floats(n.ad_h1, n.ad_h0, B, 1) + tn_part_floats(n.ad_h0, n.num_hist, B, 1) +
                 (int64_t)hb * (n.latent * n.ad_h1 + n.latent + 1) + 64 * 4;
   p.part_floats = std::max(ph1, ph3);
@@ -458,6 +499,8 @@ static int check_net(const lrl_ppo_net* n) {
   if (n->num_obs + n->latent > XS) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: obs + latent > 64");
   return 0;
 }
+
+static void launch_seg(const SegList& L, hipStream_t st);
 
 // one GEMM helper per layout
 struct G {
@@ -485,6 +528,23 @@ struct G {
     p.ga = gy; p.gb = gw; p.gc = gx; p.gaux = gaux;
     rc = gemm_launch(p, GEMM_NN, aux ? EPI_DELU : EPI_STORE, groups, st);
   }
+  // thin, long-k dX = dY W (no activation): split over k into partials + an immediate reduction
+  // (a 128x32 tile walking k = 1024 alone is load-latency bound)
+  void nn_splitk(const float* dY, int64_t ldy, const float* W, int64_t ldw, float* dX, int64_t ldx, int M, int N,
+                 int K, float* part) {
+    if (rc) return;
+    const int splits = std::max(1, std::min(16, K / 64));
+    if (part + (int64_t)splits * M * ldx > part_end) { rc = LRL_E_INVALID; return; }
+    GemmP p{};
+    p.A = dY; p.lda = ldy; p.B = W; p.ldb = ldw; p.C = part; p.ldc = ldx;
+    p.M = M; p.N = N; p.K = K; p.splits = splits; p.kps = (K + splits - 1) / splits;
+    p.part_stride = (int64_t)M * ldx;
+    rc = gemm_launch(p, GEMM_NN, EPI_PARTIAL, 1, st);
+    if (rc) return;
+    SegList L{};
+    L.s[L.n++] = Seg{part, dX, (int64_t)M * ldx, (int64_t)M * ldx, splits, 1.f};
+    launch_seg(L, st);
+  }
   // partial dW[o][i] = sum_b dY[b][o] X[rows(b)][i]; returns the segments (weights then biases)
   void tn(const float* dY, int64_t ldy, const float* X, int64_t ldx, const int64_t* rows, int M, int N, int K,
           int groups, int64_t gy, int64_t gx, float*& part, float* dw, float* db, SegList& L) {
@@ -511,7 +571,7 @@ struct G {
 static void launch_seg(const SegList& L, hipStream_t st) {
   int64_t mx = 1;
   for (int i = 0; i < L.n; ++i) mx = std::max(mx, L.s[i].len);
-  const int bx = (int)std::min<int64_t>((mx + 255) / 256, 1024);
+  const int bx = (int)std::min<int64_t>((mx + 255) / 256, 2048);
   hipLaunchKernelGGL(seg_reduce_kernel, dim3(bx, L.n), dim3(256), 0, st, L);
 }
 
@@ -584,7 +644,7 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
   g.tn(P.dh1, 2 * h0, P.xa, XS, nullptr, 2 * h0, nx, B, 1, 0, 0, part, grads + n.w1, grads + n.b1, L);
   // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
-  g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
+  g.nn_splitk(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, B, n.latent, 2 * h0, part);
   g.tn(P.dlat, LATS, P.he2, n.enc_h1, nullptr, n.latent, n.enc_h1, B, 1, 0, 0, part, grads + n.e3w, grads + n.e3b, L);
   g.nn(P.dlat, LATS, w + n.e3w, n.enc_h1, P.dhe2, n.enc_h1, P.he2, n.enc_h1, B, n.enc_h1, n.latent);
   g.tn(P.dhe2, n.enc_h1, P.he1, n.enc_h0, nullptr, n.enc_h1, n.enc_h0, B, 1, 0, 0, part, grads + n.e2w, grads + n.e2b, L);
