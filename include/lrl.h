@@ -23,7 +23,7 @@
  *                            (legged_robot.py:303-312, 710-712, 739-741)
  *   lrl_sim_refresh_rigid_body_state ~ gym.refresh_rigid_body_state_tensor (:147)
  *   lrl_gae                ~ RolloutStorage.compute_returns (rollout_storage.py:76-90)
- *   lrl_policy_act         ~ PPO.act teacher path (ppo.py:62-74 -> actor_critic.py:137-147,170-173)
+ *   lrl_ppo_act            ~ PPO.act teacher path (ppo.py:62-74 -> actor_critic.py:137-147,170-173)
  *                            fused with RolloutStorage.add_transitions (rollout_storage.py:57-71)
  *   lrl_ppo_*              ~ PPO.update (ppo.py:94-178): minibatch forward/backward of the PPO loss,
  *                            adaptive-KL LR + clip_grad_norm_ + Adam, the adaptation-module MSE step
@@ -260,31 +260,6 @@ int32_t lrl_gae_partial(const float* rewards, const uint8_t* dones, const float*
                         float* workspace, double* stats /*[3] device*/, void* stream);
 int32_t lrl_adv_normalize(float* advantages, int64_t total, const double* stats /*[3] device*/, void* stream);
 
-/* Teacher-policy MLP stack (actor_critic.py:23-173) in one flat fp32 parameter block. Layer l of a
- * chain is W_l [out,in] row-major followed by b_l [out] (torch nn.Linear layout). */
-typedef struct lrl_mlp_desc {
-  int32_t num_layers;
-  int32_t dims[8];              /* dims[0] = in, dims[l+1] = out of layer l */
-  const float* weight[7];       /* device pointers */
-  const float* bias[7];
-} lrl_mlp_desc;
-
-/* Rollout step of PPO.act (ppo.py:62-74): latent = enc(priv); mu = actor([obs, latent]);
- * a = mu + std * eps; value = critic([obs, latent]); logp = sum log N(a; mu, std).
- * eps [N,12] is given (injected) or drawn from the counter RNG when eps == NULL.
- * Optional storage writes (rollout_storage.py:60-70): if `store` != NULL the transition fields are
- * written to row `store_row` of the [T,N,...] storage arrays. */
-typedef struct lrl_rollout_store {
-  float *obs, *priv, *hist, *actions, *values, *logp, *mu, *sigma;
-  int32_t hist_dim;
-} lrl_rollout_store;
-
-int32_t lrl_policy_act(const lrl_mlp_desc* encoder, const lrl_mlp_desc* actor, const lrl_mlp_desc* critic,
-                       const float* std, const float* obs, const float* priv, const float* hist, int32_t n,
-                       int32_t num_obs, int32_t num_priv, const float* eps, uint64_t seed, uint64_t counter,
-                       float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
-                       int32_t store_row, void* stream);
-
 /* ---------------- PPO update (ppo.py:94-178) ----------------
  * All ActorCritic parameters live in ONE flat fp32 buffer (the nn.Module's tensors are views of it);
  * gradients and the Adam moments (exp_avg / exp_avg_sq) are flat buffers of the same layout.  Actor and
@@ -327,6 +302,23 @@ typedef struct lrl_ppo_ctrl {
   float mb[4];          /* this minibatch: value loss, surrogate loss, adaptation loss, kl */
   float clip_scale, step_size, total_norm, pad;
 } lrl_ppo_ctrl;
+
+/* Rollout step of PPO.act (ppo.py:62-74): latent = enc(priv); mu = actor([obs, latent]);
+ * a = mu + std * eps; value = critic([obs, latent]); logp = sum log N(a; mu, std) — the same fp32-MFMA
+ * GEMM chain as the update's forward, then one head kernel.  eps [n, num_actions] is given (injected)
+ * or drawn from the counter RNG (seed, counter, env row) when eps == NULL.  If `store` != NULL the
+ * transition (obs, priv, hist, actions, values, logp, mu, sigma) is written to row `store_row` of the
+ * [T, n, ...] storage arrays (RolloutStorage.add_transitions, rollout_storage.py:57-71). */
+typedef struct lrl_rollout_store {
+  float *obs, *priv, *hist, *actions, *values, *logp, *mu, *sigma;
+  int32_t hist_dim;
+} lrl_rollout_store;
+
+int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n);
+int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, const float* obs, const float* priv,
+                    const float* hist, int32_t n, const float* eps, uint64_t seed, uint64_t counter, float* actions,
+                    float* mu, float* values, float* logp, const lrl_rollout_store* store, int32_t store_row,
+                    void* workspace, void* stream);
 
 /* Workspace bytes for minibatches of `batch` rows. */
 int64_t lrl_ppo_workspace_bytes(const lrl_ppo_net* net, int32_t batch);

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/lrl.h"
+#include "../../include/lrl_philox.h"
 #include "lrl_gemm.h"
 
 extern "C" int lrl_set_error(int code, const char* msg);
@@ -45,7 +46,7 @@ __global__ void ppo_prep_kernel(const float* __restrict__ obs, const int64_t* __
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * xs) return;
   const int b = (int)(i / xs), c = (int)(i - (int64_t)b * xs);
-  X[i] = c < no ? obs[rows[b] * no + c] : 0.f;
+  X[i] = c < no ? obs[(rows ? rows[b] : (int64_t)b) * no + c] : 0.f;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -251,6 +252,126 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
     float s = 0.f;
     for (int r = 0; r < nrows; ++r) s += SC[r][c];
     P[hp_kl(na) + c] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Rollout head of PPO.act (ppo.py:62-74, actor_critic.py:126-135,170-173): mu = H3a W4a^T + b,
+// value = H3c W4c^T + b, a = mu + std * eps (eps injected or Box-Muller on the counter RNG), log-prob,
+// and the transition row of RolloutStorage.add_transitions (rollout_storage.py:57-71).
+struct ActHeadArgs {
+  const float* h3;  // [n][2*HW]
+  const float *w4a, *b4a, *w4c, *b4c, *stdv;
+  const float *obs, *priv, *hist, *eps;
+  int n, na, no, np;
+  uint64_t seed, counter;
+  float *actions, *mu, *values, *logp;
+  lrl_rollout_store store;
+  int store_row, do_store;
+};
+
+__global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
+  constexpr int HP = 2 * HEAD_W + 1;
+  __shared__ float H[HEAD_ROWS][HP];
+  __shared__ float W4[MAX_ACT + 1][HEAD_W];
+  __shared__ float MU[HEAD_ROWS][MAX_ACT + 1];
+  __shared__ float VP[HEAD_ROWS][4];
+  const int t = threadIdx.x, na = a.na;
+  const int r0 = blockIdx.x * HEAD_ROWS;
+  const int nrows = min(HEAD_ROWS, a.n - r0);
+  {
+    constexpr int NV = HEAD_ROWS * 2 * HEAD_W / 4 / HEAD_THREADS;
+    float4 v[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i = t + u * HEAD_THREADS, r = i / (HEAD_W / 2), c = 4 * (i % (HEAD_W / 2));
+      v[u] = r < nrows ? *reinterpret_cast<const float4*>(a.h3 + (int64_t)(r0 + r) * (2 * HEAD_W) + c)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int i = t + u * HEAD_THREADS, r = i / (HEAD_W / 2), c = 4 * (i % (HEAD_W / 2));
+      H[r][c] = v[u].x; H[r][c + 1] = v[u].y; H[r][c + 2] = v[u].z; H[r][c + 3] = v[u].w;
+    }
+  }
+  for (int i = t; i < (na + 1) * HEAD_W; i += HEAD_THREADS) {
+    const int j = i / HEAD_W, k = i - j * HEAD_W;
+    W4[j][k] = j < na ? a.w4a[j * HEAD_W + k] : a.w4c[k];
+  }
+  __syncthreads();
+  {
+    const int r = t & 63, q = t >> 6;
+    for (int j = q; j < na; j += 4) {
+      float s = 0.f;
+      for (int k = 0; k < HEAD_W; ++k) s = fmaf(H[r][k], W4[j][k], s);
+      MU[r][j] = s + a.b4a[j];
+    }
+    float s = 0.f;
+    for (int k = q * (HEAD_W / 4); k < (q + 1) * (HEAD_W / 4); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
+    VP[r][q] = s;
+  }
+  __syncthreads();
+  const int64_t so = (int64_t)a.store_row * a.n;
+  // one thread per (row, action): sample + write; the per-row log-prob sum is formed after a barrier
+  for (int i = t; i < nrows * na; i += HEAD_THREADS) {
+    const int r = i / na, j = i - r * na, g = r0 + r;
+    float e;
+    if (a.eps) {
+      e = a.eps[(int64_t)g * na + j];
+    } else {  // Box-Muller on the counter RNG (stream POLICY): pairs of actions share one Philox draw
+      lrl_u32x4 u = lrl_philox((uint32_t)g, (uint32_t)a.counter, (LRL_RNG_POLICY << 16) ^ (uint32_t)(a.counter >> 32),
+                               (uint32_t)(j >> 1), a.seed);
+      const float u1 = fmaxf(lrl_u01(u.v[0]), 1e-7f), u2 = lrl_u01(u.v[1]);
+      const float rad = sqrtf(-2.f * logf(u1)), th = 6.283185307179586f * u2;
+      e = (j & 1) ? rad * sinf(th) : rad * cosf(th);
+    }
+    const float m = MU[r][j], sd = a.stdv[j];
+    const float act = m + sd * e;
+    const float d = act - m;
+    MU[r][j] = -(d * d) / (2.f * (sd * sd)) - logf(sd) - LOG_SQRT_2PI;  // log-prob term (mu no longer needed)
+    a.actions[(int64_t)g * na + j] = act;
+    if (a.mu) a.mu[(int64_t)g * na + j] = m;
+    if (a.do_store) {
+      const int64_t o = (so + g) * na + j;
+      a.store.actions[o] = act;
+      a.store.mu[o] = m;
+      a.store.sigma[o] = sd;
+    }
+  }
+  __syncthreads();
+  if (t < nrows) {
+    const int g = r0 + t;
+    float lp = 0.f;
+    for (int j = 0; j < na; ++j) lp += MU[t][j];
+    const float v = ((VP[t][0] + VP[t][1]) + (VP[t][2] + VP[t][3])) + a.b4c[0];
+    if (a.values) a.values[g] = v;
+    if (a.logp) a.logp[g] = lp;
+    if (a.do_store) {
+      a.store.values[so + g] = v;
+      a.store.logp[so + g] = lp;
+    }
+  }
+  if (a.do_store) {  // obs / priv / history rows of this tile: contiguous spans in source and storage
+    const int64_t b = so + r0;
+    for (int i = t; i < nrows * a.no; i += HEAD_THREADS) a.store.obs[b * a.no + i] = a.obs[(int64_t)r0 * a.no + i];
+    for (int i = t; i < nrows * a.np; i += HEAD_THREADS) a.store.priv[b * a.np + i] = a.priv[(int64_t)r0 * a.np + i];
+    if (a.hist && a.store.hist) {
+      const int hd = a.store.hist_dim;
+      const float* src = a.hist + (int64_t)r0 * hd;
+      float* dst = a.store.hist + b * hd;
+      const int cnt = nrows * hd;
+      if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int i = t; i < cnt / 4; i += HEAD_THREADS) d4[i] = s4[i];
+      } else if ((((uintptr_t)src | (uintptr_t)dst) & 7) == 0 && (cnt & 1) == 0) {
+        const float2* s2 = reinterpret_cast<const float2*>(src);
+        float2* d2 = reinterpret_cast<float2*>(dst);
+        for (int i = t; i < cnt / 2; i += HEAD_THREADS) d2[i] = s2[i];
+      } else {
+        for (int i = t; i < cnt; i += HEAD_THREADS) dst[i] = src[i];
+      }
+    }
   }
 }
 
@@ -578,6 +699,73 @@ static void launch_seg(const SegList& L, hipStream_t st) {
 }  // namespace lrl
 
 using namespace lrl;
+
+// rollout forward workspace: X [n][64], HE1, HE2, H1 [n][2 h0], H2, H3
+struct ActPlan {
+  float *xa, *he1, *he2, *h1, *h2, *h3;
+  int64_t bytes;
+};
+static ActPlan make_act_plan(const lrl_ppo_net& n, int rows, char* base) {
+  ActPlan p;
+  int64_t off = 0;
+  auto take = [&](int64_t floats) {
+    float* r = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += ((floats * 4 + 255) / 256) * 256;
+    return r;
+  };
+  const int64_t R = rows;
+  p.xa = take(R * XS);
+  p.he1 = take(R * n.enc_h0);
+  p.he2 = take(R * n.enc_h1);
+  p.h1 = take(R * 2 * n.ac_h0);
+  p.h2 = take(R * 2 * n.ac_h1);
+  p.h3 = take(R * 2 * n.ac_h2);
+  p.bytes = off;
+  return p;
+}
+
+extern "C" int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n) {
+  if (check_net(net) || n <= 0) return -1;
+  return make_act_plan(*net, n, nullptr).bytes;
+}
+
+extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, const float* obs, const float* priv,
+                               const float* hist, int32_t n, const float* eps, uint64_t seed, uint64_t counter,
+                               float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
+                               int32_t store_row, void* workspace, void* stream) {
+  if (int rc = check_net(net)) return rc;
+  if (!params || !obs || !priv || !actions || !workspace || n <= 0)
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: null argument or n <= 0");
+  if (store && (!store->obs || !store->priv || !store->actions || !store->values || !store->logp || !store->mu ||
+                !store->sigma || store->hist_dim < 0))
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: incomplete rollout store");
+  const lrl_ppo_net& nt = *net;
+  ActPlan P = make_act_plan(nt, n, static_cast<char*>(workspace));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  G g{st, nullptr};
+  const float* w = params;
+  const int nx = nt.num_obs + nt.latent;
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
+                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
+  g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
+  g.nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1, nt.enc_h0, true);
+  g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, false);
+  g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, nx, true);
+  g.nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true, 2,
+       nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);
+  g.nt(P.h2, 2 * nt.ac_h1, nullptr, w + nt.w3, nt.ac_h1, P.h3, 2 * nt.ac_h2, w + nt.b3, n, nt.ac_h2, nt.ac_h1, true, 2,
+       nt.ac_h1, (int64_t)nt.ac_h2 * nt.ac_h1, nt.ac_h2, nt.ac_h2);
+  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_act: GEMM launch failed");
+  ActHeadArgs ah{};
+  ah.h3 = P.h3; ah.w4a = w + nt.w4a; ah.b4a = w + nt.b4a; ah.w4c = w + nt.w4c; ah.b4c = w + nt.b4c;
+  ah.stdv = w + nt.std_off; ah.obs = obs; ah.priv = priv; ah.hist = hist; ah.eps = eps;
+  ah.n = n; ah.na = nt.num_actions; ah.no = nt.num_obs; ah.np = nt.num_priv; ah.seed = seed; ah.counter = counter;
+  ah.actions = actions; ah.mu = mu; ah.values = values; ah.logp = logp;
+  if (store) ah.store = *store;
+  ah.store_row = store_row; ah.do_store = store ? 1 : 0;
+  hipLaunchKernelGGL(act_head_kernel, dim3((n + HEAD_ROWS - 1) / HEAD_ROWS), dim3(HEAD_THREADS), 0, st, ah);
+  return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act: launch failed");
+}
 
 extern "C" int64_t lrl_ppo_workspace_bytes(const lrl_ppo_net* net, int32_t batch) {
   if (check_net(net) || batch <= 0) return -1;

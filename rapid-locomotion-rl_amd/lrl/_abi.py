@@ -74,10 +74,6 @@ class LrlTensor(C.Structure):
                 ("strides", C.c_int64 * 4)]
 
 
-class LrlMlpDesc(C.Structure):
-    _fields_ = [("num_layers", i32), ("dims", i32 * 8), ("weight", C.c_void_p * 7), ("bias", C.c_void_p * 7)]
-
-
 class LrlRolloutStore(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("priv", C.c_void_p), ("hist", C.c_void_p), ("actions", C.c_void_p),
                 ("values", C.c_void_p), ("logp", C.c_void_p), ("mu", C.c_void_p), ("sigma", C.c_void_p),
@@ -142,12 +138,13 @@ def lib():
         for name in ["lrl_sim_create", "lrl_sim_destroy", "lrl_sim_tensor", "lrl_sim_step", "lrl_sim_reset_idx",
                      "lrl_sim_set_root_state_indexed", "lrl_sim_set_dof_state_indexed", "lrl_sim_inject_uniforms",
                      "lrl_sim_refresh_rigid_body_state", "lrl_sim_shift_history", "lrl_sim_randomize", "lrl_gae",
-                     "lrl_policy_act", "lrl_abi_version", "lrl_device_count", "lrl_gae_partial", "lrl_adv_normalize",
+                     "lrl_ppo_act", "lrl_abi_version", "lrl_device_count", "lrl_gae_partial", "lrl_adv_normalize",
                      "lrl_sim_reset_idx_ex", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
                      "lrl_gemm_f32"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_ppo_workspace_bytes.restype = C.c_int64
+        L.lrl_ppo_act_workspace_bytes.restype = C.c_int64
         _lib = L
     return _lib
 

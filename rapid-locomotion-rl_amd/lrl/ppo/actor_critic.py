@@ -2,9 +2,9 @@
 
 Parameters live in torch (nn.Module, so state dicts / checkpoints keep the reference's 35-key
 layout, including the duplicate ``encoder.*`` registration of ``env_factor_encoder`` — Q13).  The
-rollout forward of the teacher path (encoder -> actor / critic -> Normal sample -> log-prob) runs as
-ONE fused HIP launch (``lrl_policy_act``, fp32 MFMA); the minibatch update currently uses torch
-autograd on the same parameters.
+rollout forward of the teacher path (encoder -> actor / critic -> Normal sample -> log-prob -> storage
+row) runs natively (``lrl_ppo_act``: fp32-MFMA GEMMs + one head kernel) on a flat parameter buffer
+that the nn.Module's tensors are views of (``flatten_parameters``); the update uses the same buffer.
 """
 import ctypes as C
 
@@ -40,20 +40,6 @@ def _mlp(dims, act):
     return nn.Sequential(*layers)
 
 
-def mlp_desc(seq):
-    """nn.Sequential of Linear/ELU -> lrl_mlp_desc (device pointers of W [out,in], b [out])."""
-    lin = [m for m in seq if isinstance(m, nn.Linear)]
-    d = _abi.LrlMlpDesc()
-    d.num_layers = len(lin)
-    d.dims[0] = lin[0].in_features
-    for i, m in enumerate(lin):
-        assert m.weight.is_contiguous() and m.weight.dtype == torch.float32
-        d.dims[i + 1] = m.out_features
-        d.weight[i] = m.weight.data_ptr()
-        d.bias[i] = m.bias.data_ptr()
-    return d
-
-
 class ActorCritic(nn.Module):
     is_recurrent = False
 
@@ -72,7 +58,6 @@ class ActorCritic(nn.Module):
         self.std = nn.Parameter(AC_Args.init_noise_std * torch.ones(num_actions))
         self.num_obs, self.num_privileged_obs, self.num_actions = num_obs, num_privileged_obs, num_actions
         self.distribution = None
-        self._descs = None
 
     # ---- reference API (torch path; used by the update and for checkpoint-compatible inference) ----
     def reset(self, dones=None):
@@ -191,34 +176,30 @@ class ActorCritic(nn.Module):
                 [net.ac_h0, net.ac_h1, net.ac_h2]:
             raise ValueError("actor and critic must share hidden sizes and take [obs, latent]")
         self._flat, self._net = flat, net
-        self._descs = None
         return net
 
     # ---- fused HIP rollout path ----
-    def _hip_descs(self):
-        ptrs = tuple(p.data_ptr() for p in self.parameters())
-        if self._descs is None or self._descs[0] != ptrs:
-            self._descs = (ptrs, mlp_desc(self.env_factor_encoder), mlp_desc(self.actor_body),
-                           mlp_desc(self.critic_body))
-        return self._descs[1:]
-
     def act_fused(self, obs, priv, hist=None, eps=None, seed=0, counter=0, store=None, store_row=0):
-        """PPO.act teacher path in one launch.  Returns (actions, mu, values [N,1], logp [N])."""
+        """PPO.act teacher path on the flat parameters (lrl_ppo_act: fp32-MFMA GEMM chain + one head
+        kernel that samples, scores and writes the storage row).  Returns (actions, mu, values [N,1], logp [N])."""
         n = obs.shape[0]
         dev = obs.device
         assert obs.is_contiguous() and priv.is_contiguous() and obs.dtype == torch.float32
+        net = self.flatten_parameters()
+        ws = getattr(self, "_act_ws", None)
+        if ws is None or ws[0] != n or ws[1].device != dev:
+            nbytes = _abi.lib().lrl_ppo_act_workspace_bytes(C.byref(net), C.c_int32(n))
+            if nbytes < 0:
+                raise RuntimeError("lrl_ppo_act_workspace_bytes rejected the network")
+            ws = self._act_ws = (n, torch.empty(nbytes, dtype=torch.uint8, device=dev))
         actions = torch.empty(n, self.num_actions, device=dev)
         mu = torch.empty(n, self.num_actions, device=dev)
         values = torch.empty(n, 1, device=dev)
         logp = torch.empty(n, device=dev)
-        enc, act, cri = self._hip_descs()
-        std = self.std.detach()
         ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
         st = C.byref(store) if store is not None else None
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        _abi.check(_abi.lib().lrl_policy_act(C.byref(enc), C.byref(act), C.byref(cri), ptr(std), ptr(obs), ptr(priv),
-                                             ptr(hist), C.c_int32(n), C.c_int32(obs.shape[1]),
-                                             C.c_int32(priv.shape[1]), ptr(eps), C.c_uint64(seed),
-                                             C.c_uint64(counter), ptr(actions), ptr(mu), ptr(values), ptr(logp), st,
-                                             C.c_int32(store_row), stream))
+        _abi.check(_abi.lib().lrl_ppo_act(C.byref(net), ptr(self._flat), ptr(obs), ptr(priv), ptr(hist), C.c_int32(n),
+                                          ptr(eps), C.c_uint64(seed), C.c_uint64(counter), ptr(actions), ptr(mu),
+                                          ptr(values), ptr(logp), st, C.c_int32(store_row), ptr(ws[1]), stream))
         return actions, mu, values, logp

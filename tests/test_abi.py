@@ -34,7 +34,7 @@ def test_struct_layout_matches_header():
 #include <stddef.h>
 #include "lrl.h"
 int main(){printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_model), sizeof(lrl_env_params), sizeof(lrl_tensor),
- offsetof(lrl_env_params, noise_vec), offsetof(lrl_env_params, max_episode_length), sizeof(lrl_mlp_desc));
+ offsetof(lrl_env_params, noise_vec), offsetof(lrl_env_params, max_episode_length), sizeof(lrl_rollout_store));
 printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_ppo_net), offsetof(lrl_ppo_net, total), sizeof(lrl_ppo_batch),
  offsetof(lrl_ppo_batch, batch), sizeof(lrl_ppo_hparams), sizeof(lrl_ppo_ctrl));return 0;}
 """
@@ -45,7 +45,7 @@ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_ppo_net), offsetof(lrl_ppo_net, t
     out = [int(x) for x in subprocess.check_output([exe]).split()]
     assert out == [C.sizeof(_abi.LrlModel), C.sizeof(_abi.LrlEnvParams), C.sizeof(_abi.LrlTensor),
                    _abi.LrlEnvParams.noise_vec.offset, _abi.LrlEnvParams.max_episode_length.offset,
-                   C.sizeof(_abi.LrlMlpDesc), C.sizeof(_abi.LrlPpoNet), _abi.LrlPpoNet.total.offset,
+                   C.sizeof(_abi.LrlRolloutStore), C.sizeof(_abi.LrlPpoNet), _abi.LrlPpoNet.total.offset,
                    C.sizeof(_abi.LrlPpoBatch), _abi.LrlPpoBatch.batch.offset, C.sizeof(_abi.LrlPpoHparams),
                    _abi.PPO_CTRL_BYTES]
 
