@@ -26,9 +26,31 @@
 #include "lrl_kparams.h"
 
 #define WAVE 64
+// envs per workgroup (one lane each, one wave): fewer than 64 spreads the 4096 envs over more CUs and
+// shrinks the per-wave union of active contact spheres the divergent solver loops walk
+#ifndef LRL_ENV_EPB
+#define LRL_ENV_EPB 64
+#endif
+#define EPB LRL_ENV_EPB
 #define NSF 13  // LDS fields per contact sphere
 
 namespace lrl {
+
+// Phase timers (build with -DLRL_ENV_PROFILE; read with lrl_debug_env_profile): per-wave shader-clock
+// cycles of the step kernel's phases, summed over waves.
+#ifdef LRL_ENV_PROFILE
+__device__ unsigned long long g_env_prof[16];
+#define LRL_PROF_DECL unsigned long long prof_t = clock64();
+#define LRL_PROF(i)                                   \
+  {                                                   \
+    const unsigned long long t_ = clock64();          \
+    prof[i] += t_ - prof_t;                           \
+    prof_t = t_;                                      \
+  }
+#else
+#define LRL_PROF_DECL
+#define LRL_PROF(i)
+#endif
 
 struct V3 {
   float x, y, z;
@@ -148,9 +170,9 @@ __device__ __forceinline__ float sv_get(const SV& s, int r) {
 struct Lds {
   float* base;     // leg blocks, then contact rows
   int sph_off;     // field offset of the contact rows
-  __device__ __forceinline__ float& leg(int l, int f) const { return base[(l * LEGF + f) * WAVE + threadIdx.x]; }
+  __device__ __forceinline__ float& leg(int l, int f) const { return base[(l * LEGF + f) * EPB + threadIdx.x]; }
   __device__ __forceinline__ float& sph(int s, int f) const {
-    return base[(sph_off + s * NSF + f) * WAVE + threadIdx.x];
+    return base[(sph_off + s * NSF + f) * EPB + threadIdx.x];
   }
   __device__ __forceinline__ V3 a(int l, int j) const { return v3(leg(l, 3 * j), leg(l, 3 * j + 1), leg(l, 3 * j + 2)); }
   __device__ __forceinline__ V3 o(int l, int j) const {
@@ -369,7 +391,8 @@ struct Body {  // per-lane env state during the step
 // One physics sub-step.  Contact impulses of the sub-step stay in the LDS rows (fields 10..12).
 // ------------------------------------------------------------------------------------------------
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau, float mb, const float* Ib, V3 cb,
-                        float mu, float rest, const Lds& M, uint64_t& active) {
+                        float mu, float rest, const Lds& M, uint64_t& active, unsigned long long* prof) {
+  LRL_PROF_DECL
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
   const lrl_env_params& P = K->p;
   const float dt = P.sim_dt;
@@ -491,6 +514,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     M.leg(l, 44) = sdot(S[2], Fc2);
     Cb = Cb + Fc0;
   }
+  LRL_PROF(0)  // kinematics, composite inertias, leg blocks, RNEA, contact detection
   // base block A (6x6) + Schur complement, Cholesky in registers
   Sch[LI(0, 0)] += A.i[0]; Sch[LI(1, 1)] += A.i[1]; Sch[LI(2, 2)] += A.i[2];
   Sch[LI(1, 0)] += A.i[3]; Sch[LI(2, 0)] += A.i[4]; Sch[LI(2, 1)] += A.i[5];
@@ -529,6 +553,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         nu[6 + 3 * l + j] += dt * (M.leg(l, 42 + j) - kx);
       }
   }
+  LRL_PROF(1)  // Schur complement factor / inverse, free acceleration
   // contact solve.  Start state: v_b0 = free base velocity, qd0 = free joint rates (LDS), Y = 0.
   float vb0[6], vbc[6];
 #pragma unroll
@@ -559,11 +584,13 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
                         v3(M.sph(s, 11), M.sph(s, 12), M.sph(s, 10)), vbc);
     }
   }
+  LRL_PROF(2)  // Delassus rows + warm start
   // projected Gauss-Seidel, sphere order = model order (base, legs 0..3)
   for (int it = 0; it < P.solver_iterations; ++it)
     for (int s = 0; s < K->num_spheres; ++s)
       if (__any((int)((active >> s) & 1ull)))
         if ((active >> s) & 1ull) contact_pgs(M, Sch, R, s, K->sph_leg[s], K->sph_link[s], mu, vbc, vb0);
+  LRL_PROF(3)  // PGS iterations
   // materialise the lazily propagated joint rates
 #pragma unroll
   for (int r = 0; r < 6; ++r) nu[r] = vbc[r];
@@ -605,6 +632,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   const V3 V = mul(R2, v3(nu[3], nu[4], nu[5]) + cross(w, cb)), Wv = mul(R2, w);
   st.V[0] = V.x; st.V[1] = V.y; st.V[2] = V.z;
   st.W[0] = Wv.x; st.W[1] = Wv.y; st.W[2] = Wv.z;
+  LRL_PROF(4)  // integration
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -645,13 +673,13 @@ __device__ __forceinline__ float nrm3(float x, float y, float z) { return sqrtf(
 // ------------------------------------------------------------------------------------------------
 // the fused step kernel
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
+__global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict__ K, KState S,
                                                         const float* __restrict__ actions_in, uint32_t flags,
                                                         int64_t step_counter) {
   extern __shared__ float lds[];
   const lrl_env_params& P = K->p;
   const int lane = threadIdx.x;
-  const int e = blockIdx.x * WAVE + lane;
+  const int e = blockIdx.x * EPB + lane;
   const int N = S.stride;
   const bool valid = e < S.n;
   const uint64_t genv = (uint64_t)(S.env_offset + e);
@@ -693,11 +721,16 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   const float rest = 0.5f * (S.restitution[e] + P.ground_restitution);
   const bool physics = flags & LRL_STEP_PHYSICS;
   uint64_t active = 0;
-
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  LRL_PROF_DECL
+  LRL_PROF(5)  // state loads
   for (int sub = 0; sub < P.decimation; ++sub) {
     compute_torques(P, act, st.q, st.qd, S.kp + e, S.kd + e, S.motor_strength + e, N, tau);
-    if (physics) substep(K, st, tau, mb, Ib, cb, mu, rest, M, active);
+    if (physics) substep(K, st, tau, mb, Ib, cb, mu, rest, M, active, prof);
   }
+#ifdef LRL_ENV_PROFILE
+  prof_t = clock64();
+#endif
 
   // ---- contact forces per body (last sub-step) and the contact-derived signals ----
   int rst = 0;
@@ -909,7 +942,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   // observations -> LDS tile [lane][NO]
   const int NO = P.num_obs;
   float* otile = lds;                  // [64][NO]
-  float* ptile = lds + WAVE * NO;      // [64][18]
+  float* ptile = lds + EPB * NO;       // [EPB][18]
   {
     float* ob = otile + lane * NO;
     int o = 0;
@@ -992,32 +1025,69 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   S.reset[e] = (uint8_t)rst;
   S.rew[e] = rew;
 
+  LRL_PROF(6)  // contact forces + post_physics_step + SoA write-back
   // ---- AoS tiles (obs, priv) and the history shift: coalesced over the wave's contiguous rows ----
   __syncthreads();
-  const size_t row0 = (size_t)blockIdx.x * WAVE;
+  const size_t row0 = (size_t)blockIdx.x * EPB;
   {
     float* og = S.obs + row0 * NO;
-    for (int i = lane; i < WAVE * NO; i += WAVE) og[i] = otile[i];
+    for (int i = lane; i < EPB * NO; i += EPB) og[i] = otile[i];
     float* pgp = S.priv + row0 * LRL_NUM_PRIV;
-    for (int i = lane; i < WAVE * LRL_NUM_PRIV; i += WAVE) pgp[i] = ptile[i];
+    for (int i = lane; i < EPB * LRL_NUM_PRIV; i += EPB) pgp[i] = ptile[i];
   }
   if (flags & LRL_STEP_HISTORY) {
     const int H = K->num_history * NO;
     float* hg = S.hist + row0 * H;
     // in place: new[r][k] = old[r][k + NO] (k < H - NO) else obs[r][k - (H - NO)].  Reads run ahead of
     // writes within a row, and each wave-iteration reads only addresses above the ones it writes.
-    const int total = WAVE * H;
-    for (int i0 = 0; i0 < total; i0 += WAVE) {
-      int i = i0 + lane;
-      int r = i / H, k = i - r * H;
-      float v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
+    // Chunks of HU wave-iterations: all HU loads of a chunk are issued before any of its stores (one
+    // latency per chunk instead of one per element); a chunk's reads lie above every earlier write.
+    constexpr int HU = 16;
+    const int total = EPB * H;
+    int i0 = 0;
+    for (; i0 + HU * EPB <= total; i0 += HU * EPB) {
+      float v[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int i = i0 + u * EPB + lane;
+        const int r = i / H, k = i - r * H;
+        v[u] = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int u = 0; u < HU; ++u) hg[i0 + u * EPB + lane] = v[u];
+    }
+    for (; i0 < total; i0 += EPB) {
+      const int i = i0 + lane;
+      const int r = i / H, k = i - r * H;
+      const float v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
       __builtin_amdgcn_wave_barrier();
       hg[i] = v;
     }
   }
+  LRL_PROF(7)  // obs / priv tiles + history shift
+#ifdef LRL_ENV_PROFILE
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_env_prof[i], prof[i]);
+#endif
 }
 
 }  // namespace lrl
+
+extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
+#ifdef LRL_ENV_PROFILE
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 8;
+#else
+  (void)out;
+  (void)reset;
+  return 0;
+#endif
+}
 
 extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
   return hipFuncSetAttribute((const void*)lrl::env_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
@@ -1025,8 +1095,8 @@ extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
 
 extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int lds_bytes, const float* actions,
                                           uint32_t flags, int64_t step_counter, hipStream_t stream) {
-  int blocks = S->stride / WAVE;
-  hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
+  int blocks = S->stride / EPB;
+  hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(EPB), lds_bytes, stream, K, *S, actions, flags,
                      step_counter);
   return hipGetLastError();
 }

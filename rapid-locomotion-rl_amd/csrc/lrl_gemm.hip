@@ -51,50 +51,69 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ src, int vec) 
 }
 
 // ---- global -> register staging of one BK slice ----
-// k-contiguous operand X(r, k) = P[row(r) * ld + k]: item i covers (r = i / KQ, k = 4 (i % KQ) .. +3).
+// k-contiguous operand X(r, k) = P[row(r) * ld + k]: item i covers (r = i / KQ, k = 4 (i % KQ) .. +3); the
+// row pointers (through the gather list when there is one) are resolved once per workgroup.
 // r-contiguous operand X(r, k) = P[krow(k) * ld + r]: item i covers (k = i / (R/4), r = 4 (i % (R/4)) .. +3).
 template <int R, int NI, bool RCONTIG>
-__device__ __forceinline__ void stage_load(float4 (&reg)[NI], const float* __restrict__ P, int64_t ld,
-                                           const int64_t* __restrict__ rows, int vec, int r0, int R_lim, int k0,
-                                           int k_lim) {
-  constexpr int ITEMS = R * GBK / 4;
+struct Stager {
+  static constexpr int ITEMS = R * GBK / 4;
+  const float* rowp[NI];  // k-contiguous: source row (nullptr: outside the tile / matrix)
+  const float* P;
+  const int64_t* rows;
+  int64_t ld;
+  int vec, r0, R_lim;
+
+  __device__ __forceinline__ void init(const float* P_, int64_t ld_, const int64_t* rows_, int vec_, int r0_,
+                                       int R_lim_) {
+    P = P_; ld = ld_; rows = rows_; vec = vec_; r0 = r0_; R_lim = R_lim_;
+    if (!RCONTIG) {
 #pragma unroll
-  for (int u = 0; u < NI; ++u) {
-    const int i = threadIdx.x + u * GTHREADS;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ITEMS % GTHREADS != 0 && i >= ITEMS) {
-    } else if (!RCONTIG) {
-      const int r = i / KQ, k = k0 + 4 * (i % KQ);
-      const int gr = r0 + r;
-      if (gr < R_lim) {
-        const int64_t row = rows ? rows[gr] : (int64_t)gr;
-        const float* src = P + row * ld + k;
-        if (k + 3 < k_lim) {
-          v = load4(src, vec);
-        } else {
-          if (k + 0 < k_lim) v.x = src[0];
-          if (k + 1 < k_lim) v.y = src[1];
-          if (k + 2 < k_lim) v.z = src[2];
-        }
-      }
-    } else {
-      const int r = 4 * (i % (R / 4)), k = k0 + i / (R / 4);
-      const int gr = r0 + r;
-      if (k < k_lim) {
-        const int64_t row = rows ? rows[k] : (int64_t)k;
-        const float* src = P + row * ld + gr;
-        if (gr + 3 < R_lim) {
-          v = load4(src, vec);
-        } else {
-          if (gr + 0 < R_lim) v.x = src[0];
-          if (gr + 1 < R_lim) v.y = src[1];
-          if (gr + 2 < R_lim) v.z = src[2];
-        }
+      for (int u = 0; u < NI; ++u) {
+        const int i = threadIdx.x + u * GTHREADS;
+        const int gr = r0 + i / KQ;
+        rowp[u] = nullptr;
+        if ((ITEMS % GTHREADS == 0 || i < ITEMS) && gr < R_lim)
+          rowp[u] = P + (rows ? rows[gr] : (int64_t)gr) * ld + 4 * (i % KQ);
       }
     }
-    reg[u] = v;
   }
-}
+
+  __device__ __forceinline__ void load(float4 (&reg)[NI], int k0, int k_lim) const {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = threadIdx.x + u * GTHREADS;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!RCONTIG) {
+        const int k = k0 + 4 * (i % KQ);
+        if (rowp[u]) {
+          const float* src = rowp[u] + k0;
+          if (k + 3 < k_lim) {
+            v = load4(src, vec);
+          } else {
+            if (k + 0 < k_lim) v.x = src[0];
+            if (k + 1 < k_lim) v.y = src[1];
+            if (k + 2 < k_lim) v.z = src[2];
+          }
+        }
+      } else if (ITEMS % GTHREADS == 0 || i < ITEMS) {
+        const int r = 4 * (i % (R / 4)), k = k0 + i / (R / 4);
+        const int gr = r0 + r;
+        if (k < k_lim) {
+          const int64_t row = rows ? rows[k] : (int64_t)k;
+          const float* src = P + row * ld + gr;
+          if (gr + 3 < R_lim) {
+            v = load4(src, vec);
+          } else {
+            if (gr + 0 < R_lim) v.x = src[0];
+            if (gr + 1 < R_lim) v.y = src[1];
+            if (gr + 2 < R_lim) v.z = src[2];
+          }
+        }
+      }
+      reg[u] = v;
+    }
+  }
+};
 
 template <int R, int PAD, int NI, bool RCONTIG>
 __device__ __forceinline__ void stage_store(float (*S)[R + PAD], const float4 (&reg)[NI]) {
@@ -147,10 +166,14 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   float bsum = 0.f;
 
   float4 ra[T::NA], rb[T::NB];
+  Stager<BM, T::NA, T::AMC> sa;
+  Stager<BN, T::NB, T::BNC> sb;
+  sa.init(A, p.lda, a_rows, p.avec, m0, p.M);
+  sb.init(B, p.ldb, b_rows, p.bvec, n0, p.N);
   int k0 = kbeg;
   if (k0 < kend) {
-    stage_load<BM, T::NA, T::AMC>(ra, A, p.lda, a_rows, p.avec, m0, p.M, k0, kend);
-    stage_load<BN, T::NB, T::BNC>(rb, B, p.ldb, b_rows, p.bvec, n0, p.N, k0, kend);
+    sa.load(ra, k0, kend);
+    sb.load(rb, k0, kend);
     stage_store<BM, T::PA, T::NA, T::AMC>(As[0], ra);
     stage_store<BN, T::PB, T::NB, T::BNC>(Bs[0], rb);
   }
@@ -159,25 +182,33 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   for (; k0 < kend; k0 += GBK) {
     const int kn = k0 + GBK;
     if (kn < kend) {
-      stage_load<BM, T::NA, T::AMC>(ra, A, p.lda, a_rows, p.avec, m0, p.M, kn, kend);
-      stage_load<BN, T::NB, T::BNC>(rb, B, p.ldb, b_rows, p.bvec, n0, p.N, kn, kend);
+      sa.load(ra, kn, kend);
+      sb.load(rb, kn, kend);
     }
     if (do_bsum && threadIdx.x < BM) {
 #pragma unroll
       for (int k = 0; k < GBK; ++k) bsum += As[buf][k][threadIdx.x];
     }
+    // all operands of the slice first (GBK/2 x (TM + TN) ds_read_b32), then the MFMAs back to back, so no
+    // MFMA waits on an LDS read issued right before it
+    float a[GBK / 2][TM], b[GBK / 2][TN];
 #pragma unroll
-    for (int kk = 0; kk < GBK; kk += 2) {
-      float a[TM], b[TN];
+    for (int kk = 0; kk < GBK / 2; ++kk) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[buf][kk + h][wm + 32 * i + li];
+      for (int i = 0; i < TM; ++i) a[kk][i] = As[buf][2 * kk + h][wm + 32 * i + li];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[buf][kk + h][wn + 32 * j + li];
+      for (int j = 0; j < TN; ++j) b[kk][j] = Bs[buf][2 * kk + h][wn + 32 * j + li];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < GBK / 2; ++kk)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+    // keep the scheduler from sinking the LDS reads back next to their MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     if (kn < kend) {
       stage_store<BM, T::PA, T::NA, T::AMC>(As[buf ^ 1], ra);
       stage_store<BN, T::PB, T::NB, T::BNC>(Bs[buf ^ 1], rb);

@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "liblrl.so")
+# LRL_LIB overrides the library path (instrumented development builds); the default is the in-tree build
+LIB_PATH = os.environ.get("LRL_LIB") or os.path.join(os.path.dirname(_HERE), "csrc", "liblrl.so")
 
 MAX_BODIES, MAX_SPHERES, NUM_DOF, NUM_LEGS, MAX_OBS, MAX_REWARD_TERMS, NUM_PRIV = 20, 40, 12, 4, 64, 24, 18
 f32, i32, u32 = C.c_float, C.c_int32, C.c_uint32

@@ -18,6 +18,8 @@ SHAPES = [
     ("dLat     NN 1024->18", 2, 0, B, 18, 1024),
     ("dW2      TN 256x512", 3, 4, 256, 512, B),
     ("dWD1     TN 256x630 gather", 3, 4, 256, 630, B),
+    ("long-K   NT 4096->256", 0, 2, B, 256, 4096),
+    ("square   NT 4096^3", 0, 0, 4096, 4096, 4096),
 ]
 
 
