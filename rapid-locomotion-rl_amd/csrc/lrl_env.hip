@@ -26,12 +26,13 @@
 #include "lrl_kparams.h"
 
 #define WAVE 64
-// envs per workgroup (one lane each, one wave): fewer than 64 spreads the 4096 envs over more CUs and
-// shrinks the per-wave union of active contact spheres the divergent solver loops walk
-#ifndef LRL_ENV_EPB
-#define LRL_ENV_EPB 64
-#endif
-#define EPB LRL_ENV_EPB
+// Quad layout: 4 lanes per env (lane & 3 = the leg it owns), 16 envs per single-wave workgroup.  The leg
+// work (kinematics, composite inertias, leg blocks, RNEA, contact detection and Delassus rows of the leg's
+// spheres, warm-start impulses) runs leg-parallel; the base quantities are summed over the 4 lanes with
+// cross-lane shuffles; the Gauss-Seidel sweep and the integration run redundantly in the 4 lanes (so
+// every lane holds the full env state); post-physics runs in lane 0 of each env.
+#define QL 4
+#define ENVS (WAVE / QL)
 #define NSF 13  // LDS fields per contact sphere
 
 namespace lrl {
@@ -168,12 +169,11 @@ __device__ __forceinline__ float sv_get(const SV& s, int r) {
 #define LI(r, c) ((r) * ((r) + 1) / 2 + (c))
 
 struct Lds {
-  float* base;     // leg blocks, then contact rows
+  float* base;     // leg blocks, then contact rows: [field][env slot] columns shared by the env's 4 lanes
   int sph_off;     // field offset of the contact rows
-  __device__ __forceinline__ float& leg(int l, int f) const { return base[(l * LEGF + f) * EPB + threadIdx.x]; }
-  __device__ __forceinline__ float& sph(int s, int f) const {
-    return base[(sph_off + s * NSF + f) * EPB + threadIdx.x];
-  }
+  int es;          // env slot of this lane inside the workgroup
+  __device__ __forceinline__ float& leg(int l, int f) const { return base[(l * LEGF + f) * ENVS + es]; }
+  __device__ __forceinline__ float& sph(int s, int f) const { return base[(sph_off + s * NSF + f) * ENVS + es]; }
   __device__ __forceinline__ V3 a(int l, int j) const { return v3(leg(l, 3 * j), leg(l, 3 * j + 1), leg(l, 3 * j + 2)); }
   __device__ __forceinline__ V3 o(int l, int j) const {
     return v3(leg(l, 9 + 3 * j), leg(l, 9 + 3 * j + 1), leg(l, 9 + 3 * j + 2));
@@ -390,8 +390,29 @@ struct Body {  // per-lane env state during the step
 // ------------------------------------------------------------------------------------------------
 // One physics sub-step.  Contact impulses of the sub-step stay in the LDS rows (fields 10..12).
 // ------------------------------------------------------------------------------------------------
+// sum of a value over the 4 lanes of an env (xor-shuffles inside the quad)
+__device__ __forceinline__ float quad_sum(float v) {
+  v += __shfl_xor(v, 1, WAVE);
+  v += __shfl_xor(v, 2, WAVE);
+  return v;
+}
+__device__ __forceinline__ uint64_t quad_or(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo |= __shfl_xor(lo, 1, WAVE);
+  hi |= __shfl_xor(hi, 1, WAVE);
+  lo |= __shfl_xor(lo, 2, WAVE);
+  hi |= __shfl_xor(hi, 2, WAVE);
+  return ((uint64_t)hi << 32) | lo;
+}
+// lane of the quad that owns sphere s: its leg, or round-robin for the base spheres
+__device__ __forceinline__ int sph_owner(const KParams* __restrict__ K, int s) {
+  const int l = K->sph_leg[s];
+  return l >= 0 ? l : (s & 3);
+}
+
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau, float mb, const float* Ib, V3 cb,
-                        float mu, float rest, const Lds& M, uint64_t& active, unsigned long long* prof) {
+                        float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
+                        unsigned long long* prof) {
   LRL_PROF_DECL
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
   const lrl_env_params& P = K->p;
@@ -443,10 +464,14 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.sph(s, 9) = tgt;
     }
   };
-  for (int s = 0; s < K->base_sph_end; ++s) detect(s, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2]), -1, 0);
+  for (int s = ql; s < K->base_sph_end; s += QL)
+    detect(s, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2]), -1, 0);
 
-#pragma unroll 1
-  for (int l = 0; l < 4; ++l) {
+  // ---- this lane's leg ----
+  SI Aleg;     // composite inertia of the leg about the base origin
+  SV Cleg;     // its RNEA force on the base
+  {
+    const int l = ql;
     const KLeg& kl = K->leg[l];
     M3 Rp;
 #pragma unroll
@@ -475,7 +500,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       op = o;
     }
     const SI Ic2 = Ij[2], Ic1 = siadd(Ij[1], Ic2), Ic0 = siadd(Ij[0], Ic1);
-    A = siadd(A, Ic0);
+    Aleg = Ic0;
     const SV F0 = simul(Ic0, S[0]), F1 = simul(Ic1, S[1]), F2 = simul(Ic2, S[2]);
     float D[6] = {sdot(S[0], F0), sdot(S[1], F1), sdot(S[2], F2), sdot(S[0], F1), sdot(S[0], F2), sdot(S[1], F2)};
     float Di[6];
@@ -512,8 +537,18 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     M.leg(l, 42) = sdot(S[0], Fc0);
     M.leg(l, 43) = sdot(S[1], Fc1);
     M.leg(l, 44) = sdot(S[2], Fc2);
-    Cb = Cb + Fc0;
+    Cleg = Fc0;
   }
+  // ---- quad reductions: legs -> base ----
+#pragma unroll
+  for (int k = 0; k < 21; ++k) Sch[k] = quad_sum(Sch[k]);
+  A.m += quad_sum(Aleg.m);
+  A.h = A.h + v3(quad_sum(Aleg.h.x), quad_sum(Aleg.h.y), quad_sum(Aleg.h.z));
+#pragma unroll
+  for (int k = 0; k < 6; ++k) A.i[k] += quad_sum(Aleg.i[k]);
+  Cb = Cb + SV{v3(quad_sum(Cleg.a.x), quad_sum(Cleg.a.y), quad_sum(Cleg.a.z)),
+               v3(quad_sum(Cleg.l.x), quad_sum(Cleg.l.y), quad_sum(Cleg.l.z))};
+  active = quad_or(active);
   LRL_PROF(0)  // kinematics, composite inertias, leg blocks, RNEA, contact detection
   // base block A (6x6) + Schur complement, Cholesky in registers
   Sch[LI(0, 0)] += A.i[0]; Sch[LI(1, 1)] += A.i[1]; Sch[LI(2, 2)] += A.i[2];
@@ -524,19 +559,26 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   Sch[LI(3, 3)] += A.m; Sch[LI(4, 4)] += A.m; Sch[LI(5, 5)] += A.m;
   chol6(Sch);
   chol_to_inverse6(Sch);  // Sch now holds S^-1
-  // free acceleration: M acc = [0; tau] - C
+  // free acceleration: M acc = [0; tau] - C  (leg terms in the owner lane, summed over the quad)
   {
-    float pb[6] = {-Cb.a.x, -Cb.a.y, -Cb.a.z, -Cb.l.x, -Cb.l.y, -Cb.l.z};
+    float pb[6];
+    {
+      const int l = ql;
+      const V3 rl = v3(pick12(tau, 3 * l) - M.leg(l, 42), pick12(tau, 3 * l + 1) - M.leg(l, 43),
+                       pick12(tau, 3 * l + 2) - M.leg(l, 44));
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      const V3 rl = v3(tau[3 * l] - M.leg(l, 42), tau[3 * l + 1] - M.leg(l, 43), tau[3 * l + 2] - M.leg(l, 44));
-#pragma unroll
-      for (int r = 0; r < 6; ++r) pb[r] -= M.Kx(l, 0, r) * rl.x + M.Kx(l, 1, r) * rl.y + M.Kx(l, 2, r) * rl.z;
+      for (int r = 0; r < 6; ++r) pb[r] = -(M.Kx(l, 0, r) * rl.x + M.Kx(l, 1, r) * rl.y + M.Kx(l, 2, r) * rl.z);
       const V3 y = di_mul(M, l, rl);
       M.leg(l, 42) = y.x;  // reuse as y_l
       M.leg(l, 43) = y.y;
       M.leg(l, 44) = y.z;
     }
+    {
+      const float cbv[6] = {Cb.a.x, Cb.a.y, Cb.a.z, Cb.l.x, Cb.l.y, Cb.l.z};
+#pragma unroll
+      for (int r = 0; r < 6; ++r) pb[r] = quad_sum(pb[r]) - cbv[r];
+    }
+    __syncthreads();  // leg blocks of the other lanes are read below
     float xb[6];
     sym6mul(Sch, pb, xb);
 #pragma unroll
@@ -565,31 +607,50 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.leg(l, 45 + j) = nu[6 + 3 * l + j];
       M.leg(l, 48 + j) = 0.f;
     }
-  // Delassus rows of the active spheres (only spheres active in some lane of the wave are visited)
-  for (int s = 0; s < K->num_spheres; ++s)
-    if (__any((int)((active >> s) & 1ull)))
-      if ((active >> s) & 1ull) contact_setup(M, Sch, R, s, K->sph_leg[s], K->sph_link[s]);
-  // warm start: spheres in contact in the previous sub-step keep their impulse (world frame)
-  for (int s = 0; s < K->num_spheres; ++s) {
-    const bool act = (active >> s) & 1ull, warm = act && ((prev_active >> s) & 1ull);
-    if (__any((int)act)) {
-      if (act && !warm) {
-        M.sph(s, 10) = 0.f;
-        M.sph(s, 11) = 0.f;
-        M.sph(s, 12) = 0.f;
-      }
-      if (__any((int)warm))
-        if (warm)
-          apply_impulse(M, Sch, R, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), K->sph_leg[s], K->sph_link[s],
-                        v3(M.sph(s, 11), M.sph(s, 12), M.sph(s, 10)), vbc);
+  // Delassus rows of the active spheres, each in the lane that owns the sphere (only spheres active in some
+  // env of the wave are visited)
+  // (each lane walks its own active spheres: the 4 legs' rows are built at the same time)
+  for (uint64_t m = active & own; __any((int)(m != 0ull));) {
+    if (m) {
+      const int s = __builtin_ctzll(m);
+      m &= m - 1ull;
+      contact_setup(M, Sch, R, s, K->sph_leg[s], K->sph_link[s]);
     }
   }
+  // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
+  // lanes apply them in parallel and the base-velocity changes are summed over the quad
+  {
+    float dvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (uint64_t m = active & own & ~prev_active; m; m &= m - 1ull) {
+      const int s = __builtin_ctzll(m);
+      M.sph(s, 10) = 0.f;
+      M.sph(s, 11) = 0.f;
+      M.sph(s, 12) = 0.f;
+    }
+    for (uint64_t m = active & own & prev_active; __any((int)(m != 0ull));) {
+      if (m) {
+        const int s = __builtin_ctzll(m);
+        m &= m - 1ull;
+        apply_impulse(M, Sch, R, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), K->sph_leg[s], K->sph_link[s],
+                      v3(M.sph(s, 11), M.sph(s, 12), M.sph(s, 10)), dvb);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) vbc[r] += quad_sum(dvb[r]);
+  }
+  __syncthreads();  // contact rows and leg accumulators of every owner lane are read by the whole quad
   LRL_PROF(2)  // Delassus rows + warm start
   // projected Gauss-Seidel, sphere order = model order (base, legs 0..3)
+  // (each env walks its own active spheres in model order; the wave runs max-over-envs sphere updates,
+  // not the union of the 16 envs' contact sets)
   for (int it = 0; it < P.solver_iterations; ++it)
-    for (int s = 0; s < K->num_spheres; ++s)
-      if (__any((int)((active >> s) & 1ull)))
-        if ((active >> s) & 1ull) contact_pgs(M, Sch, R, s, K->sph_leg[s], K->sph_link[s], mu, vbc, vb0);
+    for (uint64_t m = active; __any((int)(m != 0ull));) {
+      if (m) {
+        const int s = __builtin_ctzll(m);
+        m &= m - 1ull;
+        contact_pgs(M, Sch, R, s, K->sph_leg[s], K->sph_link[s], mu, vbc, vb0);
+      }
+    }
   LRL_PROF(3)  // PGS iterations
   // materialise the lazily propagated joint rates
 #pragma unroll
@@ -673,13 +734,14 @@ __device__ __forceinline__ float nrm3(float x, float y, float z) { return sqrtf(
 // ------------------------------------------------------------------------------------------------
 // the fused step kernel
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict__ K, KState S,
+__global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
                                                         const float* __restrict__ actions_in, uint32_t flags,
                                                         int64_t step_counter) {
   extern __shared__ float lds[];
   const lrl_env_params& P = K->p;
   const int lane = threadIdx.x;
-  const int e = blockIdx.x * EPB + lane;
+  const int es = lane >> 2, ql = lane & 3;  // env slot, owned leg
+  const int e = blockIdx.x * ENVS + es;
   const int N = S.stride;
   const bool valid = e < S.n;
   const uint64_t genv = (uint64_t)(S.env_offset + e);
@@ -707,7 +769,7 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
       act[j] = fminf(fmaxf(a, -c), c);
     }
   }
-  const Lds M{lds, 4 * LEGF};  // leg blocks first, then the contact rows
+  const Lds M{lds, 4 * LEGF, es};  // leg blocks first, then the contact rows
   const float payload = S.payload[e];
   const V3 cb = v3(S.com[e], S.com[N + e], S.com[2 * N + e]);
   const float mb = K->base_mass + payload;
@@ -721,12 +783,15 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
   const float rest = 0.5f * (S.restitution[e] + P.ground_restitution);
   const bool physics = flags & LRL_STEP_PHYSICS;
   uint64_t active = 0;
+  uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
+  for (int s = 0; s < K->num_spheres; ++s)
+    if (sph_owner(K, s) == ql) own |= 1ull << s;
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   LRL_PROF_DECL
   LRL_PROF(5)  // state loads
   for (int sub = 0; sub < P.decimation; ++sub) {
     compute_torques(P, act, st.q, st.qd, S.kp + e, S.kd + e, S.motor_strength + e, N, tau);
-    if (physics) substep(K, st, tau, mb, Ib, cb, mu, rest, M, active, prof);
+    if (physics) substep(K, st, tau, mb, Ib, cb, mu, rest, M, active, ql, own, prof);
   }
 #ifdef LRL_ENV_PROFILE
   prof_t = clock64();
@@ -751,9 +816,11 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
       fx *= inv_dt;
       fy *= inv_dt;
       fz *= inv_dt;
-      S.contact[(3 * b) * N + e] = fx;
-      S.contact[(3 * b + 1) * N + e] = fy;
-      S.contact[(3 * b + 2) * N + e] = fz;
+      if (ql == 0) {
+        S.contact[(3 * b) * N + e] = fx;
+        S.contact[(3 * b + 1) * N + e] = fy;
+        S.contact[(3 * b + 2) * N + e] = fz;
+      }
     } else {
       fx = S.contact[(3 * b) * N + e];
       fy = S.contact[(3 * b + 1) * N + e];
@@ -768,6 +835,11 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
       if (fs == f) { ff[f][0] = fx; ff[f][1] = fy; ff[f][2] = fz; }
   }
   __syncthreads();  // LDS contact rows are dead from here on; the obs tile reuses them
+  const int NO = P.num_obs;
+  float* otile = lds;                    // [ENVS][NO]
+  float* ptile = lds + ENVS * NO;        // [ENVS][18]
+  // post-physics, observations and the state write-back: lane 0 of each env
+  if (ql == 0) {
 
   // ---- post_physics_step ----
   int32_t eplen = S.episode_length[e] + 1;
@@ -939,12 +1011,9 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
   S.command_sums[(KS + 3) * N + e] += sq(bav.z - cmd[2]);
   S.command_sums[(KS + 4) * N + e] += 1.f;
 
-  // observations -> LDS tile [lane][NO]
-  const int NO = P.num_obs;
-  float* otile = lds;                  // [64][NO]
-  float* ptile = lds + EPB * NO;       // [EPB][18]
+  // observations -> LDS tile [env slot][NO]
   {
-    float* ob = otile + lane * NO;
+    float* ob = otile + es * NO;
     int o = 0;
     if (P.observe_vel) {
       ob[o++] = blv.x * P.obs_scale_lin_vel; ob[o++] = blv.y * P.obs_scale_lin_vel; ob[o++] = blv.z * P.obs_scale_lin_vel;
@@ -976,7 +1045,7 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
       }
     }
     for (int i = 0; i < NO; ++i) ob[i] = fminf(fmaxf(ob[i], -P.clip_obs), P.clip_obs);
-    float* pr = ptile + lane * LRL_NUM_PRIV;
+    float* pr = ptile + es * LRL_NUM_PRIV;
     pr[0] = (S.friction[e] - P.priv_shift[0]) * P.priv_scale[0];
     pr[1] = (S.restitution[e] - P.priv_shift[1]) * P.priv_scale[1];
     pr[2] = (payload - P.priv_shift[2]) * P.priv_scale[2];
@@ -1024,16 +1093,17 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
   S.episode_length[e] = eplen;
   S.reset[e] = (uint8_t)rst;
   S.rew[e] = rew;
+  }  // ql == 0
 
   LRL_PROF(6)  // contact forces + post_physics_step + SoA write-back
   // ---- AoS tiles (obs, priv) and the history shift: coalesced over the wave's contiguous rows ----
   __syncthreads();
-  const size_t row0 = (size_t)blockIdx.x * EPB;
+  const size_t row0 = (size_t)blockIdx.x * ENVS;
   {
     float* og = S.obs + row0 * NO;
-    for (int i = lane; i < EPB * NO; i += EPB) og[i] = otile[i];
+    for (int i = lane; i < ENVS * NO; i += WAVE) og[i] = otile[i];
     float* pgp = S.priv + row0 * LRL_NUM_PRIV;
-    for (int i = lane; i < EPB * LRL_NUM_PRIV; i += EPB) pgp[i] = ptile[i];
+    for (int i = lane; i < ENVS * LRL_NUM_PRIV; i += WAVE) pgp[i] = ptile[i];
   }
   if (flags & LRL_STEP_HISTORY) {
     const int H = K->num_history * NO;
@@ -1043,21 +1113,21 @@ __global__ __launch_bounds__(EPB) void env_step_kernel(const KParams* __restrict
     // Chunks of HU wave-iterations: all HU loads of a chunk are issued before any of its stores (one
     // latency per chunk instead of one per element); a chunk's reads lie above every earlier write.
     constexpr int HU = 16;
-    const int total = EPB * H;
+    const int total = ENVS * H;
     int i0 = 0;
-    for (; i0 + HU * EPB <= total; i0 += HU * EPB) {
+    for (; i0 + HU * WAVE <= total; i0 += HU * WAVE) {
       float v[HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
-        const int i = i0 + u * EPB + lane;
+        const int i = i0 + u * WAVE + lane;
         const int r = i / H, k = i - r * H;
         v[u] = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int u = 0; u < HU; ++u) hg[i0 + u * EPB + lane] = v[u];
+      for (int u = 0; u < HU; ++u) hg[i0 + u * WAVE + lane] = v[u];
     }
-    for (; i0 < total; i0 += EPB) {
+    for (; i0 < total; i0 += WAVE) {
       const int i = i0 + lane;
       const int r = i / H, k = i - r * H;
       const float v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
@@ -1095,8 +1165,8 @@ extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
 
 extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int lds_bytes, const float* actions,
                                           uint32_t flags, int64_t step_counter, hipStream_t stream) {
-  int blocks = S->stride / EPB;
-  hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(EPB), lds_bytes, stream, K, *S, actions, flags,
+  int blocks = S->stride / ENVS;
+  hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
                      step_counter);
   return hipGetLastError();
 }

@@ -28,7 +28,7 @@ for _ in range(K):
     env.step(0.5 * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
 torch.cuda.synchronize()
 assert L.lrl_debug_env_profile(buf, 0) == 8, "library built without LRL_ENV_PROFILE"
-waves = (n + 63) // 64
+waves = (n + 15) // 16  # quad layout: 16 envs per wave
 names = ["kin+dyn+detect", "schur+free acc", "delassus+warm", "PGS", "integrate", "state load", "post-physics",
          "tiles+history"]
 tot = sum(buf)
