@@ -33,7 +33,7 @@
 // every lane holds the full env state); post-physics runs in lane 0 of each env.
 #define QL 4
 #define ENVS (WAVE / QL)
-#define NSF 13  // LDS fields per contact sphere
+#define NSF 67  // LDS fields per contact sphere (map above contact_setup)
 
 namespace lrl {
 
@@ -267,80 +267,87 @@ __device__ __forceinline__ void leg_dirs(const Lds& M, int lsel, int link, V3 x,
   for (int j = 0; j < 3; ++j) c[j] = (j <= link) ? cross(M.a(lsel, j), x - M.o(lsel, j)) : v3(0.f, 0.f, 0.f);
 }
 
-// current joint rates of leg L under lazy propagation
-__device__ __forceinline__ V3 leg_qd(const Lds& M, int L, const float* vb, const float* vb0) {
-  float d[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) d[r] = vb[r] - vb0[r];
+// current joint rates of leg L under lazy propagation: qd_L = q0_L + Y_L - K_L v_b  (q0 = qd0 + K v_b0)
+__device__ __forceinline__ V3 leg_qd(const Lds& M, int L, const float* vb) {
   float q[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     float k = 0.f;
 #pragma unroll
-    for (int r = 0; r < 6; ++r) k += M.Kx(L, j, r) * d[r];
+    for (int r = 0; r < 6; ++r) k += M.Kx(L, j, r) * vb[r];
     q[j] = M.leg(L, 45 + j) + M.leg(L, 48 + j) - k;
   }
   return v3(q[0], q[1], q[2]);
 }
 
-// Apply a world-frame contact impulse dl (t1, t2, n) = (x, y, z) at base-frame point x:
-//   generalized impulse p = J^T (R^T dl);  dv_b = S^-1 (p_b - K_L^T p_L);  Y_L += D_L^-1 p_L
-__device__ __forceinline__ void apply_impulse(const Lds& M, const float* Si, const M3& R, V3 x, int lsel, int link,
-                                              V3 dl, float* vb) {
-  const V3 fb = mulT(R, dl);
-  const V3 tq = cross(x, fb);
-  float r[6] = {tq.x, tq.y, tq.z, fb.x, fb.y, fb.z};
+// Contact-row field map (NSF floats per sphere, LDS [field][env slot]):
+//   0..2 contact point x (base frame)   3 1/W_nn   4 W_t1n   5 W_t2n   6..8 (W_tt)^-1 (11, 12, 22)
+//   9 velocity target   10..12 impulse (n, t1, t2)
+//   13..30 g_d (d = n, t1, t2): base-velocity row of the contact velocity along world direction d,
+//          g_d = [x x n_d, n_d] - K_L^T h_d   (the same row maps an impulse to the base: r = sum_d lambda_d g_d)
+//   31..39 h_d = C_L^T n_d (joint-rate row; C_L = joint directions of the carrying joints)
+//   40..57 z_d = S^-1 g_d (base-velocity change per unit impulse)   58..66 e_d = D_L^-1 h_d (change of Y_L)
+// so one Gauss-Seidel update is u_d = g_d . v_b + h_d . (q0_L + Y_L), the cone projection, and
+// v_b += sum_d dlambda_d z_d,  Y_L += sum_d dlambda_d e_d  — short independent dot products.
+#define SF_G 13
+#define SF_H 31
+#define SF_Z 40
+#define SF_E 58
+
+// apply a world-frame impulse change dl = (n, t1, t2) of sphere s (leg lsel) to v_b and Y_lsel
+__device__ __forceinline__ void apply_impulse(const Lds& M, int s, int lsel, float dn, float dt1, float dt2,
+                                              float* vb) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+    vb[r] += dn * M.sph(s, SF_Z + r) + dt1 * M.sph(s, SF_Z + 6 + r) + dt2 * M.sph(s, SF_Z + 12 + r);
   if (lsel >= 0) {
-    V3 c[3];
-    leg_dirs(M, lsel, link, x, c);
-    const V3 pl = v3(dot(c[0], fb), dot(c[1], fb), dot(c[2], fb));
 #pragma unroll
-    for (int k = 0; k < 6; ++k) r[k] -= M.Kx(lsel, 0, k) * pl.x + M.Kx(lsel, 1, k) * pl.y + M.Kx(lsel, 2, k) * pl.z;
-    const V3 y = di_mul(M, lsel, pl);
-    M.leg(lsel, 48) += y.x;
-    M.leg(lsel, 49) += y.y;
-    M.leg(lsel, 50) += y.z;
+    for (int j = 0; j < 3; ++j)
+      M.leg(lsel, 48 + j) += dn * M.sph(s, SF_E + j) + dt1 * M.sph(s, SF_E + 3 + j) + dt2 * M.sph(s, SF_E + 6 + j);
   }
-  float dv[6];
-  sym6mul(Si, r, dv);
-#pragma unroll
-  for (int k = 0; k < 6; ++k) vb[k] += dv[k];
 }
 
-// One contact sphere's 3x3 Delassus block W = G S^-1 G^T + J_l D^-1 J_l^T (n, t1, t2 rows)
+// One contact sphere's solver rows: g_d, h_d, z_d, e_d and the 3x3 Delassus block W_de = g_d . z_e + h_d . e_e
 __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, const M3& R, int s, int lsel, int link) {
   const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
   V3 c[3] = {v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f)};
   if (lsel >= 0) leg_dirs(M, lsel, link, x, c);
-  float g[3][6];
-  V3 h[3];
+  float g[3][6], z[3][6];
+  V3 h[3], ev[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     const V3 nd = d == 0 ? v3(R.m[6], R.m[7], R.m[8]) : d == 1 ? v3(R.m[0], R.m[1], R.m[2]) : v3(R.m[3], R.m[4], R.m[5]);
     const V3 xn = cross(x, nd);
     g[d][0] = xn.x; g[d][1] = xn.y; g[d][2] = xn.z; g[d][3] = nd.x; g[d][4] = nd.y; g[d][5] = nd.z;
     h[d] = v3(dot(c[0], nd), dot(c[1], nd), dot(c[2], nd));
+    ev[d] = v3(0.f, 0.f, 0.f);
     if (lsel >= 0) {
 #pragma unroll
       for (int r = 0; r < 6; ++r)
         g[d][r] -= M.Kx(lsel, 0, r) * h[d].x + M.Kx(lsel, 1, r) * h[d].y + M.Kx(lsel, 2, r) * h[d].z;
+      ev[d] = di_mul(M, lsel, h[d]);
     }
+    sym6mul(Si, g[d], z[d]);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      M.sph(s, SF_G + 6 * d + r) = g[d][r];
+      M.sph(s, SF_Z + 6 * d + r) = z[d][r];
+    }
+    M.sph(s, SF_H + 3 * d) = h[d].x; M.sph(s, SF_H + 3 * d + 1) = h[d].y; M.sph(s, SF_H + 3 * d + 2) = h[d].z;
+    M.sph(s, SF_E + 3 * d) = ev[d].x; M.sph(s, SF_E + 3 * d + 1) = ev[d].y; M.sph(s, SF_E + 3 * d + 2) = ev[d].z;
   }
   float W[3][3];
 #pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    float z[6];
-    sym6mul(Si, g[e], z);
+  for (int e = 0; e < 3; ++e)
 #pragma unroll
     for (int d = 0; d <= e; ++d) {
       float w = 0.f;
 #pragma unroll
-      for (int r = 0; r < 6; ++r) w += g[d][r] * z[r];
-      if (lsel >= 0) w += dot(h[d], di_mul(M, lsel, h[e]));
+      for (int r = 0; r < 6; ++r) w += g[d][r] * z[e][r];
+      w += dot(h[d], ev[e]);
       W[d][e] = w;
       W[e][d] = w;
     }
-  }
   const float id = 1.f / (W[1][1] * W[2][2] - W[1][2] * W[2][1]);
   M.sph(s, 3) = 1.f / W[0][0];
   M.sph(s, 4) = W[1][0];
@@ -351,23 +358,27 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
 }
 
 // One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone)
-__device__ __forceinline__ void contact_pgs(const Lds& M, const float* Si, const M3& R, int s, int lsel, int link,
-                                            float mu, float* vb, const float* vb0) {
-  const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
-  V3 u = cross(v3(vb[0], vb[1], vb[2]), x) + v3(vb[3], vb[4], vb[5]);
+__device__ __forceinline__ void contact_pgs(const Lds& M, int s, int lsel, float mu, float* vb) {
+  float u[3];
+  float yq[3] = {0.f, 0.f, 0.f};
   if (lsel >= 0) {
-    const V3 qd = leg_qd(M, lsel, vb, vb0);
-    V3 c[3];
-    leg_dirs(M, lsel, link, x, c);
-    u = u + qd.x * c[0] + qd.y * c[1] + qd.z * c[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) yq[j] = M.leg(lsel, 45 + j) + M.leg(lsel, 48 + j);
   }
-  const V3 uw = mul(R, u);  // world: (t1, t2, n) = (x, y, z)
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) a += M.sph(s, SF_G + 6 * d + r) * vb[r];
+    if (lsel >= 0) a += M.sph(s, SF_H + 3 * d) * yq[0] + M.sph(s, SF_H + 3 * d + 1) * yq[1] + M.sph(s, SF_H + 3 * d + 2) * yq[2];
+    u[d] = a;
+  }
   const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
   const float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
   const float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
-  const float ln = fmaxf(ln0 - (uw.z - b) * iWnn, 0.f);
+  const float ln = fmaxf(ln0 - (u[0] - b) * iWnn, 0.f);
   const float dn = ln - ln0;
-  const float ut1 = uw.x + Wt1n * dn, ut2 = uw.y + Wt2n * dn;
+  const float ut1 = u[1] + Wt1n * dn, ut2 = u[2] + Wt2n * dn;
   float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
   const float lim = mu * ln, nt2 = lt1 * lt1 + lt2 * lt2;
   if (nt2 > lim * lim) {
@@ -378,7 +389,7 @@ __device__ __forceinline__ void contact_pgs(const Lds& M, const float* Si, const
   M.sph(s, 10) = ln;
   M.sph(s, 11) = lt1;
   M.sph(s, 12) = lt2;
-  apply_impulse(M, Si, R, x, lsel, link, v3(lt1 - lt10, lt2 - lt20, dn), vb);
+  apply_impulse(M, s, lsel, dn, lt1 - lt10, lt2 - lt20, vb);
 }
 
 struct Body {  // per-lane env state during the step
@@ -600,13 +611,17 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   float vb0[6], vbc[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) vb0[r] = vbc[r] = nu[r];
-#pragma unroll
-  for (int l = 0; l < 4; ++l)
+  {  // owner lane: q0 = qd0 + K v_b0 and Y = 0 of its leg
+    const int l = ql;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      M.leg(l, 45 + j) = nu[6 + 3 * l + j];
+      float k = 0.f;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) k += M.Kx(l, j, r) * vb0[r];
+      M.leg(l, 45 + j) = pick12(nu + 6, 3 * l + j) + k;
       M.leg(l, 48 + j) = 0.f;
     }
+  }
   // Delassus rows of the active spheres, each in the lane that owns the sphere (only spheres active in some
   // env of the wave are visited)
   // (each lane walks its own active spheres: the 4 legs' rows are built at the same time)
@@ -631,8 +646,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (m) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        apply_impulse(M, Sch, R, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), K->sph_leg[s], K->sph_link[s],
-                      v3(M.sph(s, 11), M.sph(s, 12), M.sph(s, 10)), dvb);
+        apply_impulse(M, s, K->sph_leg[s], M.sph(s, 10), M.sph(s, 11), M.sph(s, 12), dvb);
       }
     }
 #pragma unroll
@@ -648,7 +662,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (m) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        contact_pgs(M, Sch, R, s, K->sph_leg[s], K->sph_link[s], mu, vbc, vb0);
+        contact_pgs(M, s, K->sph_leg[s], mu, vbc);
       }
     }
   LRL_PROF(3)  // PGS iterations
@@ -657,7 +671,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   for (int r = 0; r < 6; ++r) nu[r] = vbc[r];
 #pragma unroll
   for (int l = 0; l < 4; ++l) {
-    const V3 q = leg_qd(M, l, vbc, vb0);
+    const V3 q = leg_qd(M, l, vbc);
     nu[6 + 3 * l] = q.x;
     nu[6 + 3 * l + 1] = q.y;
     nu[6 + 3 * l + 2] = q.z;
