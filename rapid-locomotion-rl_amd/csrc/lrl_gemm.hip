@@ -305,8 +305,12 @@ int gemm_pick_splits(int M, int N, int K, int groups) {
   pick_tile(M, N, true, bm, bn);
   const int tiles = groups * ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   int splits = 1;
-  // aim for >= 512 workgroups, keep >= 256 rows per split and <= 128 splits
-  while (tiles * splits < 512 && splits < 128 && (K / (splits * 2)) >= 256) splits *= 2;
+  // aim for >= 1024 workgroups (a split-k workgroup's life is short and latency-bound), keep >= 128 rows
+  // per split and <= 256 splits
+  // per split; the partial slices (written and re-read once) stay under 12M floats
+  const int64_t out = (int64_t)groups * M * N;
+  while (tiles * splits < 1024 && splits < 256 && (K / (splits * 2)) >= 128 && out * splits * 2 <= (12ll << 20))
+    splits *= 2;
   return splits;
 }
 
