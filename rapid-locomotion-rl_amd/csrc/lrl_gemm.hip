@@ -113,6 +113,22 @@ struct Stager {
       reg[u] = v;
     }
   }
+
+  // interior slice of a tile whose rows, columns and k range are all in bounds, float4-aligned operand
+  __device__ __forceinline__ void load_fast(float4 (&reg)[NI], int k0) const {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = threadIdx.x + u * GTHREADS;
+      if (ITEMS % GTHREADS != 0 && i >= ITEMS) continue;
+      if (!RCONTIG) {
+        reg[u] = *reinterpret_cast<const float4*>(rowp[u] + k0);
+      } else {
+        const int r = 4 * (i % (R / 4)), k = k0 + i / (R / 4);
+        const int64_t row = rows ? rows[k] : (int64_t)k;
+        reg[u] = *reinterpret_cast<const float4*>(P + row * ld + r0 + r);
+      }
+    }
+  }
 };
 
 template <int R, int PAD, int NI, bool RCONTIG>
@@ -153,13 +169,19 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   const int64_t* a_rows = T::AMC ? nullptr : p.a_rows;
   const int64_t* b_rows = T::BNC ? p.b_rows : nullptr;
 
-  f32x16 acc[TM][TN];
+  // NACC independent accumulator chains per output tile (k-steps alternate between them) when a wave owns
+  // a single 32x32 tile, so consecutive MFMAs of the wave do not wait on each other's results
+#ifndef LRL_GEMM_SPLITACC
+#define LRL_GEMM_SPLITACC 1
+#endif
+  constexpr int NACC = (LRL_GEMM_SPLITACC && TM * TN == 1) ? 2 : 1;
+  f32x16 acc[TM][TN], acc2[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = acc2[i][j][r] = 0.f;
 
   // bias-gradient partial (weight-gradient products): column sums of A(m, k) over this split's k
   const bool do_bsum = EPI == EPI_PARTIAL && p.bias_part != nullptr && blockIdx.y == 0;
@@ -170,10 +192,17 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   Stager<BN, T::NB, T::BNC> sb;
   sa.init(A, p.lda, a_rows, p.avec, m0, p.M);
   sb.init(B, p.ldb, b_rows, p.bvec, n0, p.N);
+  // uniform fast path: whole tile in bounds, every k slice full, float4 staging on both operands
+  const bool fast = m0 + BM <= p.M && n0 + BN <= p.N && ((kend - kbeg) % GBK) == 0 && p.avec == 4 && p.bvec == 4;
   int k0 = kbeg;
   if (k0 < kend) {
-    sa.load(ra, k0, kend);
-    sb.load(rb, k0, kend);
+    if (fast) {
+      sa.load_fast(ra, k0);
+      sb.load_fast(rb, k0);
+    } else {
+      sa.load(ra, k0, kend);
+      sb.load(rb, k0, kend);
+    }
     stage_store<BM, T::PA, T::NA, T::AMC>(As[0], ra);
     stage_store<BN, T::PB, T::NB, T::BNC>(Bs[0], rb);
   }
@@ -182,8 +211,13 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   for (; k0 < kend; k0 += GBK) {
     const int kn = k0 + GBK;
     if (kn < kend) {
-      sa.load(ra, kn, kend);
-      sb.load(rb, kn, kend);
+      if (fast) {
+        sa.load_fast(ra, kn);
+        sb.load_fast(rb, kn);
+      } else {
+        sa.load(ra, kn, kend);
+        sb.load(rb, kn, kend);
+      }
     }
     if (do_bsum && threadIdx.x < BM) {
 #pragma unroll
@@ -205,8 +239,12 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if (NACC == 2 && (kk & 1))
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], acc2[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+        }
     // keep the scheduler from sinking the LDS reads back next to their MFMAs
     __builtin_amdgcn_sched_barrier(0);
     if (kn < kend) {
@@ -234,7 +272,7 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row < p.M) {
-          float v = acc[i][j][r];
+          float v = NACC == 2 ? acc[i][j][r] + acc2[i][j][r] : acc[i][j][r];
           if (EPI == EPI_BIAS) v += bj;
           if (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
           if (EPI == EPI_DELU) {
@@ -292,9 +330,12 @@ static int vec_width(const float* ptr, int64_t ld, int64_t goff) {
 // Measured on MI355X (scripts/gemm_bench.py): 64x64 tiles (4 workgroups/CU, one 32x32 MFMA tile per
 // wave) beat 128x128 for the batch-major forward / backward-data products; the split-k weight
 // gradients prefer 128x128.
+#ifndef LRL_GEMM_BM128
+#define LRL_GEMM_BM128 0
+#endif
 static void pick_tile(int M, int N, bool wgrad, int& bm, int& bn) {
   const int mx = wgrad ? 128 : 64;
-  bm = M > 64 && mx > 64 ? 128 : (M > 32 ? 64 : 32);
+  bm = M > 64 && (mx > 64 || LRL_GEMM_BM128) ? 128 : (M > 32 ? 64 : 32);
   bn = N > 64 && mx > 64 ? 128 : (N > 32 ? 64 : 32);
   if (bm == 32 && bn < 128) bn = 128;
   if (bn == 32 && bm < 128) bm = 128;
