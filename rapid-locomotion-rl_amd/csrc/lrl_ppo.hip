@@ -31,10 +31,11 @@ extern "C" int lrl_set_error(int code, const char* msg);
 namespace lrl {
 
 constexpr float LOG_SQRT_2PI = 0.91893853320467274178f;  // math.log(math.sqrt(2 * math.pi))
-constexpr int HEAD_ROWS = 64;                             // rows per head workgroup
+constexpr int HEAD_ROWS = 32;                             // rows per head workgroup (LDS ~45 KB: 3 per CU)
 constexpr int HEAD_THREADS = 256;
 constexpr int HEAD_W = 128;                               // actor / critic last hidden width (ac_h2)
 constexpr int MAX_ACT = 16;
+constexpr int HEAD_NA = 12;  // the PPO head kernel is specialised for the quadrupeds' 12 actions
 constexpr int MAX_LAT = 32;
 
 __device__ __forceinline__ float delu(float h) { return h > 0.f ? 1.f : h + 1.f; }  // elu'(y) from h = elu(y)
@@ -77,19 +78,30 @@ __host__ __device__ constexpr int hp_kl(int na) { return na * HEAD_W + na + HEAD
 __host__ __device__ constexpr int hp_len(int na) { return hp_kl(na) + 3; }  // kl, surrogate, value
 
 __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
+  // phases: (0) stage H3 / head weights  (1) mu, v  (2) per (row, action): log-prob and KL terms
+  // (3) per row: ratio, clipped surrogate, clipped value loss, their gradients  (4) per (row, action):
+  // d loss / d mu, d loss / d std  (5) per column: dH3 and the head weight-gradient partials
   constexpr int HP = 2 * HEAD_W + 1;  // odd pitch: row-per-lane reads conflict-free
+  constexpr int NA = HEAD_NA;
   __shared__ float H[HEAD_ROWS][HP];
-  __shared__ float W4[MAX_ACT + 1][HEAD_W];
-  __shared__ float MU[HEAD_ROWS][MAX_ACT + 1];
-  __shared__ float VP[HEAD_ROWS][4];
-  __shared__ float DMU[HEAD_ROWS][MAX_ACT + 1];  // dmu_j, [na] = dv
-  __shared__ float DS[HEAD_ROWS][MAX_ACT];       // per-row d loss / d std_j
-  __shared__ float SC[HEAD_ROWS][3];             // kl, surrogate, value loss per row
-  const int t = threadIdx.x, na = a.na;
+  __shared__ float W4[NA + 1][HEAD_W];
+  __shared__ float MU[HEAD_ROWS][NA + 1];   // mu_j, then d = a_j - mu_j
+  __shared__ float VP[HEAD_ROWS][8];
+  __shared__ float LP[HEAD_ROWS][NA];       // log-prob term, then d loss / d mu
+  __shared__ float KT[HEAD_ROWS][NA];       // KL term, then d loss / d std
+  __shared__ float DR[HEAD_ROWS][2];        // d loss / d logp, d loss / d v
+  __shared__ float SC[HEAD_ROWS][3];        // kl, surrogate, value loss per row
+  __shared__ float SD[3][NA];               // std, log std, 1/std^2
+  const int t = threadIdx.x;
   const int r0 = blockIdx.x * HEAD_ROWS;
   const int nrows = min(HEAD_ROWS, a.B - r0);
+  if (t < NA) {
+    const float sd = a.stdv[t];
+    SD[0][t] = sd;
+    SD[1][t] = logf(sd);
+    SD[2][t] = 1.f / (sd * sd);
+  }
   {
-    // 16 float4 loads in flight per thread, then scattered into the odd-pitch LDS tile
     constexpr int NV = HEAD_ROWS * 2 * HEAD_W / 4 / HEAD_THREADS;
     float4 v[NV];
 #pragma unroll
@@ -104,50 +116,55 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
       H[r][c] = v[u].x; H[r][c + 1] = v[u].y; H[r][c + 2] = v[u].z; H[r][c + 3] = v[u].w;
     }
   }
-  for (int i = t; i < (na + 1) * HEAD_W; i += HEAD_THREADS) {
+  for (int i = t; i < (NA + 1) * HEAD_W; i += HEAD_THREADS) {
     const int j = i / HEAD_W, k = i - j * HEAD_W;
-    W4[j][k] = j < na ? a.w4a[j * HEAD_W + k] : a.w4c[k];
+    W4[j][k] = j < NA ? a.w4a[j * HEAD_W + k] : a.w4c[k];
   }
   __syncthreads();
-  // forward: thread (r, q) computes actions q, q+4, q+8, ... and a quarter of the value dot
+  // (1) thread (r, q): actions q, q+8 and an eighth of the value dot
   {
-    const int r = t & 63, q = t >> 6;
-    for (int j = q; j < na; j += 4) {
+    const int r = t & (HEAD_ROWS - 1), q = t / HEAD_ROWS;
+    for (int j = q; j < NA; j += 8) {
       float s = 0.f;
       for (int k = 0; k < HEAD_W; ++k) s = fmaf(H[r][k], W4[j][k], s);
       MU[r][j] = s + a.b4a[j];
     }
     float s = 0.f;
-    for (int k = q * (HEAD_W / 4); k < (q + 1) * (HEAD_W / 4); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
+    for (int k = q * (HEAD_W / 8); k < (q + 1) * (HEAD_W / 8); ++k) s = fmaf(H[r][HEAD_W + k], W4[NA][k], s);
     VP[r][q] = s;
   }
   __syncthreads();
-  const float invB = 1.f / (float)a.B;
-  if (t < HEAD_ROWS) {
-    // one lane per row; per-action loops are unrolled to MAX_ACT with guards so the arrays stay in VGPRs
-    const int r = t;
-    float kl = 0.f, surr_loss = 0.f, vloss = 0.f, dv = 0.f;
-    float dmu[MAX_ACT], dsig[MAX_ACT];
-#pragma unroll
-    for (int j = 0; j < MAX_ACT; ++j) { dmu[j] = 0.f; dsig[j] = 0.f; }
+  // (2) per (row, action): Normal log-prob term and KL(old || new) term (ppo.py:111-114)
+  for (int i = t; i < HEAD_ROWS * NA; i += HEAD_THREADS) {
+    const int r = i / NA, j = i - r * NA;
+    float lp = 0.f, kt = 0.f, d = 0.f;
     if (r < nrows) {
       const int64_t g = a.rows[r0 + r];
-      const float v = ((VP[r][0] + VP[r][1]) + (VP[r][2] + VP[r][3])) + a.b4c[0];
+      const float s = SD[0][j], mu = MU[r][j];
+      d = a.actions[g * NA + j] - mu;
+      lp = -(d * d) / (2.f * (s * s)) - SD[1][j] - LOG_SQRT_2PI;
+      const float so = a.old_sigma[g * NA + j], dm = a.old_mu[g * NA + j] - mu;
+      kt = logf(s / so + 1.e-5f) + (so * so + dm * dm) / (2.f * (s * s)) - 0.5f;
+    }
+    MU[r][j] = d;
+    LP[r][j] = lp;
+    KT[r][j] = kt;
+  }
+  __syncthreads();
+  const float invB = 1.f / (float)a.B;
+  // (3) per row
+  if (t < HEAD_ROWS) {
+    const int r = t;
+    float kl = 0.f, surr_loss = 0.f, vloss = 0.f, dv = 0.f, dlogp = 0.f;
+    if (r < nrows) {
+      const int64_t g = a.rows[r0 + r];
+      const float v = (((VP[r][0] + VP[r][1]) + (VP[r][2] + VP[r][3])) + ((VP[r][4] + VP[r][5]) + (VP[r][6] + VP[r][7]))) +
+                      a.b4c[0];
       float logp = 0.f;
-      float dj[MAX_ACT];
 #pragma unroll
-      for (int j = 0; j < MAX_ACT; ++j) {
-        dj[j] = 0.f;
-        if (j < na) {
-          const float s = a.stdv[j], mu = MU[r][j];
-          const float var = s * s;
-          const float d = a.actions[g * na + j] - mu;
-          dj[j] = d;
-          logp += -(d * d) / (2.f * var) - logf(s) - LOG_SQRT_2PI;
-          // KL(old || new), ppo.py:111-114 (inference mode)
-          const float so = a.old_sigma[g * na + j], dm = a.old_mu[g * na + j] - mu;
-          kl += logf(s / so + 1.e-5f) + (so * so + dm * dm) / (2.f * (s * s)) - 0.5f;
-        }
+      for (int j = 0; j < NA; ++j) {
+        logp += LP[r][j];
+        kl += KT[r][j];
       }
       const float adv = a.adv[g];
       const float ratio = expf(logp - a.old_logp[g]);
@@ -160,15 +177,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
       const float gb = surr_c > surr ? invB : (surr == surr_c ? 0.5f * invB : 0.f);
       const bool in_rng = ratio >= 1.f - a.clip && ratio <= 1.f + a.clip;
       const float dratio = -adv * ga + (in_rng ? -adv * gb : 0.f);
-      const float dlogp = dratio * ratio;
-#pragma unroll
-      for (int j = 0; j < MAX_ACT; ++j) {
-        if (j < na) {
-          const float s = a.stdv[j], var = s * s, d = dj[j];
-          dmu[j] = dlogp * (d / var);
-          dsig[j] = dlogp * (d * d / (var * s) - 1.f / s) - a.ent_coef * invB / s;
-        }
-      }
+      dlogp = dratio * ratio;
       // value loss (ppo.py:133-143)
       const float tv = a.tv[g], ret = a.ret[g];
       const float gv = a.vcoef * invB;
@@ -186,72 +195,81 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
         dv = gv * 2.f * (v - ret);
       }
     }
-#pragma unroll
-    for (int j = 0; j < MAX_ACT; ++j) {
-      DMU[r][j] = dmu[j];
-      DS[r][j] = dsig[j];
-    }
-    DMU[r][MAX_ACT] = dv;
+    DR[r][0] = dlogp;
+    DR[r][1] = dv;
     SC[r][0] = kl;
     SC[r][1] = surr_loss;
     SC[r][2] = vloss;
   }
   __syncthreads();
-  // backward into H3 and the head weight-gradient partials: thread = column of [actor | critic]
+  // (4) per (row, action): d/d mu = dlogp (a - mu)/var; d/d std = dlogp ((a-mu)^2/var - 1)/std - c_e/(B std)
+  for (int i = t; i < HEAD_ROWS * NA; i += HEAD_THREADS) {
+    const int r = i / NA, j = i - r * NA;
+    float dm = 0.f, ds = 0.f;
+    if (r < nrows) {
+      const float d = MU[r][j], dl = DR[r][0], s = SD[0][j], ivar = SD[2][j];
+      dm = dl * (d * ivar);
+      ds = dl * (d * d * ivar - 1.f) / s - a.ent_coef * invB / s;
+    }
+    LP[r][j] = dm;
+    KT[r][j] = ds;
+  }
+  __syncthreads();
+  // (5) backward into H3 and the head weight-gradient partials: thread = column of [actor | critic]
   float* P = a.part + (int64_t)blockIdx.x * a.part_len;
   {
     const int k = t;  // 0..255
     if (k < HEAD_W) {
-      float wk[MAX_ACT], accw[MAX_ACT];
+      float wk[NA], accw[NA];
 #pragma unroll
-      for (int j = 0; j < MAX_ACT; ++j) {
-        wk[j] = j < na ? W4[j][k] : 0.f;
+      for (int j = 0; j < NA; ++j) {
+        wk[j] = W4[j][k];
         accw[j] = 0.f;
       }
+#pragma unroll 2
       for (int r = 0; r < nrows; ++r) {
         const float h = H[r][k];
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < MAX_ACT; ++j) {
-          const float dm = DMU[r][j];  // zero for j >= na
+        for (int j = 0; j < NA; ++j) {
+          const float dm = LP[r][j];
           s = fmaf(dm, wk[j], s);
           accw[j] = fmaf(dm, h, accw[j]);
         }
         a.dh3[(int64_t)(r0 + r) * (2 * HEAD_W) + k] = s * delu(h);
       }
 #pragma unroll
-      for (int j = 0; j < MAX_ACT; ++j)
-        if (j < na) P[hp_w4a(na) + j * HEAD_W + k] = accw[j];
+      for (int j = 0; j < NA; ++j) P[hp_w4a(NA) + j * HEAD_W + k] = accw[j];
     } else {
       const int kk = k - HEAD_W;
-      const float wk = W4[na][kk];
+      const float wk = W4[NA][kk];
       float accc = 0.f;
       for (int r = 0; r < nrows; ++r) {
         const float h = H[r][k];
-        const float d = DMU[r][MAX_ACT];
+        const float d = DR[r][1];
         accc = fmaf(d, h, accc);
         a.dh3[(int64_t)(r0 + r) * (2 * HEAD_W) + k] = (d * wk) * delu(h);
       }
-      P[hp_w4c(na) + kk] = accc;
+      P[hp_w4c(NA) + kk] = accc;
     }
   }
-  if (t < na) {
+  if (t < NA) {
     float sb = 0.f, ss = 0.f;
     for (int r = 0; r < nrows; ++r) {
-      sb += DMU[r][t];
-      ss += DS[r][t];
+      sb += LP[r][t];
+      ss += KT[r][t];
     }
-    P[hp_b4a(na) + t] = sb;
-    P[hp_std(na) + t] = ss;
+    P[hp_b4a(NA) + t] = sb;
+    P[hp_std(NA) + t] = ss;
   } else if (t == 16) {
     float sb = 0.f;
-    for (int r = 0; r < nrows; ++r) sb += DMU[r][MAX_ACT];
-    P[hp_b4c(na)] = sb;
+    for (int r = 0; r < nrows; ++r) sb += DR[r][1];
+    P[hp_b4c(NA)] = sb;
   } else if (t >= 32 && t < 35) {
     const int c = t - 32;
     float s = 0.f;
     for (int r = 0; r < nrows; ++r) s += SC[r][c];
-    P[hp_kl(na) + c] = s;
+    P[hp_kl(NA) + c] = s;
   }
 }
 
@@ -275,7 +293,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
   __shared__ float H[HEAD_ROWS][HP];
   __shared__ float W4[MAX_ACT + 1][HEAD_W];
   __shared__ float MU[HEAD_ROWS][MAX_ACT + 1];
-  __shared__ float VP[HEAD_ROWS][4];
+  __shared__ float VP[HEAD_ROWS][8];
   const int t = threadIdx.x, na = a.na;
   const int r0 = blockIdx.x * HEAD_ROWS;
   const int nrows = min(HEAD_ROWS, a.n - r0);
@@ -300,14 +318,14 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
   }
   __syncthreads();
   {
-    const int r = t & 63, q = t >> 6;
-    for (int j = q; j < na; j += 4) {
+    const int r = t & (HEAD_ROWS - 1), q = t / HEAD_ROWS;
+    for (int j = q; j < na; j += 8) {
       float s = 0.f;
       for (int k = 0; k < HEAD_W; ++k) s = fmaf(H[r][k], W4[j][k], s);
       MU[r][j] = s + a.b4a[j];
     }
     float s = 0.f;
-    for (int k = q * (HEAD_W / 4); k < (q + 1) * (HEAD_W / 4); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
+    for (int k = q * (HEAD_W / 8); k < (q + 1) * (HEAD_W / 8); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
     VP[r][q] = s;
   }
   __syncthreads();
@@ -343,7 +361,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
     const int g = r0 + t;
     float lp = 0.f;
     for (int j = 0; j < na; ++j) lp += MU[t][j];
-    const float v = ((VP[t][0] + VP[t][1]) + (VP[t][2] + VP[t][3])) + a.b4c[0];
+    const float v = (((VP[t][0] + VP[t][1]) + (VP[t][2] + VP[t][3])) + ((VP[t][4] + VP[t][5]) + (VP[t][6] + VP[t][7]))) +
+                    a.b4c[0];
     if (a.values) a.values[g] = v;
     if (a.logp) a.logp[g] = lp;
     if (a.do_store) {
@@ -465,6 +484,18 @@ struct SegList {
 
 __global__ void seg_reduce_kernel(SegList L) {
   const Seg& sg = L.s[blockIdx.y];
+  if (sg.parts >= 64 && sg.len <= 8192) {
+    // many parts, few elements (per-workgroup head partials): one wave per element, lanes stride over
+    // the parts, fixed shuffle tree (deterministic)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int64_t i = (int64_t)blockIdx.x * nw + w; i < sg.len; i += (int64_t)gridDim.x * nw) {
+      float acc = 0.f;
+      for (int q = lane; q < sg.parts; q += 64) acc += sg.src[(int64_t)q * sg.stride + i];
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+      if (lane == 0) sg.dst[i] = acc * sg.scale;
+    }
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.len; i += (int64_t)gridDim.x * blockDim.x) {
     // 8 independent loads in flight per step, summed in part order (deterministic)
     float acc = 0.f;
@@ -615,7 +646,7 @@ static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
 static int check_net(const lrl_ppo_net* n) {
   if (!n) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: null net");
   if (n->ac_h2 != HEAD_W) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: last actor/critic hidden width must be 128");
-  if (n->num_actions > MAX_ACT || n->num_actions < 1) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: num_actions > 16");
+  if (n->num_actions != HEAD_NA) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: num_actions must be 12");
   if (n->latent > MAX_LAT || n->ad_h1 > MAX_LAT) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: latent/adaptation widths > 32");
   if (n->num_obs + n->latent > XS) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: obs + latent > 64");
   return 0;
