@@ -80,11 +80,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl"); LRL_DIST_BACKEND=gloo and more ranks than GPUs are for rehearsing
+    # the multi-rank path on a single-GPU box (ranks then share devices round-robin)
+    ndev = max(1, torch.cuda.device_count())
+    local_dev = local % ndev
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    torch.cuda.set_device(local)
-    dev = f"cuda:{local}"
+        backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_dev}"))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(local_dev)
+    dev = f"cuda:{local_dev}"
 
     from lrl import config as lcfg
     from lrl.env import LeggedRobotEnv
