@@ -31,9 +31,9 @@ res = {"units": "bytes per launch (FETCH_SIZE KiB x 1024 x 2 + WRITE_SIZE KiB x 
                        "write_bytes": cal_w[0][1] * 1024 if cal_w else None},
        "kernels": {}}
 for k in fetch:
-    if not k.startswith("lrl::"):
+    if "lrl::" not in k:
         continue
-    short = k.split("(")[0]
+    short = k.split("(")[0].replace("void ", "")
     fb = fetch[k][1] * 1024 * 2
     wb = write.get(k, (0, 0.0))[1] * 1024
     res["kernels"][short] = {"dispatches": fetch[k][0], "fetch_bytes": fb, "write_bytes": wb,
