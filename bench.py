@@ -24,18 +24,22 @@ import torch.distributed as dist  # noqa: E402
 ENVS_PER_GPU = 4096
 B_ENV = 1325            # algorithmic HBM bytes per env-step; history shift adds 4872
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TF = 157.3  # dense fp32 MFMA peak (v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary (profiles/r*_pmc.json,
-    written by scripts/gpu_profile.sh + scripts/pmc_summary.py from separate rocprofv3 --pmc passes)."""
+def pmc_traffic(*kernels):
+    """HBM bytes per launch of the first of ``kernels`` (symbol, or symbol@grid) found in the newest committed
+    PMC summary (profiles/r*_pmc.json, written by scripts/gpu_profile.sh + scripts/pmc_summary.py from
+    separate rocprofv3 --pmc passes)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
     for path in reversed(files):
         with open(path) as f:
-            k = json.load(f)["kernels"].get(kernel)
-        if k:
-            return k["traffic_bytes"], os.path.relpath(path, ROOT)
+            table = json.load(f)["kernels"]
+        for kernel in kernels:
+            k = table.get(kernel)
+            if k:
+                return k["traffic_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -117,10 +121,15 @@ def main():
     if world > 1:
         dist.barrier()
     env.env.kernel_timer = timer
+    import ctypes as C
+    from lrl import _abi
+    _abi.check(_abi.lib().lrl_ppo_timing(1, None, None))  # events around the update's largest GEMM
     t0 = time.perf_counter()
     runner.learn(args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    g_ms, g_n = C.c_double(0.0), C.c_int64(0)
+    _abi.check(_abi.lib().lrl_ppo_timing(0, C.byref(g_ms), C.byref(g_n)))
     if world > 1:
         dist.barrier()
     env.env.kernel_timer = None
@@ -146,6 +155,13 @@ def main():
     if rank == 0:
         achieved = B_ENV * ENVS_PER_GPU / (k_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic("lrl::env_step_kernel")
+        # update's largest product: actor/critic layer-2 weight gradient, 2 x (256 x 512) over the minibatch rows
+        mb_rows = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env // 4
+        gemm_flop = 2.0 * 2 * 256 * 512 * mb_rows
+        gemm_ms = g_ms.value / max(1, g_n.value)
+        gemm_tf = gemm_flop / (gemm_ms * 1e-3) / 1e12 if g_n.value else None
+        # (the PMC summary keys dispatches by total grid size, which dW2 shares with dW3: no per-launch traffic)
+        gemm_traffic = None
         out = {
             "metric": "env-steps/sec, 4096 Mini Cheetah envs, 1/2/4/8 MI355X; PPO iters/sec",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -163,6 +179,13 @@ def main():
                          "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (the fused history "
                                  f"shift adds 4872 B/env-step = {4872 * ENVS_PER_GPU} B per launch); the kernel is "
                                  "latency/VALU-bound (one env per lane), see DESIGN.md"},
+            "roofline_update_gemm": {
+                "bound": "mfma", "kernel": "lrl::gemm_kernel<128,128,TN,partial> (dW2: 2 x 256x512, "
+                f"{mb_rows} rows)", "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": MFMA_F32_PEAK_TF,
+                "unit": "TFLOP/s", "frac": round(gemm_tf / MFMA_F32_PEAK_TF, 4) if gemm_tf else None,
+                "traffic": round(gemm_traffic) if gemm_traffic else None, "launch_ms": round(gemm_ms, 4),
+                "launches": g_n.value,
+                "note": "the GEMM family is ~70% of the iteration's GPU time; this is its largest launch"},
             "reference_context": {"upstream_example_run_env_steps_per_s": 41176, "upstream_ppo_iters_per_s": 0.429,
                                   "hardware": "unspecified NVIDIA GPU, 4000 envs (BASELINE.md §1)"},
         }

@@ -342,6 +342,12 @@ int32_t lrl_ppo_adaptation_step(const lrl_ppo_net* net, float* params, const flo
                                 float* exp_avg_sq, int64_t step, double lr, float grad_scale,
                                 const lrl_ppo_hparams* hp, lrl_ppo_ctrl* ctrl, void* stream);
 
+/* Timing hook for bench.py's roofline: while enabled, HIP events bracket every launch of the update's
+ * largest product (actor/critic layer-2 weight gradient, 2 x 256 x 512 over the minibatch rows) on its
+ * stream.  Each call returns the summed event time and launch count recorded since the previous call
+ * (either pointer may be NULL), clears them, and sets the enable flag for what follows. */
+int32_t lrl_ppo_timing(int32_t enable, double* total_ms, int64_t* launches);
+
 /* Test entry point of the GEMM the update is built from: C = op(A) op(B) with
  * layout 0 (NT: C[m][n] = sum_k A[m][k] B[n][k]), 2 (NN: sum_k A[m][k] B[k][n]),
  * 3 (TN: sum_k A[k][m] B[k][n], split over k, partials reduced in place);

@@ -654,6 +654,31 @@ static int check_net(const lrl_ppo_net* n) {
 
 static void launch_seg(const SegList& L, hipStream_t st);
 
+// Optional timing of the update's largest product (the actor/critic layer-2 weight gradient, 2 x 256x512
+// over the minibatch rows): HIP events around that launch on its stream, read back by lrl_ppo_timing_read.
+struct GemmTimer {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+};
+static GemmTimer g_timer;
+static hipEvent_t timer_event() {
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+static void timer_begin(hipStream_t st) {
+  if (!g_timer.on) return;
+  if (g_timer.used == g_timer.ev.size()) g_timer.ev.emplace_back(timer_event(), timer_event());
+  auto& pr = g_timer.ev[g_timer.used];
+  if (pr.first) (void)hipEventRecord(pr.first, st);
+}
+static void timer_end(hipStream_t st) {
+  if (!g_timer.on) return;
+  auto& pr = g_timer.ev[g_timer.used++];
+  if (pr.second) (void)hipEventRecord(pr.second, st);
+}
+
 // one GEMM helper per layout
 struct G {
   hipStream_t st;
@@ -859,7 +884,9 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   const int h0 = n.ac_h0, h1 = n.ac_h1, h2 = n.ac_h2;
   g.tn(P.dh3, 2 * h2, P.h2, 2 * h1, nullptr, h2, h1, B, 2, h2, h1, part, grads + n.w3, grads + n.b3, L);
   g.nn(P.dh3, 2 * h2, w + n.w3, h1, P.dh2, 2 * h1, P.h2, 2 * h1, B, h1, h2, 2, h2, (int64_t)h2 * h1, h1, h1);
+  timer_begin(st);
   g.tn(P.dh2, 2 * h1, P.h1, 2 * h0, nullptr, h1, h0, B, 2, h1, h0, part, grads + n.w2, grads + n.b2, L);
+  timer_end(st);
   g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
   g.tn(P.dh1, 2 * h0, P.xa, XS, nullptr, 2 * h0, nx, B, 1, 0, 0, part, grads + n.w1, grads + n.b1, L);
   // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
@@ -993,4 +1020,23 @@ extern "C" int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t 
   p.a_rows = rows;
   int rc = gemm_launch(p, layout, epi, 1, st);
   return rc ? lrl_set_error(rc, "lrl_gemm_f32: bad layout/epilogue or launch failure") : 0;
+}
+
+// ---- timing hook of the dominant update product (bench.py roofline) ----
+extern "C" int32_t lrl_ppo_timing(int32_t enable, double* total_ms, int64_t* launches) {
+  if (total_ms) {
+    double t = 0.0;
+    for (size_t i = 0; i < g_timer.used; ++i) {
+      float ms = 0.f;
+      if (hipEventSynchronize(g_timer.ev[i].second) != hipSuccess ||
+          hipEventElapsedTime(&ms, g_timer.ev[i].first, g_timer.ev[i].second) != hipSuccess)
+        return lrl_set_error(LRL_E_HIP, "lrl_ppo_timing: event query failed");
+      t += ms;
+    }
+    *total_ms = t;
+  }
+  if (launches) *launches = (int64_t)g_timer.used;
+  g_timer.used = 0;
+  g_timer.on = enable != 0;
+  return 0;
 }

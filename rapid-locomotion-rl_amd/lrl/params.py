@@ -133,6 +133,8 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         raise ValueError("height measurements (rough terrain) are not implemented yet")
     if cfg.control.control_type != "P":
         raise ValueError("only control_type 'P' is implemented")
+    if cfg.domain_rand.push_robots:  # off in config_mini_cheetah / config_go1 (mini_cheetah_config.py:90)
+        raise ValueError("domain_rand.push_robots is not implemented by the fused kernel")
     nrm = cfg.normalization
     priv = [get_scale_shift(nrm.friction_range), get_scale_shift(nrm.restitution_range),
             get_scale_shift(nrm.added_mass_range), get_scale_shift(nrm.com_displacement_range),
