@@ -37,8 +37,9 @@ struct GemmP {
   int M, N, K;
   int splits, kps;        // k range of split s: [s*kps, min(K, (s+1)*kps))
   int avec, bvec;         // staging access width (4/2/1 floats), set by gemm_launch from the alignment
+  int groups;             // set by gemm_launch
   int64_t lda, ldb, ldc, ld_aux;
-  int64_t ga, gb, gc, gbias, gaux;  // per-group element offsets (blockIdx.z = group * splits + split)
+  int64_t ga, gb, gc, gbias, gaux;  // per-group element offsets
   int64_t part_stride;              // EPI_PARTIAL: elements between split slices of C ([split][group][M][N])
 };
 

@@ -156,10 +156,21 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   using T = GemmTile<BM, BN, LAYOUT>;
   __shared__ __attribute__((aligned(16))) float As[2][GBK][BM + T::PA];
   __shared__ __attribute__((aligned(16))) float Bs[2][GBK][BN + T::PB];
-  const int g = blockIdx.z / p.splits, s = blockIdx.z - g * p.splits;
+  // XCD-aware tile order: the hardware deals workgroup ids round-robin over the 8 XCDs, so id i is
+  // renumbered to L with consecutive L on the same XCD; L runs n-tile fastest, then m-tile, then
+  // (group, split): the workgroups sharing an A row-panel (or a split's rows) share one XCD's L2.
+  const int mt = (p.M + BM - 1) / BM, nt = (p.N + BN - 1) / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, zz = L / (nt * mt);
+  const int groups = p.groups;
+  const int g = zz / p.splits, s = zz - g * p.splits;
   const float* __restrict__ A = p.A + g * p.ga;
   const float* __restrict__ B = p.B + g * p.gb;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
   const int kbeg = s * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -184,7 +195,7 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = acc2[i][j][r] = 0.f;
 
   // bias-gradient partial (weight-gradient products): column sums of A(m, k) over this split's k
-  const bool do_bsum = EPI == EPI_PARTIAL && p.bias_part != nullptr && blockIdx.y == 0;
+  const bool do_bsum = EPI == EPI_PARTIAL && p.bias_part != nullptr && tn_ == 0;
   float bsum = 0.f;
 
   float4 ra[T::NA], rb[T::NB];
@@ -194,6 +205,23 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   sb.init(B, p.ldb, b_rows, p.bvec, n0, p.N);
   // uniform fast path: whole tile in bounds, every k slice full, float4 staging on both operands
   const bool fast = m0 + BM <= p.M && n0 + BN <= p.N && ((kend - kbeg) % GBK) == 0 && p.avec == 4 && p.bvec == 4;
+  // backward-data epilogue operand (the layer input, for elu'): fetched up front so its latency hides
+  // under the main loop instead of trailing it
+  float xaux[EPI == EPI_DELU ? TM : 1][EPI == EPI_DELU ? TN : 1][16];
+  if constexpr (EPI == EPI_DELU) {
+    const float* __restrict__ ax = p.aux + g * p.gaux;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = min(n0 + wn + 32 * j + li, p.N - 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h, p.M - 1);
+          xaux[i][j][r] = ax[(int64_t)row * p.ld_aux + col];
+        }
+    }
+  }
   int k0 = kbeg;
   if (k0 < kend) {
     if (fast) {
@@ -263,7 +291,6 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   float* __restrict__ C = p.C + g * p.gc;
   if (EPI == EPI_PARTIAL) C += (int64_t)s * p.part_stride;
   const float* __restrict__ bias = p.bias ? p.bias + g * p.gbias : nullptr;
-  const float* __restrict__ aux = p.aux ? p.aux + g * p.gaux : nullptr;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn + 32 * j + li;
@@ -279,8 +306,8 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
           float v = NACC == 2 ? acc[i][j][r] + acc2[i][j][r] : acc[i][j][r];
           if (EPI == EPI_BIAS) v += bj;
           if (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
-          if (EPI == EPI_DELU) {
-            const float x = aux[(int64_t)row * p.ld_aux + col];
+          if constexpr (EPI == EPI_DELU) {
+            const float x = xaux[i][j][r];
             v = x > 0.f ? v : v * (x + 1.f);
           }
           C[(int64_t)row * p.ldc + col] = v;
@@ -290,7 +317,7 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   }
   // bias partial layout [split][group][M] (contiguous per split, like the C partials)
   if (do_bsum && threadIdx.x < BM && m0 + (int)threadIdx.x < p.M)
-    p.bias_part[((int64_t)s * (gridDim.z / p.splits) + g) * p.M + m0 + threadIdx.x] = bsum;
+    p.bias_part[((int64_t)s * groups + g) * p.M + m0 + threadIdx.x] = bsum;
 }
 
 template <int BM, int BN>
@@ -369,7 +396,8 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   p.bvec = vec_width(p.B, p.ldb, p.gb);
   int bm, bn;
   pick_tile(p.M, p.N, layout == GEMM_TN, bm, bn);
-  dim3 grid((p.M + bm - 1) / bm, (p.N + bn - 1) / bn, groups * p.splits);
+  p.groups = groups;
+  dim3 grid(((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * groups * p.splits);
   hipStream_t st = static_cast<hipStream_t>(stream);
   int rc = LRL_E_INVALID;
   if (bm == 128 && bn == 128) rc = launch_bm<128, 128>(p, layout, epi, grid, st);
