@@ -806,7 +806,7 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
   g.nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1, nt.enc_h0, true);
   g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, false);
-  g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, nx, true);
+  g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, XS, true);  // see phase 1
   g.nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true, 2,
        nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);
   g.nt(P.h2, 2 * nt.ac_h1, nullptr, w + nt.w3, nt.ac_h1, P.h3, 2 * nt.ac_h2, w + nt.b3, n, nt.ac_h2, nt.ac_h1, true, 2,
@@ -847,7 +847,10 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
   g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
   g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.xa + n.num_obs, XS, w + n.e3b, B, n.latent, n.enc_h1, false);
-  g.nt(P.xa, XS, nullptr, w + n.w1, nx, P.h1, 2 * n.ac_h0, w + n.b1, B, 2 * n.ac_h0, nx, true);
+  // k runs over all XS = 64 columns of X: columns nx..63 are zero, so the extra products (with the next
+  // row's first weights, or the first biases after the last row — finite values) add exactly 0, and the
+  // product takes the unguarded float4 path
+  g.nt(P.xa, XS, nullptr, w + n.w1, nx, P.h1, 2 * n.ac_h0, w + n.b1, B, 2 * n.ac_h0, XS, true);
   g.nt(P.h1, 2 * n.ac_h0, nullptr, w + n.w2, n.ac_h0, P.h2, 2 * n.ac_h1, w + n.b2, B, n.ac_h1, n.ac_h0, true, 2,
        n.ac_h0, (int64_t)n.ac_h1 * n.ac_h0, n.ac_h1, n.ac_h1);
   g.nt(P.h2, 2 * n.ac_h1, nullptr, w + n.w3, n.ac_h1, P.h3, 2 * n.ac_h2, w + n.b3, B, n.ac_h2, n.ac_h1, true, 2,
