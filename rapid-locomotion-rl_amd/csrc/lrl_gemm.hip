@@ -320,6 +320,140 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
     p.bias_part[((int64_t)s * groups + g) * p.M + m0 + threadIdx.x] = bsum;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// LDS-DMA variant for the interior batch-major products (forward NT, backward-data NN) with float4-aligned
+// operands: 64x64 tile, 4 waves each owning a 32x32 MFMA tile, BK = 16, a 3-deep ring of LDS stages
+// filled by global_load_lds_dwordx4 (no staging registers, no ds_write pass), counted vmcnt waits and a
+// raw s_barrier so the loads of slice k+2 stay in flight while slice k is consumed.
+//   k-contiguous operands (A; B of NT) land as [row][16 k] images, 16-B chunk c of row r stored in slot
+//   c ^ ((r >> 2) & 3) (the swizzle is applied to the SOURCE address, the DMA destination stays lane-linear),
+//   and each lane reads its row's 8 k-values (k = 8h .. 8h+7) with two conflict-free ds_read_b128;
+//   the n-contiguous B of NN lands as [16 k][64 n] and is read with ds_read_b32 (consecutive n per lane).
+// MFMA k-step t of lane half h uses k = 8h + t for both operands, so the sum runs over every k once.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int LAYOUT, int EPI>
+__global__ __launch_bounds__(GTHREADS) void gemm_glds_kernel(GemmP p) {
+  constexpr int BM = 64, BN = 64, BKD = 16, NST = 3, IMG = 1024;
+  constexpr bool BNC = (LAYOUT & 2) != 0;
+  static_assert((LAYOUT & 1) == 0, "A must be k-contiguous");
+  __shared__ __attribute__((aligned(16))) float S[NST * 2 * IMG];  // [stage][A | B][image], one LDS object
+  const int mt = p.M / BM, nt = p.N / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, g = L / (nt * mt);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ B = p.B + g * p.gb;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int K = p.K;
+
+  // this lane's DMA sources: A rows 16w + lane/4 (chunk pre-swizzled); B likewise (NT) or k-row 4w + lane/16 (NN)
+  const int ar = 16 * w + (lane >> 2);
+  const int achunk = (lane & 3) ^ ((ar >> 2) & 3);
+  const float* asrc = A + (p.a_rows ? p.a_rows[m0 + ar] : (int64_t)(m0 + ar)) * p.lda + 4 * achunk;
+  const float* bsrc;
+  if constexpr (!BNC) {
+    bsrc = B + (int64_t)(n0 + ar) * p.ldb + 4 * achunk;
+  } else {
+    bsrc = B + (int64_t)(4 * w + (lane >> 4)) * p.ldb + n0 + 4 * (lane & 15);
+  }
+  // the DMA is issued from inline asm so the compiler does not track it (it would otherwise drain it with
+  // vmcnt(0) before every ds_read); completion is ordered by the counted waits below
+  const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
+  auto dma = [&](const float* src, uint32_t lds_off) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_off)
+                 : "memory");
+  };
+  auto issue = [&](int st, int k0) {
+    const uint32_t base = __builtin_amdgcn_readfirstlane(s_lds + (uint32_t)((st * 2 * IMG + w * 256) * 4));
+    dma(asrc + k0, base);
+    dma(BNC ? bsrc + (int64_t)k0 * p.ldb : bsrc + k0, base + IMG * 4);
+  };
+
+  // backward-data epilogue operand (elu' of the layer input), fetched before the DMA ring starts
+  float xaux[16];
+  if constexpr (EPI == EPI_DELU) {
+    const float* __restrict__ ax = p.aux + g * p.gaux;
+    const int col = n0 + wn + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      xaux[r] = ax[(int64_t)row * p.ld_aux + col];
+    }
+  }
+
+  f32x16 acc, acc2;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+
+  const int ns = K / BKD;
+  issue(0, 0);
+  if (ns > 1) issue(1, BKD);
+  const int ai = wm + li, aswz = (ai >> 2) & 3;
+  const int bi = wn + li, bswz = (bi >> 2) & 3;
+  for (int s = 0; s < ns; ++s) {
+    // this wave's DMA of slice s has landed (slice s+1's two loads may stay in flight) ...
+    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ... and every wave's, and every wave is done reading the stage slice s+2 will overwrite
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < ns) issue((s + 2) % NST, (s + 2) * BKD);
+    const float* As = S + (s % NST) * 2 * IMG;
+    const float* Bs = As + IMG;
+    float a[8], b[8];
+    {
+      const float4 a0 = *reinterpret_cast<const float4*>(As + ai * 16 + 4 * ((2 * h) ^ aswz));
+      const float4 a1 = *reinterpret_cast<const float4*>(As + ai * 16 + 4 * ((2 * h + 1) ^ aswz));
+      a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+    }
+    if constexpr (!BNC) {
+      const float4 b0 = *reinterpret_cast<const float4*>(Bs + bi * 16 + 4 * ((2 * h) ^ bswz));
+      const float4 b1 = *reinterpret_cast<const float4*>(Bs + bi * 16 + 4 * ((2 * h + 1) ^ bswz));
+      b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) b[t] = Bs[(8 * h + t) * BN + bi];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t & 1) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[t], acc2, 0, 0, 0);
+      else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[t], acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  float* __restrict__ C = p.C + g * p.gc;
+  const int col = n0 + wn + li;
+  float bj = 0.f;
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = p.bias[g * p.gbias + col];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+    float v = acc[r] + acc2[r];
+    if constexpr (EPI == EPI_BIAS) v += bj;
+    if constexpr (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+    if constexpr (EPI == EPI_DELU) {
+      const float x = xaux[r];
+      v = x > 0.f ? v : v * (x + 1.f);
+    }
+    C[(int64_t)row * p.ldc + col] = v;
+  }
+}
+
 template <int BM, int BN>
 static int launch_bm(const GemmP& p, int layout, int epi, dim3 grid, hipStream_t st) {
 #define LRL_GEMM_LAUNCH(L, E) hipLaunchKernelGGL((gemm_kernel<BM, BN, L, E>), grid, dim3(GTHREADS), 0, st, p)
@@ -399,6 +533,22 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   p.groups = groups;
   dim3 grid(((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * groups * p.splits);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  // LDS-DMA path: batch-major product, every tile interior, float4-aligned operands, single split
+  if (layout != GEMM_TN && p.splits == 1 && p.M % 64 == 0 && p.N % 64 == 0 && p.K % 16 == 0 && p.K >= 32 &&
+      p.avec == 4 && p.bvec == 4 && epi != EPI_PARTIAL && (layout == GEMM_NT || layout == GEMM_NN)) {
+    dim3 g1((p.M / 64) * (p.N / 64) * groups);
+#define LRL_GLDS(L, E) hipLaunchKernelGGL((gemm_glds_kernel<L, E>), g1, dim3(GTHREADS), 0, st, p)
+    if (layout == GEMM_NT) {
+      if (epi == EPI_STORE) LRL_GLDS(GEMM_NT, EPI_STORE);
+      else if (epi == EPI_BIAS) LRL_GLDS(GEMM_NT, EPI_BIAS);
+      else LRL_GLDS(GEMM_NT, EPI_BIAS_ELU);
+    } else {
+      if (epi == EPI_STORE) LRL_GLDS(GEMM_NN, EPI_STORE);
+      else LRL_GLDS(GEMM_NN, EPI_DELU);
+    }
+#undef LRL_GLDS
+    return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  }
   int rc = LRL_E_INVALID;
   if (bm == 128 && bn == 128) rc = launch_bm<128, 128>(p, layout, epi, grid, st);
   else if (bm == 128 && bn == 64) rc = launch_bm<128, 64>(p, layout, epi, grid, st);
