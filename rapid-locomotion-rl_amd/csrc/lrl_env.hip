@@ -357,20 +357,21 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
   M.sph(s, 8) = W[1][1] * id;
 }
 
-// One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone)
+// One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone).
+// Branch-free over the sphere kind: a base sphere (lsel < 0) has h_d = e_d = 0 in its rows, so it reads and
+// writes leg 0's accumulators with exact-zero contributions, and the envs of a wave never split paths.
 __device__ __forceinline__ void contact_pgs(const Lds& M, int s, int lsel, float mu, float* vb) {
+  const int L = lsel < 0 ? 0 : lsel;
   float u[3];
-  float yq[3] = {0.f, 0.f, 0.f};
-  if (lsel >= 0) {
+  float yq[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) yq[j] = M.leg(lsel, 45 + j) + M.leg(lsel, 48 + j);
-  }
+  for (int j = 0; j < 3; ++j) yq[j] = M.leg(L, 45 + j) + M.leg(L, 48 + j);
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 6; ++r) a += M.sph(s, SF_G + 6 * d + r) * vb[r];
-    if (lsel >= 0) a += M.sph(s, SF_H + 3 * d) * yq[0] + M.sph(s, SF_H + 3 * d + 1) * yq[1] + M.sph(s, SF_H + 3 * d + 2) * yq[2];
+    a += M.sph(s, SF_H + 3 * d) * yq[0] + M.sph(s, SF_H + 3 * d + 1) * yq[1] + M.sph(s, SF_H + 3 * d + 2) * yq[2];
     u[d] = a;
   }
   const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
@@ -381,15 +382,19 @@ __device__ __forceinline__ void contact_pgs(const Lds& M, int s, int lsel, float
   const float ut1 = u[1] + Wt1n * dn, ut2 = u[2] + Wt2n * dn;
   float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
   const float lim = mu * ln, nt2 = lt1 * lt1 + lt2 * lt2;
-  if (nt2 > lim * lim) {
-    const float sc = nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f;
-    lt1 *= sc;
-    lt2 *= sc;
-  }
+  const float sc = nt2 > lim * lim ? (nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f) : 1.f;
+  lt1 *= sc;
+  lt2 *= sc;
   M.sph(s, 10) = ln;
   M.sph(s, 11) = lt1;
   M.sph(s, 12) = lt2;
-  apply_impulse(M, s, lsel, dn, lt1 - lt10, lt2 - lt20, vb);
+  const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+    vb[r] += dn * M.sph(s, SF_Z + r) + dt1 * M.sph(s, SF_Z + 6 + r) + dt2 * M.sph(s, SF_Z + 12 + r);
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    M.leg(L, 48 + j) += dn * M.sph(s, SF_E + j) + dt1 * M.sph(s, SF_E + 3 + j) + dt2 * M.sph(s, SF_E + 6 + j);
 }
 
 struct Body {  // per-lane env state during the step
@@ -420,12 +425,33 @@ __device__ __forceinline__ int sph_owner(const KParams* __restrict__ K, int s) {
   const int l = K->sph_leg[s];
   return l >= 0 ? l : (s & 3);
 }
+// leg of sphere s from the (wave-uniform) leg sphere ranges: a few compares against scalar registers instead
+// of a per-lane global load of K->sph_leg[s] on the solver's dependency chain
+struct SphLegs {
+  int b[4], e[4];
+};
+__device__ __forceinline__ SphLegs sph_legs(const KParams* __restrict__ K) {
+  SphLegs r;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    r.b[l] = __builtin_amdgcn_readfirstlane(K->leg_sph_begin[l]);
+    r.e[l] = __builtin_amdgcn_readfirstlane(K->leg_sph_end[l]);
+  }
+  return r;
+}
+__device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
+  int l = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) l = (s >= L.b[k] && s < L.e[k]) ? k : l;
+  return l;
+}
 
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau, float mb, const float* Ib, V3 cb,
                         float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
                         unsigned long long* prof) {
   LRL_PROF_DECL
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
+  const SphLegs SL = sph_legs(K);
   const lrl_env_params& P = K->p;
   const float dt = P.sim_dt;
   const M3 R = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
@@ -629,7 +655,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     if (m) {
       const int s = __builtin_ctzll(m);
       m &= m - 1ull;
-      contact_setup(M, Sch, R, s, K->sph_leg[s], K->sph_link[s]);
+      contact_setup(M, Sch, R, s, sph_leg_of(SL, s), K->sph_link[s]);
     }
   }
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
@@ -646,7 +672,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (m) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        apply_impulse(M, s, K->sph_leg[s], M.sph(s, 10), M.sph(s, 11), M.sph(s, 12), dvb);
+        apply_impulse(M, s, sph_leg_of(SL, s), M.sph(s, 10), M.sph(s, 11), M.sph(s, 12), dvb);
       }
     }
 #pragma unroll
@@ -662,7 +688,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (m) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        contact_pgs(M, s, K->sph_leg[s], mu, vbc);
+        contact_pgs(M, s, sph_leg_of(SL, s), mu, vbc);
       }
     }
   LRL_PROF(3)  // PGS iterations

@@ -9,9 +9,17 @@
 // the weight gradient) may be gathered through an int64 row list — the minibatch indices of
 // RolloutStorage.mini_batch_generator (rollout_storage.py:100-137) — so the minibatch is never copied.
 //
-// A workgroup (4 waves) owns a BM x BN tile (128/64 wide, 32 for thin layers); slices of BK = 32 stage through
-// LDS k-major ([k][m] / [k][n]) so each MFMA operand is one conflict-free ds_read_b32 per lane; the
-// next tile is prefetched into registers while the current one is consumed (one barrier per tile).
+// Three kernels behind one launcher (gemm_launch picks by shape):
+//  * LDS-DMA (NT / NN, every tile interior, float4-aligned operands): 64 x 64 tile, 16-k slices land in a
+//    3-stage LDS ring straight from global memory (global_load_lds_dwordx4, counted vmcnt waits, swizzled
+//    images read with ds_read_b128), two accumulators per wave;
+//  * thin (NT / NN, N <= 32, k = 512 / 1024): op(B) kept in registers per k-quarter, A streamed a block
+//    ahead, quarter sums added in wave order;
+//  * register-staged (everything else, incl. the split-k weight gradients): a workgroup (4 waves) owns a
+//    BM x BN tile (128 / 64 wide, 32 for thin layers); 16-k slices stage through LDS k-major so each MFMA
+//    operand is one ds_read_b32 per lane; the next slice is prefetched into registers while the current one
+//    is consumed; the tile order is XCD-aware (consecutive tiles on one XCD share the A row block).
+// Every path sums k in a fixed order: results are deterministic run to run.
 #pragma once
 #include <stdint.h>
 

@@ -3,6 +3,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/lrl.h"
 #include "lrl_gemm.h"
 
@@ -454,6 +456,116 @@ __global__ __launch_bounds__(GTHREADS) void gemm_glds_kernel(GemmP p) {
   }
 }
 
+
+// ---- thin products: C[M][N <= 32] = A[M][K] op(B), K = 128 NBK (512 or 1024) ----
+// (the latent gradient dY W[:, 42:60] over k = 1024, the 18-/32-wide output layers.)  A register-staged
+// 32-wide tile wastes most of its loads here and a split-k launch pays a partial round trip through HBM,
+// so: a workgroup's 4 waves take k in quarters; each lane keeps its column of op(B) for the whole quarter
+// in registers (loaded once per workgroup; lanes past N hold zeros), the workgroup walks 32-row tiles
+// (persistent grid) with A streamed from global memory one 32-k block ahead (lane (i, h) loads row i's
+// float4s at k = 8v + 4h, the k-permutation its B registers follow), and the quarter sums are added in
+// wave order (fixed, deterministic) before the epilogue.
+template <int LAYOUT, int EPI, int NBK>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_thin_kernel(GemmP p) {
+  __shared__ float red[3 * 16 * 64];
+  constexpr bool BNC = (LAYOUT & 2) != 0;
+  const int N = p.N, M = p.M;
+  const int g = blockIdx.y;
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ B = p.B + g * p.gb;
+  float* __restrict__ C = p.C + g * p.gc;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 31, h = lane >> 5;
+  const int kbeg = w * 32 * NBK;
+  const bool colv = li < N;
+  float breg[NBK][16];
+#pragma unroll
+  for (int kb = 0; kb < NBK; ++kb)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int k = kbeg + 32 * kb + 8 * (t >> 2) + 4 * h + (t & 3);
+      breg[kb][t] = colv ? (BNC ? B[(int64_t)k * p.ldb + li] : B[(int64_t)li * p.ldb + k]) : 0.f;
+    }
+  const int mt = (M + 31) >> 5;
+  auto rowp = [&](int t) -> const float* {
+    const int row = t * 32 + li;
+    if (t >= mt || row >= M) return nullptr;
+    return A + (p.a_rows ? p.a_rows[row] : (int64_t)row) * p.lda + kbeg + 4 * h;
+  };
+  auto load = [&](const float* ar, int kb, float4* dst) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      dst[v] = ar ? *reinterpret_cast<const float4*>(ar + 32 * kb + 8 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const float* ar = rowp(blockIdx.x);
+  float4 cur[4];
+  load(ar, 0, cur);
+  for (int t = blockIdx.x; t < mt; t += gridDim.x) {
+    const float* arn = rowp(t + gridDim.x);
+    f32x16 acc, acc2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NBK; ++kb) {
+      float4 nxt[4];
+      if (kb + 1 < NBK) load(ar, kb + 1, nxt);
+      else load(arn, 0, nxt);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const float av = (s & 3) == 0 ? cur[s >> 2].x : (s & 3) == 1 ? cur[s >> 2].y : (s & 3) == 2 ? cur[s >> 2].z : cur[s >> 2].w;
+        if (s & 1) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, breg[kb][s], acc2, 0, 0, 0);
+        else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, breg[kb][s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) cur[v] = nxt[v];
+    }
+    ar = arn;
+    if (w > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((w - 1) * 16 + r) * 64 + lane] = acc[r] + acc2[r];
+    }
+    __syncthreads();
+    if (w == 0) {
+      float bj = 0.f;
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = colv ? p.bias[g * p.gbias + li] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = acc[r] + acc2[r];
+        v += red[r * 64 + lane];
+        v += red[(16 + r) * 64 + lane];
+        v += red[(32 + r) * 64 + lane];
+        if constexpr (EPI == EPI_BIAS) v += bj;
+        if constexpr (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+        const int orow = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (colv && orow < M) C[(int64_t)orow * p.ldc + li] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int LAYOUT, int EPI, int NBK>
+static int launch_thin_k(const GemmP& p, int groups, hipStream_t st) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return LRL_E_HIP;
+    ncu = prop.multiProcessorCount;
+  }
+  const int mt = (p.M + 31) / 32;
+  const int gx = std::max(1, std::min(mt, 2 * ncu / std::max(1, groups)));
+  hipLaunchKernelGGL((gemm_thin_kernel<LAYOUT, EPI, NBK>), dim3(gx, groups), dim3(GTHREADS), 0, st, p);
+  return 0;
+}
+template <int LAYOUT, int EPI>
+static int launch_thin(const GemmP& p, int groups, hipStream_t st) {
+  switch (p.K / 128) {
+    case 4: return launch_thin_k<LAYOUT, EPI, 4>(p, groups, st);
+    case 8: return launch_thin_k<LAYOUT, EPI, 8>(p, groups, st);
+  }
+  return LRL_E_INVALID;
+}
+
 template <int BM, int BN>
 static int launch_bm(const GemmP& p, int layout, int epi, dim3 grid, hipStream_t st) {
 #define LRL_GEMM_LAUNCH(L, E) hipLaunchKernelGGL((gemm_kernel<BM, BN, L, E>), grid, dim3(GTHREADS), 0, st, p)
@@ -547,6 +659,24 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
       else LRL_GLDS(GEMM_NN, EPI_DELU);
     }
 #undef LRL_GLDS
+    return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  }
+  // thin output (N <= 32): B staged whole in LDS, k split over the workgroup's waves
+  const int kb128 = p.K / 128;
+  if (layout != GEMM_TN && p.splits == 1 && p.N <= 32 && p.K % 128 == 0 && p.avec == 4 && p.M >= 256 &&
+      (kb128 == 4 || kb128 == 8) &&  // (shorter k: the register-staged 128 x 32 tile is as fast)
+      (epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_ELU)) {
+    int trc = LRL_E_INVALID;
+    if (layout == GEMM_NT) {
+      if (epi == EPI_STORE) trc = launch_thin<GEMM_NT, EPI_STORE>(p, groups, st);
+      else if (epi == EPI_BIAS) trc = launch_thin<GEMM_NT, EPI_BIAS>(p, groups, st);
+      else trc = launch_thin<GEMM_NT, EPI_BIAS_ELU>(p, groups, st);
+    } else {
+      if (epi == EPI_STORE) trc = launch_thin<GEMM_NN, EPI_STORE>(p, groups, st);
+      else if (epi == EPI_BIAS) trc = launch_thin<GEMM_NN, EPI_BIAS>(p, groups, st);
+      else trc = launch_thin<GEMM_NN, EPI_BIAS_ELU>(p, groups, st);
+    }
+    if (trc) return trc;
     return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
   }
   int rc = LRL_E_INVALID;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -475,6 +476,8 @@ struct Seg {
   int64_t len, stride;
   int parts;
   float scale;
+  int lpg;      // log2 of the part groups a workgroup splits the parts into (set by launch_seg)
+  int blk0, nblk;  // this segment's workgroups in the packed 1-D grid (set by launch_seg)
 };
 constexpr int MAX_SEGS = 24;
 struct SegList {
@@ -482,34 +485,44 @@ struct SegList {
   int n;
 };
 
-__global__ void seg_reduce_kernel(SegList L) {
-  const Seg& sg = L.s[blockIdx.y];
-  if (sg.parts >= 64 && sg.len <= 8192) {
-    // many parts, few elements (per-workgroup head partials): one wave per element, lanes stride over
-    // the parts, fixed shuffle tree (deterministic)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int64_t i = (int64_t)blockIdx.x * nw + w; i < sg.len; i += (int64_t)gridDim.x * nw) {
-      float acc = 0.f;
-      for (int q = lane; q < sg.parts; q += 64) acc += sg.src[(int64_t)q * sg.stride + i];
-      for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-      if (lane == 0) sg.dst[i] = acc * sg.scale;
-    }
-    return;
-  }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.len; i += (int64_t)gridDim.x * blockDim.x) {
-    // 8 independent loads in flight per step, summed in part order (deterministic)
+// dst[i] = scale * sum_q src[q * stride + i].  A 256-thread workgroup covers E = 256 / PG consecutive
+// elements with PG part groups: thread (g, e) sums parts g, g + PG, ... (8 loads in flight, coalesced over e),
+// then group 0 adds the PG partial sums in group order — a fixed order, so the result is deterministic.
+// Few-element / many-part segments (per-workgroup head partials, thin weight gradients) use large PG.
+__global__ __launch_bounds__(256) void seg_reduce_kernel(SegList L) {
+  int si = 0;
+  while (si + 1 < L.n && (int)blockIdx.x >= L.s[si + 1].blk0) ++si;
+  const Seg& sg = L.s[si];
+  const int lpg = sg.lpg, pg = 1 << lpg, E = 256 >> lpg;
+  const int e = threadIdx.x & (E - 1), g = threadIdx.x >> (8 - lpg);
+  __shared__ float red[256];
+  for (int64_t base = (int64_t)(blockIdx.x - sg.blk0) * E; base < sg.len; base += (int64_t)sg.nblk * E) {
+    const int64_t i = base + e;
     float acc = 0.f;
-    const float* p = sg.src + i;
-    int q = 0;
-    for (; q + 8 <= sg.parts; q += 8) {
-      float v[8];
+    if (i < sg.len) {
+      const float* p = sg.src + i;
+      int q = g;
+      for (; q + 7 * pg < sg.parts; q += 8 * pg) {
+        float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(q + u) * sg.stride);
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(q + u * pg) * sg.stride);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+      for (; q < sg.parts; q += pg) acc += p[(int64_t)q * sg.stride];
     }
-    for (; q < sg.parts; ++q) acc += p[(int64_t)q * sg.stride];
-    sg.dst[i] = acc * sg.scale;
+    if (pg == 1) {
+      if (i < sg.len) sg.dst[i] = acc * sg.scale;
+      continue;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (g == 0 && i < sg.len) {
+      float t = 0.f;
+      for (int k = 0; k < pg; ++k) t += red[k * E + e];
+      sg.dst[i] = t * sg.scale;
+    }
+    __syncthreads();
   }
 }
 
@@ -634,7 +647,7 @@ static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
   int64_t ph1 = tn_part_floats(n.ac_h2, n.ac_h1, B, 2) + tn_part_floats(n.ac_h1, n.ac_h0, B, 2) +
                 tn_part_floats(2 * n.ac_h0, n.num_obs + n.latent, B, 1) + tn_part_floats(n.latent, n.enc_h1, B, 1) +
                 tn_part_floats(n.enc_h1, n.enc_h0, B, 1) + tn_part_floats(n.enc_h0, n.num_priv, B, 1) +
-                (int64_t)hb * hp_len(n.num_actions) + 64 * 8 + 16 * Bl * LATS;  // + split-k d latent
+                (int64_t)hb * hp_len(n.num_actions) + 64 * 8;
   int64_t ph3 = tn_part_floats(n.ad_h1, n.ad_h0, B, 1) + tn_part_floats(n.ad_h0, n.num_hist, B, 1) +
                 (int64_t)hb * (n.latent * n.ad_h1 + n.latent + 1) + 64 * 4;
   p.part_floats = std::max(ph1, ph3);
@@ -705,23 +718,6 @@ struct G {
     p.ga = gy; p.gb = gw; p.gc = gx; p.gaux = gaux;
     rc = gemm_launch(p, GEMM_NN, aux ? EPI_DELU : EPI_STORE, groups, st);
   }
-  // thin, long-k dX = dY W (no activation): split over k into partials + an immediate reduction
-  // (a 128x32 tile walking k = 1024 alone is load-latency bound)
-  void nn_splitk(const float* dY, int64_t ldy, const float* W, int64_t ldw, float* dX, int64_t ldx, int M, int N,
-                 int K, float* part) {
-    if (rc) return;
-    const int splits = std::max(1, std::min(16, K / 64));
-    if (part + (int64_t)splits * M * ldx > part_end) { rc = LRL_E_INVALID; return; }
-    GemmP p{};
-    p.A = dY; p.lda = ldy; p.B = W; p.ldb = ldw; p.C = part; p.ldc = ldx;
-    p.M = M; p.N = N; p.K = K; p.splits = splits; p.kps = (K + splits - 1) / splits;
-    p.part_stride = (int64_t)M * ldx;
-    rc = gemm_launch(p, GEMM_NN, EPI_PARTIAL, 1, st);
-    if (rc) return;
-    SegList L{};
-    L.s[L.n++] = Seg{part, dX, (int64_t)M * ldx, (int64_t)M * ldx, splits, 1.f};
-    launch_seg(L, st);
-  }
   // partial dW[o][i] = sum_b dY[b][o] X[rows(b)][i]; returns the segments (weights then biases)
   void tn(const float* dY, int64_t ldy, const float* X, int64_t ldx, const int64_t* rows, int M, int N, int K,
           int groups, int64_t gy, int64_t gx, float*& part, float* dw, float* db, SegList& L) {
@@ -745,11 +741,20 @@ struct G {
   }
 };
 
-static void launch_seg(const SegList& L, hipStream_t st) {
-  int64_t mx = 1;
-  for (int i = 0; i < L.n; ++i) mx = std::max(mx, L.s[i].len);
-  const int bx = (int)std::min<int64_t>((mx + 255) / 256, 2048);
-  hipLaunchKernelGGL(seg_reduce_kernel, dim3(bx, L.n), dim3(256), 0, st, L);
+static void launch_seg(const SegList& L0, hipStream_t st) {
+  SegList L = L0;
+  int total = 0;
+  for (int i = 0; i < L.n; ++i) {
+    Seg& s = L.s[i];
+    // split the parts over more groups while the segment's grid is small and each group keeps >= 4 parts
+    int lpg = 0;
+    while (lpg < 6 && (4 << (lpg + 1)) <= s.parts && (s.len << lpg) < 2048 * 256) ++lpg;
+    s.lpg = lpg;
+    s.nblk = (int)std::min<int64_t>((s.len + (256 >> lpg) - 1) / (256 >> lpg), 2048);
+    s.blk0 = total;
+    total += s.nblk;
+  }
+  if (total > 0) hipLaunchKernelGGL(seg_reduce_kernel, dim3(total), dim3(256), 0, st, L);
 }
 
 }  // namespace lrl
@@ -893,7 +898,7 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
   g.tn(P.dh1, 2 * h0, P.xa, XS, nullptr, 2 * h0, nx, B, 1, 0, 0, part, grads + n.w1, grads + n.b1, L);
   // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
-  g.nn_splitk(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, B, n.latent, 2 * h0, part);
+  g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
   g.tn(P.dlat, LATS, P.he2, n.enc_h1, nullptr, n.latent, n.enc_h1, B, 1, 0, 0, part, grads + n.e3w, grads + n.e3b, L);
   g.nn(P.dlat, LATS, w + n.e3w, n.enc_h1, P.dhe2, n.enc_h1, P.he2, n.enc_h1, B, n.enc_h1, n.latent);
   g.tn(P.dhe2, n.enc_h1, P.he1, n.enc_h0, nullptr, n.enc_h1, n.enc_h0, B, 1, 0, 0, part, grads + n.e2w, grads + n.e2b, L);
@@ -1006,7 +1011,11 @@ extern "C" int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t 
   if (layout == GEMM_TN) {
     // split-k into the workspace, then reduce into C (C must be [M][N] contiguous: ldc == N)
     if (ldc != N) return lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: TN needs ldc == N");
-    const int splits = gemm_pick_splits(M, N, K, 1);
+    int splits = gemm_pick_splits(M, N, K, 1);
+    if (const char* e = getenv("LRL_GEMM_SPLITS")) {  // development knob (scripts/tn_sweep.py)
+      const int s = atoi(e);
+      if (s > 0) splits = s;
+    }
     if ((int64_t)splits * ((int64_t)M * N + M) > workspace_floats)
       return lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: workspace too small");
     p.b_rows = rows; p.splits = splits; p.kps = (K + splits - 1) / splits;

@@ -1,7 +1,8 @@
 """fp32 MFMA GEMM of the native PPO update (csrc/lrl_gemm.hip, through lrl_gemm_f32) against a plain
 torch fp32 reference of the same op: the three layouts an MLP's forward / backward-data / weight-gradient
 need, every epilogue, gathered rows, ragged and unaligned shapes; the 64-aligned float4 shapes take the
-LDS-DMA kernel, the others the register-staged one."""
+LDS-DMA kernel, outputs <= 32 wide with k = 512 / 1024 the thin kernel (B in registers), the others the
+register-staged one."""
 import ctypes as C
 
 import numpy as np
@@ -35,7 +36,9 @@ def _tol(ref, k):
 @pytest.mark.parametrize("M,N,K,gather,epi", [(1024, 256, 512, True, 2), (2048, 1024, 64, False, 1),
                                                (1536, 128, 256, False, 0), (300, 200, 60, False, 2), (1000, 1024, 60, True, 2),
                                                (777, 256, 18, True, 2), (513, 18, 128, False, 1),
-                                               (640, 256, 630, True, 2), (64, 64, 16, False, 0)])
+                                               (640, 256, 630, True, 2), (64, 64, 16, False, 0),
+                                               (2048, 32, 512, True, 2), (4096, 18, 128, False, 1), (777, 7, 512, True, 0),
+                                               (1000, 24, 1024, False, 1)])
 def test_forward_nt(M, N, K, gather, epi):
     g = torch.Generator(device=dev).manual_seed(M * 7 + N)
     src_rows = M + 37
@@ -57,7 +60,7 @@ def test_forward_nt(M, N, K, gather, epi):
 
 @pytest.mark.parametrize("M,N,K,delu", [(1024, 512, 256, True), (1536, 256, 128, False), (300, 256, 128, True),
                                          (1000, 18, 1024, False), (513, 512, 256, True),
-                                         (96, 128, 18, True)])
+                                         (96, 128, 18, True), (3000, 18, 1024, False), (300, 32, 128, False)])
 def test_backward_data_nn(M, N, K, delu):
     g = torch.Generator(device=dev).manual_seed(M + 3 * N + K)
     dY = torch.randn(M, K, device=dev, generator=g)
