@@ -287,6 +287,8 @@ typedef struct lrl_ppo_batch {
   const float *obs, *priv, *hist, *actions, *values, *returns, *logp, *adv, *mu, *sigma;
   const int64_t* rows;
   int32_t batch;
+  int32_t hist_ld; /* row pitch of hist in floats (0 = num_hist).  A pitch of num_hist rounded up to 16 with
+                    * finite (zero) padding lets the adaptation module's first layer run on float4 rows. */
 } lrl_ppo_batch;
 
 typedef struct lrl_ppo_hparams { /* PPO_Args (ppo.py:15-34) + torch.optim.Adam defaults */
@@ -312,6 +314,7 @@ typedef struct lrl_ppo_ctrl {
 typedef struct lrl_rollout_store {
   float *obs, *priv, *hist, *actions, *values, *logp, *mu, *sigma;
   int32_t hist_dim;
+  int32_t hist_ld; /* row pitch of the history storage in floats (0 = hist_dim); padding is left untouched */
 } lrl_rollout_store;
 
 int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n);

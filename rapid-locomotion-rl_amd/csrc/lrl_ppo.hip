@@ -289,6 +289,43 @@ struct ActHeadArgs {
   int store_row, do_store;
 };
 
+// rows [0, nrows) of src (pitch sld) -> dst (pitch dld), `cols` floats each, by the block's HEAD_THREADS
+// threads with 8 loads in flight per thread (float2 when both sides allow)
+__device__ __forceinline__ void copy_rows(const float* __restrict__ src, int64_t sld, float* __restrict__ dst,
+                                          int64_t dld, int nrows, int cols, int t) {
+  if (((((uintptr_t)src | (uintptr_t)dst) & 7) == 0) && (((sld | dld | cols) & 1) == 0)) {
+    const int c2 = cols / 2, n = nrows * c2;
+    for (int i0 = t; i0 < n; i0 += 8 * HEAD_THREADS) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * HEAD_THREADS, r = i / c2, c = i - r * c2;
+        if (i < n) v[u] = reinterpret_cast<const float2*>(src + r * sld)[c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * HEAD_THREADS, r = i / c2, c = i - r * c2;
+        if (i < n) reinterpret_cast<float2*>(dst + r * dld)[c] = v[u];
+      }
+    }
+  } else {
+    const int n = nrows * cols;
+    for (int i0 = t; i0 < n; i0 += 8 * HEAD_THREADS) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * HEAD_THREADS, r = i / cols, c = i - r * cols;
+        if (i < n) v[u] = src[r * sld + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * HEAD_THREADS, r = i / cols, c = i - r * cols;
+        if (i < n) dst[r * dld + c] = v[u];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
   constexpr int HP = 2 * HEAD_W + 1;
   __shared__ float H[HEAD_ROWS][HP];
@@ -371,26 +408,13 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
       a.store.logp[so + g] = lp;
     }
   }
-  if (a.do_store) {  // obs / priv / history rows of this tile: contiguous spans in source and storage
+  if (a.do_store) {  // obs / priv / history rows of this tile into storage row `store_row`
     const int64_t b = so + r0;
-    for (int i = t; i < nrows * a.no; i += HEAD_THREADS) a.store.obs[b * a.no + i] = a.obs[(int64_t)r0 * a.no + i];
-    for (int i = t; i < nrows * a.np; i += HEAD_THREADS) a.store.priv[b * a.np + i] = a.priv[(int64_t)r0 * a.np + i];
+    copy_rows(a.obs + (int64_t)r0 * a.no, a.no, a.store.obs + b * a.no, a.no, nrows, a.no, t);
+    copy_rows(a.priv + (int64_t)r0 * a.np, a.np, a.store.priv + b * a.np, a.np, nrows, a.np, t);
     if (a.hist && a.store.hist) {
-      const int hd = a.store.hist_dim;
-      const float* src = a.hist + (int64_t)r0 * hd;
-      float* dst = a.store.hist + b * hd;
-      const int cnt = nrows * hd;
-      if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (cnt & 3) == 0) {
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        float4* d4 = reinterpret_cast<float4*>(dst);
-        for (int i = t; i < cnt / 4; i += HEAD_THREADS) d4[i] = s4[i];
-      } else if ((((uintptr_t)src | (uintptr_t)dst) & 7) == 0 && (cnt & 1) == 0) {
-        const float2* s2 = reinterpret_cast<const float2*>(src);
-        float2* d2 = reinterpret_cast<float2*>(dst);
-        for (int i = t; i < cnt / 2; i += HEAD_THREADS) d2[i] = s2[i];
-      } else {
-        for (int i = t; i < cnt; i += HEAD_THREADS) dst[i] = src[i];
-      }
+      const int hd = a.store.hist_dim, ld = a.store.hist_ld > hd ? a.store.hist_ld : hd;
+      copy_rows(a.hist + (int64_t)r0 * hd, hd, a.store.hist + b * ld, ld, nrows, hd, t);
     }
   }
 }
@@ -597,11 +621,22 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 }
 
 // ---------------------------------------------------------------------------------------------------
+// W[r][0:h) -> Wp[r][0:hp) with zero columns [h, hp): the adaptation module's first layer over history rows
+// stored at the padded pitch hp (the k-padding contributes exact zeros)
+__global__ void pad_cols_kernel(const float* __restrict__ W, int rows, int h, int hp, float* __restrict__ Wp) {
+  const int64_t n = (int64_t)rows * hp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / hp), c = (int)(i - (int64_t)r * hp);
+    Wp[i] = c < h ? W[(int64_t)r * h + c] : 0.f;
+  }
+}
+
 // host side: workspace plan
 struct Plan {
   int B;
   float *xa, *he1, *he2, *h1, *h2, *h3, *dh3, *dh2, *dh1, *dlat, *dhe2, *dhe1;
   float *tgt, *hd1, *hd2, *dhd2, *dhd1;
+  float* wd1p;     // adaptation layer-1 weights at the padded history pitch (zero columns past num_hist)
   float* part;     // partial area (reused by phases 1 and 3)
   int64_t part_floats;
   int64_t bytes;
@@ -610,6 +645,8 @@ struct Plan {
 constexpr int XS = 64;      // X row pitch (obs + latent <= 64)
 constexpr int LATS = 32;    // latent-wide buffers pitch
 constexpr int HD2S = 32;    // adaptation hidden-2 pitch
+
+static int hist_pad(int h) { return (h + 15) / 16 * 16; }
 
 static int64_t tn_part_floats(int M, int N, int K, int groups) {
   const int s = gemm_pick_splits(M, N, K, groups);
@@ -643,6 +680,7 @@ static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
   p.hd2 = take(Bl * HD2S);
   p.dhd2 = take(Bl * HD2S);
   p.dhd1 = take(Bl * n.ad_h0);
+  p.wd1p = take((int64_t)n.ad_h0 * hist_pad(n.num_hist));
   const int hb = (B + HEAD_ROWS - 1) / HEAD_ROWS;
   int64_t ph1 = tn_part_floats(n.ac_h2, n.ac_h1, B, 2) + tn_part_floats(n.ac_h1, n.ac_h0, B, 2) +
                 tn_part_floats(2 * n.ac_h0, n.num_obs + n.latent, B, 1) + tn_part_floats(n.latent, n.enc_h1, B, 1) +
@@ -798,7 +836,7 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   if (!params || !obs || !priv || !actions || !workspace || n <= 0)
     return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: null argument or n <= 0");
   if (store && (!store->obs || !store->priv || !store->actions || !store->values || !store->logp || !store->mu ||
-                !store->sigma || store->hist_dim < 0))
+                !store->sigma || store->hist_dim < 0 || (store->hist_ld != 0 && store->hist_ld < store->hist_dim)))
     return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: incomplete rollout store");
   const lrl_ppo_net& nt = *net;
   ActPlan P = make_act_plan(nt, n, static_cast<char*>(workspace));
@@ -953,7 +991,17 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
   g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
   g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.tgt, LATS, w + n.e3b, B, n.latent, n.enc_h1, false);
   // prediction = adaptation_module(obs_history)
-  g.nt(bt->hist, n.num_hist, bt->rows, w + n.d1w, n.num_hist, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, n.num_hist, true);
+  const int hld = bt->hist_ld ? bt->hist_ld : n.num_hist, hpad = hist_pad(n.num_hist);
+  if (hld < n.num_hist) return lrl_set_error(LRL_E_INVALID, "lrl_ppo_adaptation: hist_ld < num_hist");
+  if (hld >= hpad && hld % 4 == 0 && ((uintptr_t)bt->hist & 15) == 0 && hpad != n.num_hist) {
+    // history rows carry finite padding up to hpad: run k = hpad against zero-padded weights (float4 rows)
+    const int64_t cnt = (int64_t)n.ad_h0 * hpad;
+    hipLaunchKernelGGL(pad_cols_kernel, dim3((unsigned)std::min<int64_t>((cnt + 255) / 256, 1024)), dim3(256), 0, st,
+                       w + n.d1w, n.ad_h0, n.num_hist, hpad, P.wd1p);
+    g.nt(bt->hist, hld, bt->rows, P.wd1p, hpad, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, hpad, true);
+  } else {
+    g.nt(bt->hist, hld, bt->rows, w + n.d1w, n.num_hist, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, n.num_hist, true);
+  }
   g.nt(P.hd1, n.ad_h0, nullptr, w + n.d2w, n.ad_h0, P.hd2, HD2S, w + n.d2b, B, n.ad_h1, n.ad_h0, true);
   if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_adaptation: forward GEMM launch failed");
   SegList L{};
@@ -973,7 +1021,7 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
   }
   g.tn(P.dhd2, HD2S, P.hd1, n.ad_h0, nullptr, n.ad_h1, n.ad_h0, B, 1, 0, 0, part, grads + n.d2w, grads + n.d2b, L);
   g.nn(P.dhd2, HD2S, w + n.d2w, n.ad_h0, P.dhd1, n.ad_h0, P.hd1, n.ad_h0, B, n.ad_h0, n.ad_h1);
-  g.tn(P.dhd1, n.ad_h0, bt->hist, n.num_hist, bt->rows, n.ad_h0, n.num_hist, B, 1, 0, 0, part, grads + n.d1w,
+  g.tn(P.dhd1, n.ad_h0, bt->hist, hld, bt->rows, n.ad_h0, n.num_hist, B, 1, 0, 0, part, grads + n.d1w,
        grads + n.d1b, L);
   if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_adaptation: backward GEMM launch failed");
   launch_seg(L, st);

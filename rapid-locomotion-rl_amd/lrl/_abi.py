@@ -78,7 +78,7 @@ class LrlTensor(C.Structure):
 class LrlRolloutStore(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("priv", C.c_void_p), ("hist", C.c_void_p), ("actions", C.c_void_p),
                 ("values", C.c_void_p), ("logp", C.c_void_p), ("mu", C.c_void_p), ("sigma", C.c_void_p),
-                ("hist_dim", i32)]
+                ("hist_dim", i32), ("hist_ld", i32)]
 
 
 i64 = C.c_int64
@@ -94,7 +94,7 @@ class LrlPpoNet(C.Structure):
 
 class LrlPpoBatch(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("obs", "priv", "hist", "actions", "values", "returns", "logp", "adv", "mu",
-                                          "sigma", "rows")] + [("batch", i32)]
+                                          "sigma", "rows")] + [("batch", i32), ("hist_ld", i32)]
 
 
 class LrlPpoHparams(C.Structure):

@@ -189,12 +189,13 @@ class PPO:
                     hist=flat(s.observation_histories), actions=flat(s.actions), values=flat(s.values),
                     returns=flat(s.returns), logp=flat(s.actions_log_prob), adv=flat(s.advantages), mu=flat(s.mu),
                     sigma=flat(s.sigma))
-        for v in bufs.values():
-            assert v.is_contiguous() and v.dtype == torch.float32
+        for k, v in bufs.items():
+            assert v.dtype == torch.float32 and (v.is_contiguous() or (k == "hist" and v.stride(1) == 1)), k
         batch = _abi.LrlPpoBatch()
         for k, v in bufs.items():
             setattr(batch, k, v.data_ptr())
         batch.batch = mb
+        batch.hist_ld = bufs["hist"].stride(0)
         ctrl = st["ctrl"]
         ctrl[0] = self.learning_rate
         ctrl[1:4] = 0.0

@@ -39,7 +39,15 @@ class RolloutStorage:
         z = lambda *s: torch.zeros(T, N, *s, device=device)
         self.observations = z(*obs_shape)
         self.privileged_observations = z(*privileged_obs_shape)
-        self.observation_histories = z(*obs_history_shape)
+        # history rows at a 16-float pitch (zero padding): the adaptation module's first layer then reads
+        # float4-aligned rows (lrl_ppo_batch.hist_ld); the [T, N, H] view keeps the reference's shape
+        h = int(obs_history_shape[0]) if len(obs_history_shape) == 1 else None
+        if h is not None and h % 16:
+            hp = (h + 15) // 16 * 16
+            self._hist_padded = torch.zeros(T, N, hp, device=device)
+            self.observation_histories = self._hist_padded[..., :h]
+        else:
+            self.observation_histories = z(*obs_history_shape)
         self.rewards = z(1)
         self.actions = z(*actions_shape)
         self.dones = z(1).byte()
@@ -63,6 +71,7 @@ class RolloutStorage:
         s.actions, s.values, s.logp = self.actions.data_ptr(), self.values.data_ptr(), self.actions_log_prob.data_ptr()
         s.mu, s.sigma = self.mu.data_ptr(), self.sigma.data_ptr()
         s.hist_dim = self.obs_history_shape[0]
+        s.hist_ld = self.observation_histories.stride(1)
         return s
 
     def add_transitions(self, transition, fused=False):

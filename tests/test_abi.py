@@ -36,7 +36,8 @@ def test_struct_layout_matches_header():
 int main(){printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_model), sizeof(lrl_env_params), sizeof(lrl_tensor),
  offsetof(lrl_env_params, noise_vec), offsetof(lrl_env_params, max_episode_length), sizeof(lrl_rollout_store));
 printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_ppo_net), offsetof(lrl_ppo_net, total), sizeof(lrl_ppo_batch),
- offsetof(lrl_ppo_batch, batch), sizeof(lrl_ppo_hparams), sizeof(lrl_ppo_ctrl));return 0;}
+ offsetof(lrl_ppo_batch, batch), sizeof(lrl_ppo_hparams), sizeof(lrl_ppo_ctrl));
+printf("%zu %zu\n", offsetof(lrl_ppo_batch, hist_ld), offsetof(lrl_rollout_store, hist_ld));return 0;}
 """
     exe = "/tmp/lrl_layout_check"
     src = exe + ".c"
@@ -47,7 +48,7 @@ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_ppo_net), offsetof(lrl_ppo_net, t
                    _abi.LrlEnvParams.noise_vec.offset, _abi.LrlEnvParams.max_episode_length.offset,
                    C.sizeof(_abi.LrlRolloutStore), C.sizeof(_abi.LrlPpoNet), _abi.LrlPpoNet.total.offset,
                    C.sizeof(_abi.LrlPpoBatch), _abi.LrlPpoBatch.batch.offset, C.sizeof(_abi.LrlPpoHparams),
-                   _abi.PPO_CTRL_BYTES]
+                   _abi.PPO_CTRL_BYTES, _abi.LrlPpoBatch.hist_ld.offset, _abi.LrlRolloutStore.hist_ld.offset]
 
 
 def test_product_fails_loudly_without_gpu():

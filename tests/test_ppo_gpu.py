@@ -107,6 +107,8 @@ def test_ppo_rollout_gae_update_match_reference():
     np.testing.assert_allclose(alg.storage.returns.cpu().numpy(), g["returns"], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(alg.storage.advantages.cpu().numpy(), g["advantages"], rtol=1e-4, atol=1e-4)
     np.testing.assert_array_equal(alg.storage.observation_histories.cpu().numpy(), g["hist_seq"][:T])
+    assert alg.storage.observation_histories.stride(1) == 640  # padded pitch; the padding stays zero
+    assert not alg.storage._hist_padded[..., 630:].any()
     alg.record_lr = True
     perm = torch.as_tensor(g["perm"], device="cuda:0")
     orig = torch.randperm
@@ -187,10 +189,12 @@ def _random_storage(alg, N, T, seed=1):
         st.actions_log_prob.copy_(-11.0 + torch.randn(st.values.shape, device="cuda:0", generator=g))
 
 
-def test_native_minibatch_gradients_match_autograd():
+@pytest.mark.parametrize("padded_hist", [True, False])
+def test_native_minibatch_gradients_match_autograd(padded_hist):
     """One minibatch of lrl_ppo_forward_backward / lrl_ppo_adaptation_forward_backward against torch
     autograd of the reference's loss (ppo.py:98-147, 157-166): every parameter's gradient, the KL mean,
-    the losses."""
+    the losses.  History rows either at the storage's padded pitch (640: the float4 / zero-k-padding
+    path of the adaptation module's first layer) or packed (630)."""
     import ctypes as C
     import torch.nn.functional as F
     from lrl.ppo.actor_critic import ActorCritic
@@ -213,6 +217,12 @@ def test_native_minibatch_gradients_match_autograd():
                      adv=s.advantages, mu=s.mu, sigma=s.sigma).items():
         setattr(batch, k, fl(t).data_ptr())
     batch.rows, batch.batch = rows.data_ptr(), mb
+    hist_flat = fl(s.observation_histories)
+    if not padded_hist:
+        hist_flat = hist_flat.contiguous()
+        batch.hist = hist_flat.data_ptr()
+    assert hist_flat.stride(0) == (640 if padded_hist else 630)
+    batch.hist_ld = hist_flat.stride(0)
     p = lambda t: C.c_void_p(t.data_ptr())
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     L = _abi.lib()
