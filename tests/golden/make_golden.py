@@ -19,8 +19,10 @@ Fixtures written (all small .npz, inputs + expected outputs):
   ppo_update.npz      PPO.act/process_env_step/compute_returns/update (ppo.py:62-178) with
                       deterministic weights (see ``init_params``) and injected randomness.
   state_dict_keys.json  ActorCritic state-dict layout (actor_critic.py, 35 keys incl. encoder.*)
+  checkpoint_last.npz   the reference run's trained ac_weights_last.pt (loaded weights_only=True) and the
+                      reference ActorCritic's teacher / student / value outputs on it for fixed inputs.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [generator ...]
 """
 import json
 import os
@@ -518,9 +520,36 @@ def gen_ppo():
     print("ppo: lr", lrs[:4], "losses", mv, ms_, ma)
 
 
+# ----------------------------------------------------------------------------------------
+CKPT = REF + "/runs/rapid-locomotion/example/train/201852.132488/checkpoints/ac_weights_last.pt"
+
+
+def gen_checkpoint():
+    """The reference's trained checkpoint (35-key ActorCritic state dict, loaded with weights_only=True)
+    and the reference ActorCritic's outputs on it: act_teacher / act_student (adaptation module on the
+    630-history) / evaluate / both latents (actor_critic.py:149-173) for fixed inputs."""
+    from mini_gym_learn.ppo.actor_critic import ActorCritic
+    sd = torch.load(CKPT, map_location="cpu", weights_only=True)
+    ac = ActorCritic(42, 18, 630, 12)
+    ac.load_state_dict(sd, strict=True)
+    rng = np.random.default_rng(31)
+    q = lambda a: (np.round(a * 64) / 64).astype(np.float32)
+    n = 64
+    obs, priv, hist = q(rng.normal(size=(n, 42))), q(rng.normal(size=(n, 18))), q(rng.normal(size=(n, 630)))
+    with torch.no_grad():
+        ti, si = {}, {}
+        mean_t = ac.act_teacher(torch.tensor(obs), torch.tensor(priv), ti).numpy()
+        mean_s = ac.act_student(torch.tensor(obs), torch.tensor(hist), si).numpy()
+        value = ac.evaluate(torch.tensor(obs), torch.tensor(priv)).numpy()
+    out = {"sd/" + k: v.numpy() for k, v in sd.items()}
+    out.update(keys=np.array(list(sd.keys())), obs=obs, priv=priv, hist=hist, mean_teacher=mean_t,
+               mean_student=mean_s, value=value, latent_teacher=ti["latents"], latent_student=si["latents"])
+    np.savez_compressed(os.path.join(HERE, "checkpoint_last.npz"), **out)
+    print("checkpoint:", len(sd), "tensors,", sum(v.numel() for v in sd.values()), "values")
+
+
 if __name__ == "__main__":
-    gen_post_physics("mc")
-    gen_post_physics("go1")
-    gen_curriculum()
-    gen_gae()
-    gen_ppo()
+    gens = dict(post_physics_mc=lambda: gen_post_physics("mc"), post_physics_go1=lambda: gen_post_physics("go1"),
+                curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint)
+    for name in (sys.argv[1:] or list(gens)):
+        gens[name]()

@@ -1,0 +1,65 @@
+"""Checkpoint compatibility: the reference run's trained ac_weights_last.pt
+(35-key state dict incl. the duplicate encoder.* registration, actor_critic.py:46-110) loads strictly into
+this ActorCritic and reproduces the reference's teacher / student / value outputs
+(tests/golden/checkpoint_last.npz, made by tests/golden/make_golden.py from the reference itself)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import GOLDEN, golden
+
+
+def _trained():
+    from lrl.ppo.actor_critic import ActorCritic
+    g = golden("checkpoint_last.npz")
+    sd = {k: torch.from_numpy(g["sd/" + k]) for k in g["keys"]}
+    ac = ActorCritic(42, 18, 630, 12)
+    ac.load_state_dict(sd, strict=True)
+    return ac, g
+
+
+def test_state_dict_layout_matches_reference():
+    from lrl.ppo.actor_critic import ActorCritic
+    ref = json.load(open(os.path.join(GOLDEN, "state_dict_keys.json")))
+    ours = [[k, list(v.shape)] for k, v in ActorCritic(42, 18, 630, 12).state_dict().items()]
+    assert ours == ref
+    assert sum(p.numel() for p in ActorCritic(42, 18, 630, 12).parameters()) == 603037
+
+
+def test_trained_checkpoint_outputs_match_reference():
+    ac, g = _trained()
+    obs, priv, hist = (torch.from_numpy(g[k]) for k in ("obs", "priv", "hist"))
+    with torch.no_grad():
+        ti, si = {}, {}
+        np.testing.assert_allclose(ac.act_teacher(obs, priv, ti).numpy(), g["mean_teacher"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(ac.act_student(obs, hist, si).numpy(), g["mean_student"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(ac.evaluate(obs, priv).numpy(), g["value"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(ti["latents"], g["latent_teacher"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(si["latents"], g["latent_student"], rtol=1e-5, atol=1e-5)
+    # the flat-buffer layout the native kernels use survives load_state_dict (views, not copies)
+    ac.flatten_parameters()
+    sd = {k: torch.from_numpy(g["sd/" + k]) for k in g["keys"]}
+    ac.load_state_dict(sd, strict=True)
+    assert ac.std.data_ptr() == ac._flat.data_ptr() + 4 * ac._net.std_off
+    with torch.no_grad():
+        np.testing.assert_allclose(ac.act_teacher(obs, priv).numpy(), g["mean_teacher"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_trained_checkpoint_fused_act_matches_reference():
+    """Native rollout act (lrl_ppo_act) and native student act (lrl_ppo_act_student) on the trained
+    weights: mean actions, values and latents against the reference's outputs."""
+    ac, g = _trained()
+    ac = ac.cuda()
+    d = lambda k: torch.from_numpy(g[k]).cuda()
+    eps = torch.zeros(64, 12, device="cuda:0")
+    actions, mu, values, logp = ac.act_fused(d("obs"), d("priv"), eps=eps)
+    np.testing.assert_allclose(mu.cpu().numpy(), g["mean_teacher"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(actions.cpu().numpy(), g["mean_teacher"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(values.cpu().numpy(), g["value"], rtol=1e-4, atol=1e-4)
+    mean_s, lat_s = ac.act_student_fused(d("obs"), d("hist"))
+    np.testing.assert_allclose(mean_s.cpu().numpy(), g["mean_student"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(lat_s.cpu().numpy(), g["latent_student"], rtol=1e-4, atol=1e-4)
