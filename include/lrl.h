@@ -323,6 +323,14 @@ int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, const float* ob
                     float* mu, float* values, float* logp, const lrl_rollout_store* store, int32_t store_row,
                     void* workspace, void* stream);
 
+/* Student act (actor_critic.py:160-164, the eval-env path of Runner.learn __init__.py:130-135 and the
+ * deployed policy of play.py): latent = adaptation_module(hist) (630 -> 256 -> 32 -> 18, ELU), mean =
+ * actor_body([obs, latent]) — deterministic, no sampling.  hist rows at pitch hist_ld (0 = num_hist; a
+ * 16-float pitch with finite padding takes the float4 path).  latent [n, latent] may be NULL. */
+int64_t lrl_ppo_act_student_workspace_bytes(const lrl_ppo_net* net, int32_t n);
+int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* params, const float* obs, const float* hist,
+                            int32_t hist_ld, int32_t n, float* mean, float* latent, void* workspace, void* stream);
+
 /* Workspace bytes for minibatches of `batch` rows. */
 int64_t lrl_ppo_workspace_bytes(const lrl_ppo_net* net, int32_t batch);
 /* Forward + backward of the PPO loss (ppo.py:98-147): writes grads[main_begin:main_end) and

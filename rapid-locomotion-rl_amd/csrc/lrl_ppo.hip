@@ -866,6 +866,76 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act: launch failed");
 }
 
+// ---- student act (actor_critic.py:160-164): latent = adaptation_module(hist), mean = actor_body([obs, latent]) ----
+struct StudentPlan {
+  float *xa, *hd1, *hd2, *h1, *h2, *h3, *wd1p;
+  int64_t bytes;
+};
+static StudentPlan make_student_plan(const lrl_ppo_net& n, int rows, char* base) {
+  StudentPlan p;
+  int64_t off = 0;
+  auto take = [&](int64_t floats) {
+    float* r = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += ((floats * 4 + 255) / 256) * 256;
+    return r;
+  };
+  const int64_t R = rows;
+  p.xa = take(R * XS);
+  p.hd1 = take(R * n.ad_h0);
+  p.hd2 = take(R * HD2S);
+  p.h1 = take(R * n.ac_h0);
+  p.h2 = take(R * n.ac_h1);
+  p.h3 = take(R * n.ac_h2);
+  p.wd1p = take((int64_t)n.ad_h0 * hist_pad(n.num_hist));
+  p.bytes = off;
+  return p;
+}
+
+extern "C" int64_t lrl_ppo_act_student_workspace_bytes(const lrl_ppo_net* net, int32_t n) {
+  if (check_net(net) || n <= 0) return -1;
+  return make_student_plan(*net, n, nullptr).bytes;
+}
+
+extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* params, const float* obs,
+                                       const float* hist, int32_t hist_ld, int32_t n, float* mean, float* latent,
+                                       void* workspace, void* stream) {
+  if (int rc = check_net(net)) return rc;
+  if (!params || !obs || !hist || !mean || !workspace || n <= 0)
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act_student: null argument or n <= 0");
+  const lrl_ppo_net& nt = *net;
+  const int hld = hist_ld ? hist_ld : nt.num_hist, hpad = hist_pad(nt.num_hist);
+  if (hld < nt.num_hist) return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act_student: hist_ld < num_hist");
+  StudentPlan P = make_student_plan(nt, n, static_cast<char*>(workspace));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  G g{st, nullptr};
+  const float* w = params;
+  const int nx = nt.num_obs + nt.latent;
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
+                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
+  if (hld >= hpad && hld % 4 == 0 && ((uintptr_t)hist & 15) == 0 && hpad != nt.num_hist) {
+    const int64_t cnt = (int64_t)nt.ad_h0 * hpad;
+    hipLaunchKernelGGL(pad_cols_kernel, dim3((unsigned)std::min<int64_t>((cnt + 255) / 256, 1024)), dim3(256), 0, st,
+                       w + nt.d1w, nt.ad_h0, nt.num_hist, hpad, P.wd1p);
+    g.nt(hist, hld, nullptr, P.wd1p, hpad, P.hd1, nt.ad_h0, w + nt.d1b, n, nt.ad_h0, hpad, true);
+  } else {
+    g.nt(hist, hld, nullptr, w + nt.d1w, nt.num_hist, P.hd1, nt.ad_h0, w + nt.d1b, n, nt.ad_h0, nt.num_hist, true);
+  }
+  g.nt(P.hd1, nt.ad_h0, nullptr, w + nt.d2w, nt.ad_h0, P.hd2, HD2S, w + nt.d2b, n, nt.ad_h1, nt.ad_h0, true);
+  g.nt(P.hd2, HD2S, nullptr, w + nt.d3w, nt.ad_h1, P.xa + nt.num_obs, XS, w + nt.d3b, n, nt.latent, nt.ad_h1, false);
+  // actor half of the grouped actor/critic layers (rows [0, h) of each grouped weight / bias)
+  g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, nt.ac_h0, w + nt.b1, n, nt.ac_h0, XS, true);  // k-padding: see phase 1
+  g.nt(P.h1, nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true);
+  g.nt(P.h2, nt.ac_h1, nullptr, w + nt.w3, nt.ac_h1, P.h3, nt.ac_h2, w + nt.b3, n, nt.ac_h2, nt.ac_h1, true);
+  g.nt(P.h3, nt.ac_h2, nullptr, w + nt.w4a, nt.ac_h2, mean, nt.num_actions, w + nt.b4a, n, nt.num_actions, nt.ac_h2,
+       false);
+  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_act_student: GEMM launch failed");
+  if (latent &&
+      hipMemcpy2DAsync(latent, (size_t)nt.latent * 4, P.xa + nt.num_obs, (size_t)XS * 4, (size_t)nt.latent * 4, n,
+                       hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return lrl_set_error(LRL_E_HIP, "lrl_ppo_act_student: latent copy failed");
+  return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act_student: launch failed");
+}
+
 extern "C" int64_t lrl_ppo_workspace_bytes(const lrl_ppo_net* net, int32_t batch) {
   if (check_net(net) || batch <= 0) return -1;
   return make_plan(*net, batch, nullptr).bytes;

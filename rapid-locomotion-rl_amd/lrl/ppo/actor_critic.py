@@ -179,6 +179,30 @@ class ActorCritic(nn.Module):
         return net
 
     # ---- fused HIP rollout path ----
+    def act_student_fused(self, obs, hist):
+        """act_student (actor_critic.py:160-164) on the flat parameters (lrl_ppo_act_student: adaptation
+        module + actor body as one fp32-MFMA GEMM chain).  ``hist`` may be a row-strided view (e.g. the
+        rollout storage's padded history).  Returns (actions_mean [N, A], latent [N, L])."""
+        n = obs.shape[0]
+        dev = obs.device
+        assert obs.is_contiguous() and obs.dtype == torch.float32 and hist.dtype == torch.float32
+        assert hist.dim() == 2 and hist.stride(1) == 1 and hist.shape[0] == n
+        net = self.flatten_parameters()
+        ws = getattr(self, "_student_ws", None)
+        if ws is None or ws[0] != n or ws[1].device != dev:
+            nbytes = _abi.lib().lrl_ppo_act_student_workspace_bytes(C.byref(net), C.c_int32(n))
+            if nbytes < 0:
+                raise RuntimeError("lrl_ppo_act_student_workspace_bytes rejected the network")
+            ws = self._student_ws = (n, torch.empty(nbytes, dtype=torch.uint8, device=dev))
+        mean = torch.empty(n, self.num_actions, device=dev)
+        latent = torch.empty(n, net.latent, device=dev)
+        ptr = lambda t: C.c_void_p(t.data_ptr())
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _abi.check(_abi.lib().lrl_ppo_act_student(C.byref(net), ptr(self._flat), ptr(obs), ptr(hist),
+                                                  C.c_int32(hist.stride(0)), C.c_int32(n), ptr(mean), ptr(latent),
+                                                  ptr(ws[1]), stream))
+        return mean, latent
+
     def act_fused(self, obs, priv, hist=None, eps=None, seed=0, counter=0, store=None, store_row=0):
         """PPO.act teacher path on the flat parameters (lrl_ppo_act: fp32-MFMA GEMM chain + one head
         kernel that samples, scores and writes the storage row).  Returns (actions, mu, values [N,1], logp [N])."""

@@ -102,6 +102,8 @@ class Runner:
             with torch.inference_mode():
                 for _ in range(self.num_steps_per_env):
                     actions = self.alg.act(obs[:n_train], priv[:n_train], hist[:n_train])
+                    if self.env.num_envs > n_train:  # eval envs: teacher or student means (__init__.py:130-135)
+                        actions = torch.cat((actions, self._eval_actions(obs, priv, hist, n_train, eval_expert)), 0)
                     obs_dict, rewards, dones, infos = self.env.step(actions)
                     obs, priv, hist = obs_dict["obs"], obs_dict["privileged_obs"], obs_dict["obs_history"]
                     self.alg.process_env_step(rewards[:n_train], dones[:n_train], infos)
@@ -117,6 +119,14 @@ class Runner:
             if RunnerArgs.save_interval and it % RunnerArgs.save_interval == 0:
                 self.save(it)
         self.current_learning_iteration += num_learning_iterations
+
+    def _eval_actions(self, obs, priv, hist, n_train, eval_expert):
+        ac = self.alg.actor_critic
+        if eval_expert:
+            return ac.act_teacher(obs[n_train:], priv[n_train:])
+        if self.alg.fused:
+            return ac.act_student_fused(obs[n_train:].contiguous(), hist[n_train:])[0]
+        return ac.act_student(obs[n_train:], hist[n_train:])
 
     def save(self, it):
         lg = self.logger
