@@ -233,6 +233,12 @@ int32_t lrl_sim_reset_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, void*
  * fork's custom-origin quirk), 1 writes base_init_state + env_origin + (xo, yo). */
 int32_t lrl_sim_reset_idx_ex(lrl_sim* sim, const int32_t* env_ids, int32_t n, int32_t root_mode, float xo, float yo,
                              void* stream);
+/* Upstream reset path (legged_robot.py:177 `reset_idx` inside post_physics_step, re-enabled with
+ * legacy_fork=False): after lrl_sim_step + lrl_sim_reset_idx_ex of the envs the step reset, re-run
+ * compute_observations (:342-417) for them from the post-reset state with the step's own noise draws, set
+ * last_actions / last_dof_vel / last_root_vel as post_physics_step does after reset_idx (:182-184), and with
+ * flags & LRL_STEP_HISTORY rewrite the newest history slot (the HistoryWrapper shift of that step). */
+int32_t lrl_sim_observe_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, uint32_t flags, void* stream);
 /* common_step_counter (legged_robot.py:153); lrl_sim_step increments it before the launch */
 int32_t lrl_sim_set_step_counter(lrl_sim* sim, int64_t counter);
 int32_t lrl_sim_set_root_state_indexed(lrl_sim* sim, const float* root /*[N,13] full tensor*/,

@@ -27,6 +27,7 @@ extern "C" int lrl_set_error(int code, const char* msg) { return fail(code, "%s"
 
 extern "C" {
 hipError_t lrl_launch_env_step(const KParams*, const KState*, int, const float*, uint32_t, int64_t, hipStream_t);
+hipError_t lrl_launch_observe(const KParams*, const KState*, const int32_t*, int32_t, uint32_t, int64_t, hipStream_t);
 hipError_t lrl_env_kernel_setup(int lds_bytes);
 hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, int64_t,
                             hipStream_t);
@@ -314,6 +315,12 @@ int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t 
   if (!s || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
   s->reset_counter += 1;
   HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, root_mode, xo, yo, s->reset_counter, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_observe_idx(lrl_sim* s, const int32_t* ids, int32_t n, uint32_t flags, void* stream) {
+  if (!s || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  HIPCHECK(lrl_launch_observe(s->dk, &s->S, ids, n, flags, s->step_counter, (hipStream_t)stream));
   return 0;
 }
 

@@ -774,6 +774,58 @@ __device__ __forceinline__ float nrm3(float x, float y, float z) { return sqrtf(
 // ------------------------------------------------------------------------------------------------
 // the fused step kernel
 // ------------------------------------------------------------------------------------------------
+// compute_observations (legged_robot.py:342-417): obs row (noise: U[-1,1] x noise_vec from the counter RNG
+// keyed by (env, step counter), so a re-evaluation after a reset draws the same noise) and priv-obs row
+__device__ __forceinline__ void obs_row(const lrl_env_params& P, const KState& S, int e, uint64_t genv,
+                                        int64_t step_counter, bool inject, V3 blv, V3 bav, V3 pg, const float* cmd,
+                                        const float* q, const float* qd, const float* act, float* ob) {
+  const int NO = P.num_obs;
+  int o = 0;
+  if (P.observe_vel) {
+    ob[o++] = blv.x * P.obs_scale_lin_vel; ob[o++] = blv.y * P.obs_scale_lin_vel; ob[o++] = blv.z * P.obs_scale_lin_vel;
+    ob[o++] = bav.x * P.obs_scale_ang_vel; ob[o++] = bav.y * P.obs_scale_ang_vel; ob[o++] = bav.z * P.obs_scale_ang_vel;
+  }
+  ob[o++] = pg.x; ob[o++] = pg.y; ob[o++] = pg.z;
+  if (P.observe_command) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ob[o++] = cmd[k] * P.commands_scale[k];
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ob[o + j] = (q[j] - P.default_dof_pos[j]) * P.obs_scale_dof_pos;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ob[o + 12 + j] = qd[j] * P.obs_scale_dof_vel;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ob[o + 24 + j] = act[j];
+  if (P.add_noise) {
+    for (int i0 = 0; i0 < NO; i0 += 4) {
+      lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter,
+                               (LRL_RNG_OBS_NOISE << 16) ^ (uint32_t)(step_counter >> 32), (uint32_t)(i0 >> 2), S.seed);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int i = i0 + k;
+        if (i < NO) {
+          float u = inject ? S.inj_noise[(size_t)e * NO + i] : lrl_u01(r.v[k]);
+          ob[i] += (2.f * u - 1.f) * P.noise_vec[i];
+        }
+      }
+    }
+  }
+  for (int i = 0; i < NO; ++i) ob[i] = fminf(fmaxf(ob[i], -P.clip_obs), P.clip_obs);
+}
+__device__ __forceinline__ void priv_row(const lrl_env_params& P, const KState& S, int e, float payload, V3 cb,
+                                         const float* ms, float* pr) {
+  pr[0] = (S.friction[e] - P.priv_shift[0]) * P.priv_scale[0];
+  pr[1] = (S.restitution[e] - P.priv_shift[1]) * P.priv_scale[1];
+  pr[2] = (payload - P.priv_shift[2]) * P.priv_scale[2];
+  pr[3] = (cb.x - P.priv_shift[3]) * P.priv_scale[3];
+  pr[4] = (cb.y - P.priv_shift[3]) * P.priv_scale[3];
+  pr[5] = (cb.z - P.priv_shift[3]) * P.priv_scale[3];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) pr[6 + j] = (ms[j] - P.priv_shift[4]) * P.priv_scale[4];
+#pragma unroll
+  for (int i = 0; i < LRL_NUM_PRIV; ++i) pr[i] = fminf(fmaxf(pr[i], -P.clip_obs), P.clip_obs);
+}
+
 __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
                                                         const float* __restrict__ actions_in, uint32_t flags,
                                                         int64_t step_counter) {
@@ -926,6 +978,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
     }
   }
   if (P.use_terminal_body_height && st.pos[2] < P.terminal_body_height) rst = 1;
+  // time-outs (legged_robot.py:196-198, commented out in the fork — Q2): upstream semantics only
+  const int tout = (P.auto_reset && eplen > P.max_episode_length) ? 1 : 0;
+  rst |= tout;
 
   // rewards
   float cmd[4];
@@ -1040,7 +1095,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   const int KS = P.num_sum_keys;
   S.episode_sums[KS * N + e] += rew;
   if (P.termination_scale != 0.f) {
-    float r = (rst ? 1.f : 0.f) * P.termination_scale;
+    float r = ((rst && !tout) ? 1.f : 0.f) * P.termination_scale;  // _reward_termination: reset & ~time_out
     rew += r;
     S.episode_sums[P.termination_slot * N + e] += r;
     S.command_sums[P.termination_slot * N + e] += r;
@@ -1051,52 +1106,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   S.command_sums[(KS + 3) * N + e] += sq(bav.z - cmd[2]);
   S.command_sums[(KS + 4) * N + e] += 1.f;
 
-  // observations -> LDS tile [env slot][NO]
-  {
-    float* ob = otile + es * NO;
-    int o = 0;
-    if (P.observe_vel) {
-      ob[o++] = blv.x * P.obs_scale_lin_vel; ob[o++] = blv.y * P.obs_scale_lin_vel; ob[o++] = blv.z * P.obs_scale_lin_vel;
-      ob[o++] = bav.x * P.obs_scale_ang_vel; ob[o++] = bav.y * P.obs_scale_ang_vel; ob[o++] = bav.z * P.obs_scale_ang_vel;
-    }
-    ob[o++] = pg.x; ob[o++] = pg.y; ob[o++] = pg.z;
-    if (P.observe_command) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) ob[o++] = cmd[k] * P.commands_scale[k];
-    }
-#pragma unroll
-    for (int j = 0; j < 12; ++j) ob[o + j] = (st.q[j] - P.default_dof_pos[j]) * P.obs_scale_dof_pos;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) ob[o + 12 + j] = st.qd[j] * P.obs_scale_dof_vel;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) ob[o + 24 + j] = act[j];
-    if (P.add_noise) {
-      for (int i0 = 0; i0 < NO; i0 += 4) {
-        lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter,
-                                 (LRL_RNG_OBS_NOISE << 16) ^ (uint32_t)(step_counter >> 32), (uint32_t)(i0 >> 2), S.seed);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          int i = i0 + k;
-          if (i < NO) {
-            float u = inject ? S.inj_noise[(size_t)e * NO + i] : lrl_u01(r.v[k]);
-            ob[i] += (2.f * u - 1.f) * P.noise_vec[i];
-          }
-        }
-      }
-    }
-    for (int i = 0; i < NO; ++i) ob[i] = fminf(fmaxf(ob[i], -P.clip_obs), P.clip_obs);
-    float* pr = ptile + es * LRL_NUM_PRIV;
-    pr[0] = (S.friction[e] - P.priv_shift[0]) * P.priv_scale[0];
-    pr[1] = (S.restitution[e] - P.priv_shift[1]) * P.priv_scale[1];
-    pr[2] = (payload - P.priv_shift[2]) * P.priv_scale[2];
-    pr[3] = (cb.x - P.priv_shift[3]) * P.priv_scale[3];
-    pr[4] = (cb.y - P.priv_shift[3]) * P.priv_scale[3];
-    pr[5] = (cb.z - P.priv_shift[3]) * P.priv_scale[3];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) pr[6 + j] = (ms_e[j] - P.priv_shift[4]) * P.priv_scale[4];
-#pragma unroll
-    for (int i = 0; i < LRL_NUM_PRIV; ++i) pr[i] = fminf(fmaxf(pr[i], -P.clip_obs), P.clip_obs);
-  }
+  // observations / privileged observations -> LDS tiles [env slot][.]
+  obs_row(P, S, e, genv, step_counter, inject, blv, bav, pg, cmd, st.q, st.qd, act, otile + es * NO);
+  priv_row(P, S, e, payload, cb, ms_e, ptile + es * LRL_NUM_PRIV);
 
   // ---- write back the SoA state ----
 #pragma unroll
@@ -1132,6 +1144,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
   S.episode_length[e] = eplen;
   S.reset[e] = (uint8_t)rst;
+  S.time_out[e] = (uint8_t)tout;
   S.rew[e] = rew;
   }  // ql == 0
 
@@ -1203,10 +1216,76 @@ extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
   return hipFuncSetAttribute((const void*)lrl::env_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
 }
 
+namespace lrl {
+// compute_observations for envs just reset inside a step (upstream semantics, legged_robot.py:177-184):
+// obs / priv rows from the post-reset state with the step's noise draws, the newest history slot, and the
+// last_* buffers post_physics_step sets after the reset (last_actions = actions, last_dof_vel = dof_vel,
+// last_root_vel = root velocity).  One thread per listed env.
+__global__ void observe_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
+                               uint32_t flags, int64_t step_counter) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int e = ids[t];
+  if (e < 0 || e >= S.n) return;
+  const lrl_env_params& P = K->p;
+  const int N = S.stride, NO = P.num_obs;
+  const uint64_t genv = (uint64_t)(S.env_offset + e);
+  float quat[4], V[3], W[3], q[12], qd[12], act[12], cmd[4], ms[12];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) quat[k] = S.root[(3 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    V[k] = S.root[(7 + k) * N + e];
+    W[k] = S.root[(10 + k) * N + e];
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    q[j] = S.dof_pos[j * N + e];
+    qd[j] = S.dof_vel[j * N + e];
+    act[j] = S.actions[j * N + e];
+    ms[j] = S.motor_strength[j * N + e];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cmd[k] = S.commands[k * N + e];
+  const V3 blv = quat_rotate_inverse(quat, v3(V[0], V[1], V[2]));
+  const V3 bav = quat_rotate_inverse(quat, v3(W[0], W[1], W[2]));
+  const V3 pg = quat_rotate_inverse(quat, v3(0.f, 0.f, -1.f));
+  S.base_lin_vel[e] = blv.x; S.base_lin_vel[N + e] = blv.y; S.base_lin_vel[2 * N + e] = blv.z;
+  S.base_ang_vel[e] = bav.x; S.base_ang_vel[N + e] = bav.y; S.base_ang_vel[2 * N + e] = bav.z;
+  S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
+  float* ob = S.obs + (size_t)e * NO;
+  obs_row(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, blv, bav, pg, cmd, q, qd, act, ob);
+  priv_row(P, S, e, S.payload[e], v3(S.com[e], S.com[N + e], S.com[2 * N + e]), ms, S.priv + (size_t)e * LRL_NUM_PRIV);
+  if (flags & LRL_STEP_HISTORY) {
+    const int H = K->num_history * NO;
+    float* h = S.hist + (size_t)e * H + (H - NO);
+    for (int i = 0; i < NO; ++i) h[i] = ob[i];
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    S.last_actions[j * N + e] = act[j];
+    S.last_dof_vel[j * N + e] = qd[j];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    S.last_root_vel[k * N + e] = V[k];
+    S.last_root_vel[(3 + k) * N + e] = W[k];
+  }
+}
+}  // namespace lrl
+
 extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int lds_bytes, const float* actions,
                                           uint32_t flags, int64_t step_counter, hipStream_t stream) {
   int blocks = S->stride / ENVS;
   hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
+                     step_counter);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lrl_launch_observe(const KParams* K, const KState* S, const int32_t* ids, int32_t n,
+                                         uint32_t flags, int64_t step_counter, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lrl::observe_kernel, dim3((n + 127) / 128), dim3(128), 0, stream, K, *S, ids, n, flags,
                      step_counter);
   return hipGetLastError();
 }

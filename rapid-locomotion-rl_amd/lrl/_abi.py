@@ -140,7 +140,7 @@ def lib():
                      "lrl_sim_set_root_state_indexed", "lrl_sim_set_dof_state_indexed", "lrl_sim_inject_uniforms",
                      "lrl_sim_refresh_rigid_body_state", "lrl_sim_shift_history", "lrl_sim_randomize", "lrl_gae",
                      "lrl_ppo_act", "lrl_abi_version", "lrl_device_count", "lrl_gae_partial", "lrl_adv_normalize",
-                     "lrl_sim_reset_idx_ex", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
+                     "lrl_sim_reset_idx_ex", "lrl_sim_observe_idx", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
                      "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student"]:
             getattr(L, name).restype = C.c_int32

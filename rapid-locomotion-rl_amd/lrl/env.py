@@ -59,7 +59,7 @@ class _LazyExtras(dict):
 class LeggedRobotEnv:
     def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
                  eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=0,
-                 solver_iterations=None):
+                 solver_iterations=None, legacy_fork=True):
         if cfg is None:
             from .config import Cfg as cfg
         if num_envs is not None:
@@ -76,6 +76,9 @@ class LeggedRobotEnv:
         if eval_cfg is not None:
             raise NotImplementedError("train/eval env split is a next-row item (SURVEY.md §8(f) rank 2)")
         self.cfg, self.eval_cfg = cfg, eval_cfg
+        # legacy_fork=False re-enables what the fork comments out: reset_idx inside step
+        # for terminated / timed-out envs, command resampling every resampling_time and at resets
+        self.legacy_fork = bool(legacy_fork)
         self.device = torch.device(sim_device)
         if self.device.type != "cuda" or not torch.cuda.is_available():
             raise RuntimeError("LeggedRobotEnv runs on the GPU through liblrl.so; no CPU path exists")
@@ -97,7 +100,8 @@ class LeggedRobotEnv:
         self.custom_origins = cfg.terrain.mesh_type in ("heightfield", "trimesh")
         if self.custom_origins:
             self._flat_terrain()
-        self._P = lparams.build_params(cfg, self.robot, solver_iterations=solver_iterations)
+        self._P = lparams.build_params(cfg, self.robot, auto_reset=not self.legacy_fork,
+                                       solver_iterations=solver_iterations)
         self._M = lparams.build_model(self.robot)
         self.sim_params = Section(dt=lparams.sim_dt(cfg))
         self.dt = cfg.control.decimation * self.sim_params.dt
@@ -306,6 +310,12 @@ class LeggedRobotEnv:
         if actions.shape != (self.num_envs, self.num_actions):
             raise ValueError(f"actions must be [{self.num_envs}, {self.num_actions}], got {tuple(actions.shape)}")
         flags = _abi.STEP_PHYSICS | (_abi.STEP_HISTORY if _history else 0)
+        if not self.legacy_fork:  # _post_physics_step_callback resampling (legged_robot.py:578-581): the
+            # envs whose episode length reaches a multiple of resampling_time in this step, before its rewards
+            interval = int(self.cfg.commands.resampling_time / self.dt)
+            due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
+            if len(due):
+                self.resample_commands(due)
         timer = self.kernel_timer
         if timer is not None:  # HIP events on the launch stream around the fused kernel (bench.py)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -315,6 +325,13 @@ class LeggedRobotEnv:
             ev1.record()
             timer.append((ev0, ev1))
         self.common_step_counter += 1
+        if not self.legacy_fork:  # reset_idx of the terminated / timed-out envs, then their observations
+            ids = self._reset_u8.nonzero(as_tuple=False).flatten()
+            if len(ids):
+                self.reset_idx(ids)
+                ids32 = ids.to(torch.int32).contiguous()
+                _abi.check(self._L.lrl_sim_observe_idx(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
+                                                       C.c_uint32(flags), self._stream()))
         ex = self.extras
         ex["privileged_obs"] = self.privileged_obs_buf
         ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())
@@ -356,6 +373,8 @@ class LeggedRobotEnv:
         if len(env_ids) == 0:
             return
         self.update_command_curriculum(env_ids, self.cfg)
+        if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
+            self.resample_commands(env_ids)
         ids32 = env_ids.to(torch.int32).contiguous()
         xo = yo = 0.0
         if self.custom_origins:  # torch_rand_float(x_init_range, y_init_range) == constant (Q8)

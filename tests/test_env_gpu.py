@@ -211,3 +211,50 @@ def test_history_and_reset_semantics():
     d2 = env.get_observations()  # shifts the history (Q6)
     assert torch.equal(d2["obs_history"][:, :-42], before[:, 42:])
     env.env.close()
+
+
+def test_upstream_resets_timeouts_and_command_resampling():
+    """legacy_fork=False (SURVEY.md §8(f) rank 2, Q2/Q3 re-enabled): time-outs (legged_robot.py:196-198) and
+    terminations reset envs inside step (:177 reset_idx -> _reset_dofs / _reset_root_states / buffer
+    zeroing, :227-290); the reset envs observe their post-reset state (compute_observations after reset_idx,
+    :179) incl. the newest history slot; episode logging and time_outs reach extras; commands are resampled
+    from the curriculum every resampling_time (:578-581) and at resets (_resample_commands :595-626)."""
+    from lrl.env import LeggedRobotEnv
+    from lrl.history import HistoryWrapper
+    n = 64
+    cfg = _cfg("mc", n, **{"env.episode_length_s": 0.1, "commands.resampling_time": 0.06, "noise.add_noise": False})
+    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, legacy_fork=False))
+    inner = env.env
+    M = int(inner.max_episode_length)
+    interval = int(cfg.commands.resampling_time / inner.dt)
+    assert M == 6 and interval == 3
+    env.reset()
+    q0 = inner.default_dof_pos.expand(n, 12)
+    zero = torch.zeros(n, 12, device="cuda:0")
+    seen_timeout = seen_resample = False
+    for step in range(16):
+        elen = inner.episode_length_buf.clone().long()
+        cmd0 = inner.commands.clone()
+        obs_dict, rew, done, info = env.step(zero)
+        torch.cuda.synchronize()
+        tout = inner.time_out_buf
+        assert torch.equal(tout, elen + 1 > M)  # time-out exactly when the episode passes max_episode_length
+        assert bool(done[tout].all())
+        reset = done
+        assert torch.equal(inner.episode_length_buf[reset].long(), torch.zeros_like(elen[reset]))
+        assert torch.equal(inner.episode_length_buf[~reset].long(), elen[~reset] + 1)
+        if reset.any():
+            assert torch.equal(inner.dof_pos[reset], q0[reset])
+            assert inner.dof_vel[reset].abs().max().item() == 0.0
+            o = obs_dict["obs"][reset]
+            assert o[:, 6:30].abs().max().item() == 0.0  # (q - q0) and qd terms of the post-reset state
+            assert "train/episode" in info and "time_outs" in info
+            seen_timeout |= bool(tout.any())
+        # the newest history slot is the step's (post-reset) observation for every env
+        assert torch.equal(obs_dict["obs_history"][:, -42:], obs_dict["obs"])
+        changed = (inner.commands != cmd0).any(dim=1)
+        due = (elen + 1) % interval == 0
+        assert not bool((changed & ~(due | reset)).any())  # commands move only when due or reset
+        seen_resample |= bool((changed & due & ~reset).any())
+    assert seen_timeout and seen_resample
+    inner.close()
