@@ -566,6 +566,121 @@ static int launch_thin(const GemmP& p, int groups, hipStream_t st) {
   return LRL_E_INVALID;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// LDS-DMA weight-gradient product (TN, split-k partials): dW[o][i] = sum_b dY[b][o] X[rows(b)][i] over a
+// split's rows b.  Both operands are b-major in memory, so a 16-row slice of each is a [16 k][128] image
+// that global_load_lds_dwordx4 fills row by row (DMA d of a slice covers k-rows 2d, 2d + 1); a 3-deep ring
+// of slices with counted vmcnt waits keeps two slices in flight under the MFMAs.  128x128 tile, 4 waves
+// each 64x64 (2x2 MFMA tiles); MFMA operands are ds_read_b32 of [k][m] / [k][n] (consecutive m / n per
+// lane).  The split's gathered row list is converted to int32 in LDS once.  Bias-gradient partial: column
+// sums of the dY slice (n-tile 0 workgroups).
+template <int NST>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
+  constexpr int BM = 128, BN = 128, BKD = 16, IMG = BKD * 128;
+  extern __shared__ __attribute__((aligned(16))) float S[];  // [NST][A | B][16][128], then int32 rows
+  const int mt = p.M / BM, nt = (p.N + BN - 1) / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, zz = L / (nt * mt);
+  const int g = zz / p.splits, sp = zz - g * p.splits;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int kbeg = sp * p.kps, kend = min(p.K, kbeg + p.kps);
+  const int ns = (kend - kbeg) / BKD;
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ B = p.B + g * p.gb;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  int* rows = reinterpret_cast<int*>(S + NST * 2 * IMG);
+  if (p.b_rows) {
+    for (int i = threadIdx.x; i < kend - kbeg; i += GTHREADS) rows[i] = (int)p.b_rows[kbeg + i];
+    __syncthreads();
+  }
+  const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
+  auto dma = [&](const float* src, uint32_t lds_off) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_off)
+                 : "memory");
+  };
+  // DMA d = 4 i + w (i = 0, 1) of a slice: k-rows 2d + h of both images, 16-B chunk li
+  auto issue = [&](int st, int s) {
+    const int kl = s * BKD;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int d = 4 * i + w, kr = kl + 2 * d + h;
+      const uint32_t base = __builtin_amdgcn_readfirstlane(s_lds + (uint32_t)((st * 2 * IMG + d * 256) * 4));
+      dma(A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * li, base);
+      const int64_t brow = p.b_rows ? (int64_t)rows[kr] : (int64_t)(kbeg + kr);
+      dma(B + brow * p.ldb + n0 + 4 * li, base + IMG * 4);
+    }
+  };
+  const bool do_bsum = p.bias_part != nullptr && tn_ == 0;
+  float bsum = 0.f;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+  static_assert(NST == 3, "the counted waits below assume a 3-deep ring");
+  if (ns > 0) issue(0, 0);
+  if (ns > 1) issue(1, 1);
+  for (int s = 0; s < ns; ++s) {
+    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < ns) issue((s + 2) % NST, s + 2);
+    const float* As = S + (s % NST) * 2 * IMG;
+    const float* Bs = As + IMG;
+    if (do_bsum && threadIdx.x < BM) {
+#pragma unroll
+      for (int k = 0; k < BKD; ++k) bsum += As[k * 128 + threadIdx.x];
+    }
+    float av[8][2], bv[8][2];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        av[t][a] = As[(2 * t + h) * 128 + wm + 32 * a + li];
+        bv[t][a] = Bs[(2 * t + h) * 128 + wn + 32 * a + li];
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t][a], bv[t][c], acc[a][c], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float* __restrict__ C = p.C + g * p.gc + (int64_t)sp * p.part_stride;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = n0 + wn + 32 * c + li;
+    if (col >= p.N) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        C[(int64_t)row * p.ldc + col] = acc[a][c][r];
+      }
+  }
+  if (do_bsum && threadIdx.x < BM)
+    p.bias_part[((int64_t)sp * p.groups + g) * p.M + m0 + threadIdx.x] = bsum;
+}
+
 template <int BM, int BN>
 static int launch_bm(const GemmP& p, int layout, int epi, dim3 grid, hipStream_t st) {
 #define LRL_GEMM_LAUNCH(L, E) hipLaunchKernelGGL((gemm_kernel<BM, BN, L, E>), grid, dim3(GTHREADS), 0, st, p)
@@ -659,6 +774,26 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
       else LRL_GLDS(GEMM_NN, EPI_DELU);
     }
 #undef LRL_GLDS
+    return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  }
+  // LDS-DMA weight gradient: 128-row m tiles, 128-wide n tiles whose reads stay inside the row pitch,
+  // whole 16-row slices in every split, float4-aligned operands
+#ifndef LRL_GLDS_TN
+#define LRL_GLDS_TN 1
+#endif
+  if (LRL_GLDS_TN && layout == GEMM_TN && epi == EPI_PARTIAL && p.M % 128 == 0 &&
+      (int64_t)((p.N + 127) / 128) * 128 <= p.ldb && p.K % 16 == 0 && p.kps % 16 == 0 && p.avec == 4 &&
+      p.bvec == 4 && p.kps <= 8192) {
+    const size_t lds = (size_t)3 * 2 * 16 * 128 * sizeof(float) + (p.b_rows ? (size_t)p.kps * sizeof(int) : 0);
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_glds_tn_kernel<3>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return LRL_E_HIP;
+      attr = true;
+    }
+    dim3 gt((p.M / 128) * ((p.N + 127) / 128) * groups * p.splits);
+    hipLaunchKernelGGL((gemm_glds_tn_kernel<3>), gt, dim3(GTHREADS), lds, st, p);
     return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
   }
   // thin output (N <= 32): B staged whole in LDS, k split over the workgroup's waves

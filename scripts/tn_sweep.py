@@ -9,9 +9,10 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 B = 24576
 dev = "cuda:0"
-SHAPES = [("dW2 256x1024", 256, 1024, False), ("dW3 256x256", 256, 256, False), ("dW1 1024x60", 1024, 60, False),
-          ("dWD1 256x630 g", 256, 630, True), ("dWe2 128x256", 128, 256, False), ("dWe1 256x18 g", 256, 18, True),
-          ("dWe3 18x128", 18, 128, False), ("dWD2 32x256", 32, 256, False), ("dWD3 18x32", 18, 32, False)]
+SHAPES = [("dW2 256x1024", 256, 1024, False, 0), ("dW3 256x256", 256, 256, False, 0),
+          ("dW1 1024x60", 1024, 60, False, 64), ("dWD1 256x630 g", 256, 630, True, 640),
+          ("dWe2 128x256", 128, 256, False, 0), ("dWe1 256x18 g", 256, 18, True, 0), ("dWe3 18x128", 18, 128, False, 0),
+          ("dWD2 32x256", 32, 256, False, 0), ("dWD3 18x32", 18, 32, False, 0)]
 SPLITS = [0, 8, 16, 32, 64, 128, 256]
 
 
@@ -21,10 +22,11 @@ def main():
     p = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     torch.randn(8192, 8192, device=dev) @ torch.randn(8192, 8192, device=dev)  # clocks
-    for name, M, N, gather in SHAPES:
+    for name, M, N, gather, ldb in SHAPES:
         K = B
+        ldb = ldb or N
         A = torch.randn(K, M, device=dev)
-        Bm = torch.randn(K + 100 if gather else K, N, device=dev)
+        Bm = torch.randn(K + 100 if gather else K, ldb, device=dev)
         rows = torch.randperm(K + 100, device=dev)[:K].contiguous() if gather else None
         Cm = torch.empty(M, N, device=dev)
         db = torch.empty(M, device=dev)
@@ -34,7 +36,7 @@ def main():
             os.environ["LRL_GEMM_SPLITS"] = str(s)
 
             def call():
-                rc = L.lrl_gemm_f32(3, 4, M, N, K, p(A), C.c_int64(M), p(Bm), C.c_int64(N), p(Cm), C.c_int64(N),
+                rc = L.lrl_gemm_f32(3, 4, M, N, K, p(A), C.c_int64(M), p(Bm), C.c_int64(ldb), p(Cm), C.c_int64(N),
                                     p(db), None, C.c_int64(0), p(rows), p(ws), C.c_int64(ws.numel()), st)
                 assert rc == 0, rc
             for _ in range(3):

@@ -74,21 +74,26 @@ def test_backward_data_nn(M, N, K, delu):
     assert (out - ref).abs().max().item() <= _tol(ref, K)
 
 
-@pytest.mark.parametrize("M,N,K,gather", [(256, 512, 24576, False), (128, 256, 6000, False), (18, 128, 4097, False),
-                                          (256, 630, 24576, True), (1024, 60, 3000, False), (12, 128, 96, False)])
-def test_weight_grad_tn(M, N, K, gather):
-    """dW[o][i] = sum_b dY[b][o] X[b][i] (split over b, partials reduced), db[o] = sum_b dY[b][o]."""
+@pytest.mark.parametrize("M,N,K,gather,ldx", [(256, 512, 24576, False, 0), (128, 256, 6000, False, 0),
+                                              (18, 128, 4097, False, 0), (256, 630, 24576, True, 0),
+                                              (256, 630, 24576, True, 640), (1024, 60, 3000, False, 0),
+                                              (12, 128, 96, False, 0), (384, 128, 1024, True, 0)])
+def test_weight_grad_tn(M, N, K, gather, ldx):
+    """dW[o][i] = sum_b dY[b][o] X[b][i] (split over b, partials reduced), db[o] = sum_b dY[b][o].  128-row
+    m tiles with 128-wide n tiles inside X's row pitch take the LDS-DMA kernel (ldx = 640: the padded
+    history pitch), the others the register-staged one."""
     g = torch.Generator(device=dev).manual_seed(M * N + K)
     dY = torch.randn(K, M, device=dev, generator=g)
     src = K + 11
-    X = torch.randn(src, N, device=dev, generator=g)
+    ldx = ldx or N
+    X = torch.randn(src, ldx, device=dev, generator=g)
     rows = torch.randperm(src, device=dev)[:K].contiguous() if gather else None
-    Xk = X[rows] if gather else X[:K]
+    Xk = (X[rows] if gather else X[:K])[:, :N]
     ref = dY.T.double() @ Xk.double()
     out = torch.empty(M, N, device=dev)
     db = torch.empty(M, device=dev)
     ws = torch.empty(64 * (M * N + M) * 2, device=dev)
-    _gemm(3, 4, M, N, K, dY, M, X, N, out, N, bias=db, rows=rows, ws=ws)
+    _gemm(3, 4, M, N, K, dY, M, X, ldx, out, N, bias=db, rows=rows, ws=ws)
     err = (out.double() - ref).abs().max().item()
     assert err <= 4e-6 * np.sqrt(K) * (ref.abs().max().item() + 1.0), err
     assert (db.double() - dY.double().sum(0)).abs().max().item() <= 1e-5 * np.sqrt(K) * 10
