@@ -178,9 +178,9 @@ def main():
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (the fused history "
                                  f"shift adds 4872 B/env-step = {4872 * ENVS_PER_GPU} B per launch); the kernel is "
-                                 "latency/VALU-bound (one env per lane), see DESIGN.md"},
+                                 "latency-bound (4 lanes per env, one single-wave workgroup per 16 envs), see DESIGN.md"},
             "roofline_update_gemm": {
-                "bound": "mfma", "kernel": "lrl::gemm_kernel<128,128,TN,partial> (dW2: 2 x 256x512, "
+                "bound": "mfma", "kernel": "lrl::gemm_glds_tn_kernel<3> (dW2: 2 x 256x512, "
                 f"{mb_rows} rows)", "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": MFMA_F32_PEAK_TF,
                 "unit": "TFLOP/s", "frac": round(gemm_tf / MFMA_F32_PEAK_TF, 4) if gemm_tf else None,
                 "traffic": round(gemm_traffic) if gemm_traffic else None, "launch_ms": round(gemm_ms, 4),
