@@ -446,7 +446,7 @@ __device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
   return l;
 }
 
-__device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau, float mb, const float* Ib, V3 cb,
+__device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau3, float mb, const float* Ib, V3 cb,
                         float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
                         unsigned long long* prof) {
   LRL_PROF_DECL
@@ -601,8 +601,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     float pb[6];
     {
       const int l = ql;
-      const V3 rl = v3(pick12(tau, 3 * l) - M.leg(l, 42), pick12(tau, 3 * l + 1) - M.leg(l, 43),
-                       pick12(tau, 3 * l + 2) - M.leg(l, 44));
+      const V3 rl = v3(tau3[0] - M.leg(l, 42), tau3[1] - M.leg(l, 43), tau3[2] - M.leg(l, 44));
 #pragma unroll
       for (int r = 0; r < 6; ++r) pb[r] = -(M.Kx(l, 0, r) * rl.x + M.Kx(l, 1, r) * rl.y + M.Kx(l, 2, r) * rl.z);
       const V3 y = di_mul(M, l, rl);
@@ -745,19 +744,6 @@ __device__ __forceinline__ float pos_target(const lrl_env_params& P, const float
   if (j % 3 == 0) as = as * P.hip_scale_reduction;  // hip columns 0,3,6,9 (legged_robot.py:666)
   return as + P.default_dof_pos[j];
 }
-// kpf/kdf/ms point at this env's column of the SoA [12][N] factor arrays
-__device__ __forceinline__ void compute_torques(const lrl_env_params& P, const float* act, const float* q,
-                                                const float* qd, const float* kpf, const float* kdf, const float* ms,
-                                                int N, float* tau) {
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    float t0 = pos_target(P, act, j);
-    float t = P.p_gains[j] * kpf[j * N] * (t0 - q[j]) - P.d_gains[j] * kdf[j * N] * qd[j];
-    t = t * ms[j * N];
-    float lim = P.torque_limits[j];
-    tau[j] = fminf(fmaxf(t, -lim), lim);
-  }
-}
 __device__ __forceinline__ V3 quat_rotate_inverse(const float* q, V3 v) {
   float w = q[3];
   float s = 2.0f * (w * w) - 1.0f;
@@ -829,6 +815,9 @@ __device__ __forceinline__ void priv_row(const lrl_env_params& P, const KState& 
 __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
                                                         const float* __restrict__ actions_in, uint32_t flags,
                                                         int64_t step_counter) {
+#ifdef LRL_ENV_PROFILE
+  const unsigned long long kt0 = clock64();
+#endif
   extern __shared__ float lds[];
   const lrl_env_params& P = K->p;
   const int lane = threadIdx.x;
@@ -878,13 +867,42 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
   for (int s = 0; s < K->num_spheres; ++s)
     if (sph_owner(K, s) == ql) own |= 1ull << s;
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   LRL_PROF_DECL
-  LRL_PROF(5)  // state loads
-  for (int sub = 0; sub < P.decimation; ++sub) {
-    compute_torques(P, act, st.q, st.qd, S.kp + e, S.kd + e, S.motor_strength + e, N, tau);
-    if (physics) substep(K, st, tau, mb, Ib, cb, mu, rest, M, active, ql, own, prof);
+#ifdef LRL_ENV_PROFILE
+  prof_t = kt0;
+#endif
+  LRL_PROF(5)  // kernel start: state loads, setup
+  // _compute_torques (legged_robot.py:653-688) for this lane's leg: the gain / strength factors and the
+  // position targets do not change over the sub-steps, so they are read once
+  float kp3[3], kd3[3], ms3[3], tg3[3], lim3[3], tau3[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int jj = 3 * ql + j;
+    kp3[j] = P.p_gains[jj] * S.kp[jj * N + e];
+    kd3[j] = P.d_gains[jj] * S.kd[jj * N + e];
+    ms3[j] = S.motor_strength[jj * N + e];
+    tg3[j] = pos_target(P, act, jj);
+    lim3[j] = P.torque_limits[jj];
   }
+  for (int sub = 0; sub < P.decimation; ++sub) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float t = kp3[j] * (tg3[j] - pick12(st.q, 3 * ql + j)) - kd3[j] * pick12(st.qd, 3 * ql + j);
+      t = t * ms3[j];
+      tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
+    }
+    LRL_PROF(8)  // PD torques
+    if (physics) substep(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, prof);
+#ifdef LRL_ENV_PROFILE
+    prof_t = clock64();
+#endif
+  }
+  // the last sub-step's torques of all 12 joints (rewards, torques buffer): from the quad's 4 lanes
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) tau[3 * l + j] = __shfl(tau3[j], (lane & ~3) | l, WAVE);
 #ifdef LRL_ENV_PROFILE
   prof_t = clock64();
 #endif
@@ -1190,8 +1208,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   }
   LRL_PROF(7)  // obs / priv tiles + history shift
 #ifdef LRL_ENV_PROFILE
+  prof[9] = clock64() - kt0;  // the wave's whole lifetime (the phases above should sum to it)
   if (lane == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&g_env_prof[i], prof[i]);
+    for (int i = 0; i < 10; ++i) atomicAdd(&g_env_prof[i], prof[i]);
 #endif
 }
 
@@ -1199,12 +1218,12 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 
 extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
 #ifdef LRL_ENV_PROFILE
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 10) != hipSuccess) return -2;
   if (reset) {
     unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
   }
-  return 8;
+  return 10;
 #else
   (void)out;
   (void)reset;

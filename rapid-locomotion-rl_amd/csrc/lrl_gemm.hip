@@ -574,10 +574,13 @@ static int launch_thin(const GemmP& p, int groups, hipStream_t st) {
 // each 64x64 (2x2 MFMA tiles); MFMA operands are ds_read_b32 of [k][m] / [k][n] (consecutive m / n per
 // lane).  The split's gathered row list is converted to int32 in LDS once.  Bias-gradient partial: column
 // sums of the dY slice (n-tile 0 workgroups).
-template <int NST>
+template <int NST, int BN>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
-  constexpr int BM = 128, BN = 128, BKD = 16, IMG = BKD * 128;
-  extern __shared__ __attribute__((aligned(16))) float S[];  // [NST][A | B][16][128], then int32 rows
+  // BN = 128: 4 waves of 64x64 (2x2 MFMA tiles); BN = 64 (narrow inputs, e.g. the 60-wide actor/critic input):
+  // 4 waves of 64x32
+  constexpr int BM = 128, BKD = 16, IMGA = BKD * BM, IMGB = BKD * BN, TN = BN / 64;
+  constexpr int NB_DMA = IMGB / 256;  // 1 KiB DMAs per B slice (4 or 8): per wave NB_DMA / 4
+  extern __shared__ __attribute__((aligned(16))) float S[];  // [NST][A 16x128 | B 16xBN], then int32 rows
   const int mt = p.M / BM, nt = (p.N + BN - 1) / BN;
   int L;
   {
@@ -594,8 +597,9 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 31, h = lane >> 5;
-  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
-  int* rows = reinterpret_cast<int*>(S + NST * 2 * IMG);
+  const int wm = (w >> 1) * 64, wn = (w & 1) * (BN / 2);
+  constexpr int STG = IMGA + IMGB;
+  int* rows = reinterpret_cast<int*>(S + NST * STG);
   if (p.b_rows) {
     for (int i = threadIdx.x; i < kend - kbeg; i += GTHREADS) rows[i] = (int)p.b_rows[kbeg + i];
     __syncthreads();
@@ -608,49 +612,60 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
                  : "v"(src), "s"(lds_off)
                  : "memory");
   };
-  // DMA d = 4 i + w (i = 0, 1) of a slice: k-rows 2d + h of both images, 16-B chunk li
+  // A: DMA d = 4 i + w (i = 0, 1) fills k-rows 2d + h (128 floats each), 16-B chunk li;
+  // B: DMA d = 4 i + w (i < NB_DMA / 4) fills k-rows d * (256 / BN) + lane / (BN / 4), chunk lane % (BN / 4)
   auto issue = [&](int st, int s) {
     const int kl = s * BKD;
+    const uint32_t sbase = s_lds + (uint32_t)(st * STG * 4);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int d = 4 * i + w, kr = kl + 2 * d + h;
-      const uint32_t base = __builtin_amdgcn_readfirstlane(s_lds + (uint32_t)((st * 2 * IMG + d * 256) * 4));
-      dma(A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * li, base);
+      dma(A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * li, __builtin_amdgcn_readfirstlane(sbase + d * 1024));
+    }
+#pragma unroll
+    for (int i = 0; i < NB_DMA / 4; ++i) {
+      constexpr int CPR = BN / 4;
+      const int d = 4 * i + w, kr = kl + d * (64 / CPR) + lane / CPR;
       const int64_t brow = p.b_rows ? (int64_t)rows[kr] : (int64_t)(kbeg + kr);
-      dma(B + brow * p.ldb + n0 + 4 * li, base + IMG * 4);
+      dma(B + brow * p.ldb + n0 + 4 * (lane % CPR), __builtin_amdgcn_readfirstlane(sbase + IMGA * 4 + d * 1024));
     }
   };
   const bool do_bsum = p.bias_part != nullptr && tn_ == 0;
   float bsum = 0.f;
-  f32x16 acc[2][2];
+  f32x16 acc[2][TN];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < TN; ++c)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
   static_assert(NST == 3, "the counted waits below assume a 3-deep ring");
   if (ns > 0) issue(0, 0);
   if (ns > 1) issue(1, 1);
   for (int s = 0; s < ns; ++s) {
-    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's DMAs of slice s have landed (slice s+1's 2 + NB_DMA/4 may stay in flight) ...
+    if (s + 1 < ns) {
+      if constexpr (NB_DMA == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     if (s + 2 < ns) issue((s + 2) % NST, s + 2);
-    const float* As = S + (s % NST) * 2 * IMG;
-    const float* Bs = As + IMG;
+    const float* As = S + (s % NST) * STG;
+    const float* Bs = As + IMGA;
     if (do_bsum && threadIdx.x < BM) {
 #pragma unroll
-      for (int k = 0; k < BKD; ++k) bsum += As[k * 128 + threadIdx.x];
+      for (int k = 0; k < BKD; ++k) bsum += As[k * BM + threadIdx.x];
     }
-    float av[8][2], bv[8][2];
+    float av[8][2], bv[8][TN];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < 8; ++t) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        av[t][a] = As[(2 * t + h) * 128 + wm + 32 * a + li];
-        bv[t][a] = Bs[(2 * t + h) * 128 + wn + 32 * a + li];
-      }
+      for (int a = 0; a < 2; ++a) av[t][a] = As[(2 * t + h) * BM + wm + 32 * a + li];
+#pragma unroll
+      for (int c = 0; c < TN; ++c) bv[t][c] = Bs[(2 * t + h) * BN + wn + 32 * c + li];
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -659,14 +674,14 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < TN; ++c)
           acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t][a], bv[t][c], acc[a][c], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   }
   float* __restrict__ C = p.C + g * p.gc + (int64_t)sp * p.part_stride;
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < TN; ++c) {
     const int col = n0 + wn + 32 * c + li;
     if (col >= p.N) continue;
 #pragma unroll
@@ -679,6 +694,21 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
   }
   if (do_bsum && threadIdx.x < BM)
     p.bias_part[((int64_t)sp * p.groups + g) * p.M + m0 + threadIdx.x] = bsum;
+}
+
+template <int BN>
+static int launch_glds_tn(const GemmP& p, int groups, hipStream_t st) {
+  const size_t lds = (size_t)3 * 16 * (128 + BN) * sizeof(float) + (p.b_rows ? (size_t)p.kps * sizeof(int) : 0);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_glds_tn_kernel<3, BN>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return LRL_E_HIP;
+    attr = true;
+  }
+  dim3 gt((p.M / 128) * ((p.N + BN - 1) / BN) * groups * p.splits);
+  hipLaunchKernelGGL((gemm_glds_tn_kernel<3, BN>), gt, dim3(GTHREADS), lds, st, p);
+  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
 }
 
 template <int BM, int BN>
@@ -781,20 +811,10 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
 #ifndef LRL_GLDS_TN
 #define LRL_GLDS_TN 1
 #endif
-  if (LRL_GLDS_TN && layout == GEMM_TN && epi == EPI_PARTIAL && p.M % 128 == 0 &&
-      (int64_t)((p.N + 127) / 128) * 128 <= p.ldb && p.K % 16 == 0 && p.kps % 16 == 0 && p.avec == 4 &&
-      p.bvec == 4 && p.kps <= 8192) {
-    const size_t lds = (size_t)3 * 2 * 16 * 128 * sizeof(float) + (p.b_rows ? (size_t)p.kps * sizeof(int) : 0);
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_glds_tn_kernel<3>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-        return LRL_E_HIP;
-      attr = true;
-    }
-    dim3 gt((p.M / 128) * ((p.N + 127) / 128) * groups * p.splits);
-    hipLaunchKernelGGL((gemm_glds_tn_kernel<3>), gt, dim3(GTHREADS), lds, st, p);
-    return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+  if (LRL_GLDS_TN && layout == GEMM_TN && epi == EPI_PARTIAL && p.M % 128 == 0 && p.K % 16 == 0 &&
+      p.kps % 16 == 0 && p.avec == 4 && p.bvec == 4 && p.kps <= 8192) {
+    if (p.N <= 64 && p.ldb >= 64) return launch_glds_tn<64>(p, groups, st);
+    if ((int64_t)((p.N + 127) / 128) * 128 <= p.ldb) return launch_glds_tn<128>(p, groups, st);
   }
   // thin output (N <= 32): B staged whole in LDS, k split over the workgroup's waves
   const int kb128 = p.K / 128;

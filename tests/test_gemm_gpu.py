@@ -77,11 +77,12 @@ def test_backward_data_nn(M, N, K, delu):
 @pytest.mark.parametrize("M,N,K,gather,ldx", [(256, 512, 24576, False, 0), (128, 256, 6000, False, 0),
                                               (18, 128, 4097, False, 0), (256, 630, 24576, True, 0),
                                               (256, 630, 24576, True, 640), (1024, 60, 3000, False, 0),
-                                              (12, 128, 96, False, 0), (384, 128, 1024, True, 0)])
+                                              (12, 128, 96, False, 0), (384, 128, 1024, True, 0),
+                                              (1024, 60, 3072, False, 64), (256, 40, 2048, True, 64)])
 def test_weight_grad_tn(M, N, K, gather, ldx):
     """dW[o][i] = sum_b dY[b][o] X[b][i] (split over b, partials reduced), db[o] = sum_b dY[b][o].  128-row
-    m tiles with 128-wide n tiles inside X's row pitch take the LDS-DMA kernel (ldx = 640: the padded
-    history pitch), the others the register-staged one."""
+    m tiles with 128- (or, for n <= 64, 64-) wide n tiles inside X's row pitch take the LDS-DMA kernel
+    (ldx = 640: the padded history pitch; 64: the padded actor/critic input), the others the register-staged one."""
     g = torch.Generator(device=dev).manual_seed(M * N + K)
     dY = torch.randn(K, M, device=dev, generator=g)
     src = K + 11
