@@ -1178,32 +1178,35 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   }
   if (flags & LRL_STEP_HISTORY) {
     const int H = K->num_history * NO;
-    float* hg = S.hist + row0 * H;
-    // in place: new[r][k] = old[r][k + NO] (k < H - NO) else obs[r][k - (H - NO)].  Reads run ahead of
-    // writes within a row, and each wave-iteration reads only addresses above the ones it writes.
-    // Chunks of HU wave-iterations: all HU loads of a chunk are issued before any of its stores (one
-    // latency per chunk instead of one per element); a chunk's reads lie above every earlier write.
-    constexpr int HU = 16;
-    const int total = ENVS * H;
-    int i0 = 0;
-    for (; i0 + HU * WAVE <= total; i0 += HU * WAVE) {
-      float v[HU];
+    // in place: new[r][k] = old[r][k + NO] (k < H - NO) else obs[r][k - (H - NO)].  The wave's 16 rows are
+    // contiguous; a pass covers one 64-wide column block of every row (one 8-B pair per lane and row, 16
+    // loads in flight), all its loads before any of its stores, and column blocks run left to right, so a
+    // pass only reads pairs no earlier pass has written.
+    if (((H | NO) & 1) == 0) {
+      const int H2 = H >> 1, S2 = (H - NO) >> 1, NO2 = NO >> 1;
+      float2* hg2 = reinterpret_cast<float2*>(S.hist + row0 * H);
+      const float2* ot2 = reinterpret_cast<const float2*>(otile);
+      for (int c0 = 0; c0 < H2; c0 += WAVE) {
+        const int k2 = c0 + lane;
+        float2 v[ENVS];
 #pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        const int i = i0 + u * WAVE + lane;
-        const int r = i / H, k = i - r * H;
-        v[u] = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
+        for (int r = 0; r < ENVS; ++r)
+          if (k2 < H2) v[r] = k2 < S2 ? hg2[r * H2 + k2 + NO2] : ot2[r * NO2 + (k2 - S2)];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < ENVS; ++r)
+          if (k2 < H2) hg2[r * H2 + k2] = v[r];
       }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int u = 0; u < HU; ++u) hg[i0 + u * WAVE + lane] = v[u];
-    }
-    for (; i0 < total; i0 += WAVE) {
-      const int i = i0 + lane;
-      const int r = i / H, k = i - r * H;
-      const float v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
-      __builtin_amdgcn_wave_barrier();
-      hg[i] = v;
+    } else {
+      float* hg = S.hist + row0 * H;
+      for (int i0 = 0; i0 < ENVS * H; i0 += WAVE) {
+        const int i = i0 + lane;
+        const int r = i / H, k = i - r * H;
+        float v = 0.f;
+        if (i < ENVS * H) v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
+        __builtin_amdgcn_wave_barrier();
+        if (i < ENVS * H) hg[i] = v;
+      }
     }
   }
   LRL_PROF(7)  // obs / priv tiles + history shift
