@@ -760,12 +760,12 @@ __device__ __forceinline__ float nrm3(float x, float y, float z) { return sqrtf(
 // ------------------------------------------------------------------------------------------------
 // the fused step kernel
 // ------------------------------------------------------------------------------------------------
-// compute_observations (legged_robot.py:342-417): obs row (noise: U[-1,1] x noise_vec from the counter RNG
-// keyed by (env, step counter), so a re-evaluation after a reset draws the same noise) and priv-obs row
-__device__ __forceinline__ void obs_row(const lrl_env_params& P, const KState& S, int e, uint64_t genv,
-                                        int64_t step_counter, bool inject, V3 blv, V3 bav, V3 pg, const float* cmd,
-                                        const float* q, const float* qd, const float* act, float* ob) {
-  const int NO = P.num_obs;
+// compute_observations (legged_robot.py:342-417) in two parts: obs_values writes the row's values;
+// obs_noise_clip adds U[-1,1] x noise_vec from the counter RNG keyed by (env, step counter, 4-entry chunk)
+// and clips, for chunks c0, c0 + cstep, ... (the step kernel spreads the chunks over an env's 4 lanes; a
+// re-evaluation after a reset draws the same noise)
+__device__ __forceinline__ void obs_values(const lrl_env_params& P, V3 blv, V3 bav, V3 pg, const float* cmd,
+                                           const float* q, const float* qd, const float* act, float* ob) {
   int o = 0;
   if (P.observe_vel) {
     ob[o++] = blv.x * P.obs_scale_lin_vel; ob[o++] = blv.y * P.obs_scale_lin_vel; ob[o++] = blv.z * P.obs_scale_lin_vel;
@@ -782,8 +782,12 @@ __device__ __forceinline__ void obs_row(const lrl_env_params& P, const KState& S
   for (int j = 0; j < 12; ++j) ob[o + 12 + j] = qd[j] * P.obs_scale_dof_vel;
 #pragma unroll
   for (int j = 0; j < 12; ++j) ob[o + 24 + j] = act[j];
-  if (P.add_noise) {
-    for (int i0 = 0; i0 < NO; i0 += 4) {
+}
+__device__ __forceinline__ void obs_noise_clip(const lrl_env_params& P, const KState& S, int e, uint64_t genv,
+                                               int64_t step_counter, bool inject, float* ob, int c0, int cstep) {
+  const int NO = P.num_obs;
+  for (int i0 = 4 * c0; i0 < NO; i0 += 4 * cstep) {
+    if (P.add_noise) {
       lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter,
                                (LRL_RNG_OBS_NOISE << 16) ^ (uint32_t)(step_counter >> 32), (uint32_t)(i0 >> 2), S.seed);
 #pragma unroll
@@ -795,8 +799,10 @@ __device__ __forceinline__ void obs_row(const lrl_env_params& P, const KState& S
         }
       }
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k < NO) ob[i0 + k] = fminf(fmaxf(ob[i0 + k], -P.clip_obs), P.clip_obs);
   }
-  for (int i = 0; i < NO; ++i) ob[i] = fminf(fmaxf(ob[i], -P.clip_obs), P.clip_obs);
 }
 __device__ __forceinline__ void priv_row(const lrl_env_params& P, const KState& S, int e, float payload, V3 cb,
                                          const float* ms, float* pr) {
@@ -867,7 +873,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
   for (int s = 0; s < K->num_spheres; ++s)
     if (sph_owner(K, s) == ql) own |= 1ull << s;
-  unsigned long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   LRL_PROF_DECL
 #ifdef LRL_ENV_PROFILE
   prof_t = kt0;
@@ -907,6 +913,22 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   prof_t = clock64();
 #endif
 
+  // the post-physics inputs, read before the contact pass so their latency hides under it
+  float cmd[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) cmd[k] = S.commands[k * N + e];
+  float la[12], lqd[12], fat[4];
+  uint8_t lc[4];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    la[j] = S.last_actions[j * N + e];
+    lqd[j] = S.last_dof_vel[j * N + e];
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    fat[f] = S.feet_air_time[f * N + e];
+    lc[f] = S.last_contacts[f * N + e];
+  }
   // ---- contact forces per body (last sub-step) and the contact-derived signals ----
   int rst = 0;
   float collision = 0.f;
@@ -914,7 +936,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 #pragma unroll
   for (int f = 0; f < 4; ++f) ff[f][0] = ff[f][1] = ff[f][2] = 0.f;
   const float inv_dt = 1.f / P.sim_dt;
-  for (int b = 0; b < K->num_bodies; ++b) {
+  // bodies spread over the env's 4 lanes, then OR / sums over the quad (each foot is one lane's body, so its
+  // force sums exactly with three zeros)
+  for (int b = ql; b < K->num_bodies; b += QL) {
     float fx = 0.f, fy = 0.f, fz = 0.f;
     if (physics) {
       for (int s = K->body_sph_begin[b]; s < K->body_sph_end[b]; ++s)
@@ -926,11 +950,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
       fx *= inv_dt;
       fy *= inv_dt;
       fz *= inv_dt;
-      if (ql == 0) {
-        S.contact[(3 * b) * N + e] = fx;
-        S.contact[(3 * b + 1) * N + e] = fy;
-        S.contact[(3 * b + 2) * N + e] = fz;
-      }
+      S.contact[(3 * b) * N + e] = fx;
+      S.contact[(3 * b + 1) * N + e] = fy;
+      S.contact[(3 * b + 2) * N + e] = fz;
     } else {
       fx = S.contact[(3 * b) * N + e];
       fy = S.contact[(3 * b + 1) * N + e];
@@ -944,7 +966,15 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
     for (int f = 0; f < 4; ++f)
       if (fs == f) { ff[f][0] = fx; ff[f][1] = fy; ff[f][2] = fz; }
   }
+  rst |= __shfl_xor(rst, 1, WAVE);
+  rst |= __shfl_xor(rst, 2, WAVE);
+  collision = quad_sum(collision);
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ff[f][c] = quad_sum(ff[f][c]);
   __syncthreads();  // LDS contact rows are dead from here on; the obs tile reuses them
+  LRL_PROF(10)  // contact forces per body
   const int NO = P.num_obs;
   float* otile = lds;                    // [ENVS][NO]
   float* ptile = lds + ENVS * NO;        // [ENVS][18]
@@ -1000,22 +1030,11 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   const int tout = (P.auto_reset && eplen > P.max_episode_length) ? 1 : 0;
   rst |= tout;
 
+  LRL_PROF(11)  // post-physics loads, teleport, DR redraw
   // rewards
-  float cmd[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) cmd[k] = S.commands[k * N + e];
-  float la[12], lqd[12], fat[4];
-  uint8_t lc[4];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    la[j] = S.last_actions[j * N + e];
-    lqd[j] = S.last_dof_vel[j * N + e];
-  }
-#pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    fat[f] = S.feet_air_time[f * N + e];
-    lc[f] = S.last_contacts[f * N + e];
-  }
+  // per-term rewards go to an LDS row first (the contact rows are dead): no global traffic inside the term
+  // loop, so the episode / command sum updates below can keep all their loads in flight at once
+  float* rt = lds + ENVS * (NO + LRL_NUM_PRIV) + es * LRL_MAX_REWARD_TERMS;
   float rew = 0.f;
   for (int t = 0; t < P.num_reward_terms; ++t) {
     float r = 0.f;
@@ -1105,29 +1124,62 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
     }
     r = r * P.reward_scale[t];
     rew += r;
-    const int slot = P.reward_slot[t];
-    S.episode_sums[slot * N + e] += r;
-    S.command_sums[slot * N + e] += r;
+    rt[t] = r;
+  }
+  {  // episode_sums / command_sums rows of the terms (distinct rows), 8 terms' loads in flight per batch
+    const int nt = P.num_reward_terms;
+    for (int t0 = 0; t0 < nt; t0 += 8) {
+      float ev[8], cv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = t0 + u;
+        if (t < nt) {
+          const int slot = P.reward_slot[t];
+          ev[u] = S.episode_sums[slot * N + e];
+          cv[u] = S.command_sums[slot * N + e];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = t0 + u;
+        if (t < nt) {
+          const int slot = P.reward_slot[t];
+          S.episode_sums[slot * N + e] = ev[u] + rt[t];
+          S.command_sums[slot * N + e] = cv[u] + rt[t];
+        }
+      }
+    }
   }
   if (P.only_positive_rewards) rew = fmaxf(rew, 0.f);
-  const int KS = P.num_sum_keys;
-  S.episode_sums[KS * N + e] += rew;
-  if (P.termination_scale != 0.f) {
-    float r = ((rst && !tout) ? 1.f : 0.f) * P.termination_scale;  // _reward_termination: reset & ~time_out
-    rew += r;
-    S.episode_sums[P.termination_slot * N + e] += r;
-    S.command_sums[P.termination_slot * N + e] += r;
+  {
+    const int KS = P.num_sum_keys;
+    const bool term = P.termination_scale != 0.f;
+    const int ts = term ? P.termination_slot : KS;
+    const float e_tot = S.episode_sums[KS * N + e];
+    const float e_term = S.episode_sums[ts * N + e], c_term = S.command_sums[ts * N + e];
+    float cx[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) cx[k] = S.command_sums[(KS + k) * N + e];
+    S.episode_sums[KS * N + e] = e_tot + rew;
+    if (term) {
+      const float r = ((rst && !tout) ? 1.f : 0.f) * P.termination_scale;  // _reward_termination: reset & ~time_out
+      rew += r;
+      S.episode_sums[ts * N + e] = e_term + r;
+      S.command_sums[ts * N + e] = c_term + r;
+    }
+    S.command_sums[(KS + 0) * N + e] = cx[0] + blv.x;
+    S.command_sums[(KS + 1) * N + e] = cx[1] + bav.z;
+    S.command_sums[(KS + 2) * N + e] = cx[2] + sq(blv.x - cmd[0]);
+    S.command_sums[(KS + 3) * N + e] = cx[3] + sq(bav.z - cmd[2]);
+    S.command_sums[(KS + 4) * N + e] = cx[4] + 1.f;
   }
-  S.command_sums[(KS + 0) * N + e] += blv.x;
-  S.command_sums[(KS + 1) * N + e] += bav.z;
-  S.command_sums[(KS + 2) * N + e] += sq(blv.x - cmd[0]);
-  S.command_sums[(KS + 3) * N + e] += sq(bav.z - cmd[2]);
-  S.command_sums[(KS + 4) * N + e] += 1.f;
 
   // observations / privileged observations -> LDS tiles [env slot][.]
-  obs_row(P, S, e, genv, step_counter, inject, blv, bav, pg, cmd, st.q, st.qd, act, otile + es * NO);
+  LRL_PROF(12)  // rewards, termination, episode / command sums
+  obs_values(P, blv, bav, pg, cmd, st.q, st.qd, act, otile + es * NO);
   priv_row(P, S, e, payload, cb, ms_e, ptile + es * LRL_NUM_PRIV);
 
+  LRL_PROF(13)  // obs / priv rows
   // ---- write back the SoA state ----
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -1165,6 +1217,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   S.time_out[e] = (uint8_t)tout;
   S.rew[e] = rew;
   }  // ql == 0
+  // observation noise + clip, the row's 4-entry chunks spread over the env's 4 lanes
+  __syncthreads();
+  obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, otile + es * NO, ql, QL);
 
   LRL_PROF(6)  // contact forces + post_physics_step + SoA write-back
   // ---- AoS tiles (obs, priv) and the history shift: coalesced over the wave's contiguous rows ----
@@ -1213,7 +1268,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 #ifdef LRL_ENV_PROFILE
   prof[9] = clock64() - kt0;  // the wave's whole lifetime (the phases above should sum to it)
   if (lane == 0)
-    for (int i = 0; i < 10; ++i) atomicAdd(&g_env_prof[i], prof[i]);
+    for (int i = 0; i < 14; ++i) atomicAdd(&g_env_prof[i], prof[i]);
 #endif
 }
 
@@ -1221,12 +1276,12 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 
 extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
 #ifdef LRL_ENV_PROFILE
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 10) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 14) != hipSuccess) return -2;
   if (reset) {
     unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
   }
-  return 10;
+  return 14;
 #else
   (void)out;
   (void)reset;
@@ -1276,7 +1331,8 @@ __global__ void observe_kernel(const KParams* __restrict__ K, KState S, const in
   S.base_ang_vel[e] = bav.x; S.base_ang_vel[N + e] = bav.y; S.base_ang_vel[2 * N + e] = bav.z;
   S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
   float* ob = S.obs + (size_t)e * NO;
-  obs_row(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, blv, bav, pg, cmd, q, qd, act, ob);
+  obs_values(P, blv, bav, pg, cmd, q, qd, act, ob);
+  obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, ob, 0, 1);
   priv_row(P, S, e, S.payload[e], v3(S.com[e], S.com[N + e], S.com[2 * N + e]), ms, S.priv + (size_t)e * LRL_NUM_PRIV);
   if (flags & LRL_STEP_HISTORY) {
     const int H = K->num_history * NO;

@@ -15,11 +15,17 @@ SHAPES = [
     ("AC1 fwd  NT 60->1024", 0, 2, B, 1024, 60),
     ("D1 fwd   NT 630->256 gather", 0, 2, B, 256, 630),
     ("E1 fwd   NT 18->256 gather", 0, 2, B, 256, 18),
+    ("E1 noelu NT 18->256 gather", 0, 1, B, 256, 18),
+    ("E1 plain NT 18->256", 0, 1, B, 256, 18),
+    ("E1 k16   NT 16->256", 0, 1, B, 256, 16),
+    ("E2 fwd   NT 256->128", 0, 2, B, 128, 256),
+    ("E2 noelu NT 256->128", 0, 1, B, 128, 256),
     ("E3 fwd   NT 128->18", 0, 1, B, 18, 128),
     ("D2 fwd   NT 256->32", 0, 2, B, 32, 256),
     ("dH1      NN 256->512 x2", 2, 3, B, 512, 256),
     ("dLat     NN 1024->18", 2, 0, B, 18, 1024),
     ("dHe2     NN 18->128", 2, 3, B, 128, 18),
+    ("dHD1     NN 32->256", 2, 3, B, 256, 32),
     ("dW2      TN 256x512", 3, 4, 256, 512, B),
     ("dWD1     TN 256x630 gather", 3, 4, 256, 630, B),
     ("long-K   NT 4096->256", 0, 2, B, 256, 4096),

@@ -38,7 +38,7 @@ def _tol(ref, k):
                                                (777, 256, 18, True, 2), (513, 18, 128, False, 1),
                                                (640, 256, 630, True, 2), (64, 64, 16, False, 0),
                                                (2048, 32, 512, True, 2), (4096, 18, 128, False, 1), (777, 7, 512, True, 0),
-                                               (1000, 24, 1024, False, 1)])
+                                               (1000, 24, 1024, False, 1), (4096, 256, 18, True, 2), (300, 128, 30, False, 0)])
 def test_forward_nt(M, N, K, gather, epi):
     g = torch.Generator(device=dev).manual_seed(M * 7 + N)
     src_rows = M + 37
@@ -60,7 +60,8 @@ def test_forward_nt(M, N, K, gather, epi):
 
 @pytest.mark.parametrize("M,N,K,delu", [(1024, 512, 256, True), (1536, 256, 128, False), (300, 256, 128, True),
                                          (1000, 18, 1024, False), (513, 512, 256, True),
-                                         (96, 128, 18, True), (3000, 18, 1024, False), (300, 32, 128, False)])
+                                         (96, 128, 18, True), (3000, 18, 1024, False), (300, 32, 128, False),
+                                         (3000, 128, 18, True), (1024, 256, 7, False)])
 def test_backward_data_nn(M, N, K, delu):
     g = torch.Generator(device=dev).manual_seed(M + 3 * N + K)
     dY = torch.randn(M, K, device=dev, generator=g)
