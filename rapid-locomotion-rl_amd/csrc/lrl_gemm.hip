@@ -457,6 +457,129 @@ __global__ __launch_bounds__(GTHREADS) void gemm_glds_kernel(GemmP p) {
 }
 
 
+// BK = 32 variant of the LDS-DMA kernel (k a multiple of 32): 16 MFMAs per wave between barriers instead
+// of 8.  [row][32 k] images (128-B rows): 16-B chunk c of row r sits in slot c ^ ((r >> 1) & 7), so the 8
+// lanes of a ds_read_b128 group (8 consecutive rows, one chunk) hit 8 distinct 16-B bank groups; DMA d of a
+// slice fills rows 8d .. 8d+7 (lane l: row 8d + l / 8, slot l % 8, source chunk pre-swizzled).  The NN B image
+// is [32 k][64 n], DMA d filling k-rows 4d .. 4d+3.  Lane half h uses k = 16h .. 16h+15 at MFMA steps 0..15.
+template <int LAYOUT, int EPI>
+__global__ __launch_bounds__(GTHREADS) void gemm_glds32_kernel(GemmP p) {
+  constexpr int BM = 64, BN = 64, BKD = 32, NST = 3, IMG = 2048;
+  constexpr bool BNC = (LAYOUT & 2) != 0;
+  static_assert((LAYOUT & 1) == 0, "A must be k-contiguous");
+  __shared__ __attribute__((aligned(16))) float S[NST * 2 * IMG];
+  const int mt = p.M / BM, nt = p.N / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, g = L / (nt * mt);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ B = p.B + g * p.gb;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int K = p.K;
+  const float* asrc[2];
+  const float* bsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = 2 * w + i, row = 8 * d + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    asrc[i] = A + (p.a_rows ? p.a_rows[m0 + row] : (int64_t)(m0 + row)) * p.lda + 4 * chunk;
+    if constexpr (!BNC) bsrc[i] = B + (int64_t)(n0 + row) * p.ldb + 4 * chunk;
+    else bsrc[i] = B + (int64_t)(4 * d + (lane >> 4)) * p.ldb + n0 + 4 * (lane & 15);
+  }
+  const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
+  auto dma = [&](const float* src, uint32_t lds_off) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_off)
+                 : "memory");
+  };
+  auto issue = [&](int st, int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t base =
+          __builtin_amdgcn_readfirstlane(s_lds + (uint32_t)((st * 2 * IMG + (2 * w + i) * 256) * 4));
+      dma(asrc[i] + k0, base);
+      dma(BNC ? bsrc[i] + (int64_t)k0 * p.ldb : bsrc[i] + k0, base + IMG * 4);
+    }
+  };
+  float xaux[16];
+  if constexpr (EPI == EPI_DELU) {
+    const float* __restrict__ ax = p.aux + g * p.gaux;
+    const int col = n0 + wn + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+      xaux[r] = ax[(int64_t)row * p.ld_aux + col];
+    }
+  }
+  f32x16 acc, acc2;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+  const int ns = K / BKD;
+  issue(0, 0);
+  if (ns > 1) issue(1, BKD);
+  const int ai = wm + li, aswz = (ai >> 1) & 7;
+  const int bi = wn + li, bswz = (bi >> 1) & 7;
+  for (int s = 0; s < ns; ++s) {
+    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < ns) issue((s + 2) % NST, (s + 2) * BKD);
+    const float* As = S + (s % NST) * 2 * IMG;
+    const float* Bs = As + IMG;
+    float a[16], b[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(As + ai * 32 + 4 * ((4 * h + q) ^ aswz));
+      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+    }
+    if constexpr (!BNC) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(Bs + bi * 32 + 4 * ((4 * h + q) ^ bswz));
+        b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) b[t] = Bs[(16 * h + t) * BN + bi];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (t & 1) acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[t], acc2, 0, 0, 0);
+      else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[t], acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float* __restrict__ C = p.C + g * p.gc;
+  const int col = n0 + wn + li;
+  float bj = 0.f;
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = p.bias[g * p.gbias + col];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+    float v = acc[r] + acc2[r];
+    if constexpr (EPI == EPI_BIAS) v += bj;
+    if constexpr (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+    if constexpr (EPI == EPI_DELU) {
+      const float x = xaux[r];
+      v = x > 0.f ? v : v * (x + 1.f);
+    }
+    C[(int64_t)row * p.ldc + col] = v;
+  }
+}
+
 // ---- thin products: C[M][N <= 32] = A[M][K] op(B), K = 128 NBK (512 or 1024) ----
 // (the latent gradient dY W[:, 42:60] over k = 1024, the 18-/32-wide output layers.)  A register-staged
 // 32-wide tile wastes most of its loads here and a split-k launch pays a partial round trip through HBM,
@@ -794,7 +917,15 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   if (layout != GEMM_TN && p.splits == 1 && p.M % 64 == 0 && p.N % 64 == 0 && p.K % 16 == 0 && p.K >= 32 &&
       p.avec == 4 && p.bvec == 4 && epi != EPI_PARTIAL && (layout == GEMM_NT || layout == GEMM_NN)) {
     dim3 g1((p.M / 64) * (p.N / 64) * groups);
-#define LRL_GLDS(L, E) hipLaunchKernelGGL((gemm_glds_kernel<L, E>), g1, dim3(GTHREADS), 0, st, p)
+#ifndef LRL_GLDS_BK32
+#define LRL_GLDS_BK32 1
+#endif
+    const bool bk32 = LRL_GLDS_BK32 && p.K % 32 == 0 && p.K >= 64;
+#define LRL_GLDS(L, E)                                                                      \
+  do {                                                                                      \
+    if (bk32) hipLaunchKernelGGL((gemm_glds32_kernel<L, E>), g1, dim3(GTHREADS), 0, st, p); \
+    else hipLaunchKernelGGL((gemm_glds_kernel<L, E>), g1, dim3(GTHREADS), 0, st, p);        \
+  } while (0)
     if (layout == GEMM_NT) {
       if (epi == EPI_STORE) LRL_GLDS(GEMM_NT, EPI_STORE);
       else if (epi == EPI_BIAS) LRL_GLDS(GEMM_NT, EPI_BIAS);
