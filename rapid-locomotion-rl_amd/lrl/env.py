@@ -73,8 +73,6 @@ class LeggedRobotEnv:
             cfg.domain_rand.push_robots = False
             cfg.domain_rand.randomize_friction = False
             cfg.env.episode_length_s = 100
-        if eval_cfg is not None:
-            raise NotImplementedError("train/eval env split is a next-row item (SURVEY.md §8(f) rank 2)")
         self.cfg, self.eval_cfg = cfg, eval_cfg
         # legacy_fork=False re-enables what the fork comments out: reset_idx inside step
         # for terminated / timed-out envs, command resampling every resampling_time and at resets
@@ -83,8 +81,10 @@ class LeggedRobotEnv:
         if self.device.type != "cuda" or not torch.cuda.is_available():
             raise RuntimeError("LeggedRobotEnv runs on the GPU through liblrl.so; no CPU path exists")
         self.headless = True
-        self.num_train_envs = self.num_envs = cfg.env.num_envs
-        self.num_eval_envs = 0
+        # train / eval split (base_task.py:43-50): eval envs follow the train envs in one sim
+        self.num_train_envs = cfg.env.num_envs
+        self.num_eval_envs = eval_cfg.env.num_envs if eval_cfg is not None else 0
+        self.num_envs = self.num_train_envs + self.num_eval_envs
         self.num_obs = cfg.env.num_observations
         self.num_privileged_obs = cfg.env.num_privileged_obs
         self.num_actions = cfg.env.num_actions
@@ -102,6 +102,20 @@ class LeggedRobotEnv:
             self._flat_terrain()
         self._P = lparams.build_params(cfg, self.robot, auto_reset=not self.legacy_fork,
                                        solver_iterations=solver_iterations)
+        if eval_cfg is not None:
+            # one kernel parameter block serves both groups: the eval cfg may differ from the train cfg only in
+            # what the host applies per group (command ranges / curriculum, reset logging)
+            if eval_cfg.terrain.mesh_type in ("heightfield", "trimesh"):
+                eval_cfg.terrain.x_offset = 0  # flat-terrain bookkeeping, as for the train cfg
+            Pe = lparams.build_params(eval_cfg, self.robot, auto_reset=not self.legacy_fork,
+                                      solver_iterations=solver_iterations)
+            def differs(f):
+                a, b = getattr(self._P, f), getattr(Pe, f)
+                return bytes(a) != bytes(b) if isinstance(a, C.Array) else a != b
+            diff = [f for f, _ in type(self._P)._fields_ if differs(f)]
+            if diff:
+                raise NotImplementedError(f"eval_cfg differs from cfg in per-step kernel parameters {diff}; "
+                                          "only host-side (command / curriculum) differences are supported")
         self._M = lparams.build_model(self.robot)
         self.sim_params = Section(dt=lparams.sim_dt(cfg))
         self.dt = cfg.control.decimation * self.sim_params.dt
@@ -162,6 +176,9 @@ class LeggedRobotEnv:
         self.base_quat = self.root_states[:, 3:7]
         keys = list(self.reward_scales)
         self.episode_sums = {k: self._episode_sums[i] for i, k in enumerate(keys + ["total"])}
+        # eval-env episode results (legged_robot.py:1101-1105): -1 = not finished in this evaluation batch
+        self.episode_sums_eval = {k: -torch.ones(self.num_envs, device=self.device) for k in keys}
+        self.episode_sums_eval["total"] = torch.zeros(self.num_envs, device=self.device)
         self.command_sums = {k: self._command_sums[i] for i, k in enumerate(
             keys + ["lin_vel_raw", "ang_vel_raw", "lin_vel_residual", "ang_vel_residual", "ep_timesteps"])}
         self.default_dof_pos = torch.tensor(self._P.default_dof_pos[:], device=self.device).unsqueeze(0)
@@ -368,11 +385,20 @@ class LeggedRobotEnv:
         return obs
 
     def reset_idx(self, env_ids):
-        """legged_robot.py:227-290 (train envs)."""
+        """legged_robot.py:227-290; train and eval envs (env id >= num_train_envs) go through their own cfg
+        for the command curriculum (_call_train_eval, :456-469) and their own episode logging."""
         env_ids = torch.as_tensor(env_ids, device=self.device).long()
         if len(env_ids) == 0:
             return
-        self.update_command_curriculum(env_ids, self.cfg)
+        n_tr = self.num_train_envs
+        if self.num_eval_envs:
+            tr, ev = env_ids[env_ids < n_tr], env_ids[env_ids >= n_tr]
+        else:
+            tr, ev = env_ids, env_ids[:0]
+        if len(tr):
+            self.update_command_curriculum(tr, self.cfg)
+        if len(ev):
+            self.update_command_curriculum(ev, self.eval_cfg)
         if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
             self.resample_commands(env_ids)
         ids32 = env_ids.to(torch.int32).contiguous()
@@ -381,16 +407,25 @@ class LeggedRobotEnv:
             t = self.cfg.terrain
             xo = float(t.x_init_range) + float(t.x_init_offset)
             yo = float(t.x_init_range) + float(t.y_init_offset)
-        # episode logging before the kernel zeroes the per-env state (:261-267)
-        ep = {}
-        sel = self._episode_sums[:, env_ids]
-        means = sel.mean(dim=1)
-        for i, k in enumerate(self.episode_sums):
-            ep["rew_" + k] = means[i]
-        self._episode_sums[:, env_ids] = 0.0
+        # episode logging before the per-env sums are zeroed (:261-276)
+        if len(tr):
+            ep = {}
+            means = self._episode_sums[:, tr].mean(dim=1)
+            for i, k in enumerate(self.episode_sums):
+                ep["rew_" + k] = means[i]
+            self._episode_sums[:, tr] = 0.0
+            self.extras["train/episode"] = ep
+        if len(ev):
+            self.extras["eval/episode"] = {}
+            for i, k in enumerate(self.episode_sums):  # keep the first finished episode of each eval env
+                unset = ev[self.episode_sums_eval[k][ev] == -1]
+                self.episode_sums_eval[k][unset] = self.episode_sums[k][unset]
+            self._episode_sums[:, ev] = 0.0
         _abi.check(self._L.lrl_sim_reset_idx_ex(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
                                                 C.c_int32(1), C.c_float(xo), C.c_float(yo), self._stream()))
-        self.extras["train/episode"] = ep
+        ep = self.extras.get("train/episode")
+        if ep is None:
+            ep = self.extras["train/episode"] = {}
         if self.cfg.commands.command_curriculum:
             self.env_command_bins_t = torch.tensor(self.env_command_bins, dtype=torch.float, device=self.device)
             self.extras["env_bins"] = self.env_command_bins_t[:self.num_train_envs]
@@ -419,7 +454,23 @@ class LeggedRobotEnv:
                                                                    c.max_yaw_curriculum)
 
     def reset_evaluation_envs(self):
-        return None  # no eval_cfg (legged_robot.py:205)
+        """legged_robot.py:204-225: log the evaluation batch (mean of each eval env's first finished episode,
+        or its running sum if none finished), advance the eval command curriculum, reset every eval env."""
+        if self.eval_cfg is None:
+            return
+        ids = torch.arange(self.num_train_envs, self.num_envs, device=self.device)
+        ep = self.extras.get("eval/episode")
+        if ep is None:
+            ep = self.extras["eval/episode"] = {}
+        for k in self.episode_sums_eval:
+            unset = ids[self.episode_sums_eval[k][ids] == -1]
+            self.episode_sums_eval[k][unset] = self.episode_sums[k][unset]
+            s = self.episode_sums_eval[k]
+            ep["rew_" + k] = torch.mean(s[s != -1])
+        self.update_command_curriculum(ids, self.eval_cfg, self.episode_sums_eval)
+        self.reset_idx(ids)
+        for k in self.episode_sums_eval:
+            self.episode_sums_eval[k] = -torch.ones(self.num_envs, device=self.device)
 
     # ---- gymapi-style setters (data is already in place when written through the views) ----
     def set_actor_root_state_tensor_indexed(self, root_states, env_ids):

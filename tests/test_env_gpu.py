@@ -258,3 +258,55 @@ def test_upstream_resets_timeouts_and_command_resampling():
         seen_resample |= bool((changed & due & ~reset).any())
     assert seen_timeout and seen_resample
     inner.close()
+
+
+def test_train_eval_split():
+    """eval_cfg (base_task.py:43-50, legged_robot.py:204-290, 456-469): eval envs follow the train envs in one
+    sim; resets log train envs into extras['train/episode'] and keep each eval env's first finished episode;
+    reset_evaluation_envs reports the batch and resets the eval envs; Runner drives the eval envs with the
+    student policy.  An eval cfg that changes per-step kernel parameters is refused."""
+    from lrl.env import LeggedRobotEnv
+    from lrl.history import HistoryWrapper
+    from lrl.ppo import runner as R
+    n_tr, n_ev = 64, 32
+    env = LeggedRobotEnv("cuda:0", cfg=_cfg("mc", n_tr), eval_cfg=_cfg("mc", n_ev))
+    assert (env.num_train_envs, env.num_eval_envs, env.num_envs) == (n_tr, n_ev, n_tr + n_ev)
+    env.reset()  # (the initial reset_idx of every env records the eval envs' zero sums, as in the reference)
+    env.reset_evaluation_envs()  # a fresh evaluation batch: every eval env unset (-1)
+    a = torch.zeros(n_tr + n_ev, 12, device="cuda:0")
+    for _ in range(3):
+        env.step(a)
+    sums = {k: v.clone() for k, v in env.episode_sums.items()}
+    ids = torch.tensor([1, 5, n_tr + 2, n_tr + 7], device="cuda:0")
+    env.reset_idx(ids)
+    torch.cuda.synchronize()
+    assert "train/episode" in env.extras and "eval/episode" in env.extras
+    k0 = next(iter(env.episode_sums_eval))
+    ev = env.episode_sums_eval[k0]
+    assert torch.equal(ev[ids[2:]], sums[k0][ids[2:]])  # eval envs: their finished episode kept
+    assert bool((ev[:n_tr] == -1).all()) and bool((ev[n_tr:][ev[n_tr:] != -1].numel() == 2))
+    np.testing.assert_allclose(env.extras["train/episode"]["rew_" + k0].item(), sums[k0][ids[:2]].mean().item(),
+                               rtol=1e-6)
+    assert bool((env.episode_sums[k0][ids] == 0).all())
+    logged = {}
+    env.extras["eval/episode"] = logged
+    env.reset_evaluation_envs()
+    # the batch means land in the current eval/episode dict; reset_idx of the eval envs then starts a fresh
+    # one (legged_robot.py:216 then :270 — the reference's order, reproduced)
+    assert set("rew_" + k for k in env.episode_sums_eval) <= set(logged)
+    assert env.extras["eval/episode"] is not logged
+    assert bool((env.episode_sums_eval[k0] == -1).all())
+    assert bool((env.episode_length_buf[n_tr:] == 0).all())
+    env.close()
+    bad = _cfg("mc", n_ev)
+    bad.control.stiffness = {k: 2 * v for k, v in bad.control.stiffness.items()}
+    with pytest.raises(NotImplementedError):
+        LeggedRobotEnv("cuda:0", cfg=_cfg("mc", n_tr), eval_cfg=bad)
+    # Runner: train envs through PPO.act, eval envs through the student (act_student_fused)
+    R.RunnerArgs.save_interval = 0
+    henv = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=_cfg("mc", n_tr), eval_cfg=_cfg("mc", n_ev)))
+    runner = R.Runner(henv, device="cuda:0", seed=3)
+    runner.learn(1, eval_freq=1)
+    assert runner.alg.storage.num_envs == n_tr
+    assert "eval/episode" in henv.env.extras
+    henv.env.close()
