@@ -19,6 +19,7 @@ Fixtures written (all small .npz, inputs + expected outputs):
   ppo_update.npz      PPO.act/process_env_step/compute_returns/update (ppo.py:62-178) with
                       deterministic weights (see ``init_params``) and injected randomness.
   state_dict_keys.json  ActorCritic state-dict layout (actor_critic.py, 35 keys incl. encoder.*)
+  terrain.npz         the reference's Terrain (terrain.py) over this repo's terrain_utils restatement.
   checkpoint_last.npz   the reference run's trained ac_weights_last.pt (loaded weights_only=True) and the
                       reference ActorCritic's teacher / student / value outputs on it for fixed inputs.
 
@@ -548,8 +549,45 @@ def gen_checkpoint():
     print("checkpoint:", len(sd), "tensors,", sum(v.numel() for v in sd.values()), "values")
 
 
+# ----------------------------------------------------------------------------------------
+def _terrain_cfg(**kw):
+    c = types.SimpleNamespace(mesh_type="trimesh", curriculum=True, selected=False, terrain_kwargs=None,
+                              terrain_proportions=[0.1] * 10, num_rows=3, num_cols=10, terrain_length=8.0,
+                              terrain_width=8.0, horizontal_scale=0.1, vertical_scale=0.005, border_size=2.0,
+                              difficulty_scale=1.0, max_platform_height=0.2, terrain_smoothness=0.005,
+                              terrain_noise_magnitude=0.1, slope_treshold=0.75)
+    c.__dict__.update(kw)
+    return c
+
+
+def gen_terrain():
+    """The reference's Terrain (mini_gym/utils/terrain.py) over this repo's restatement of the un-vendored
+    isaacgym.terrain_utils primitives (installed as the stub module): pins the tile layout, curriculum /
+    random type selection, border and env origins; the primitives themselves stay parity-unpinned."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "rapid-locomotion-rl_amd"))
+    from lrl import terrain as ours
+    tu = sys.modules["isaacgym.terrain_utils"]
+    for k in ("SubTerrain", "random_uniform_terrain", "pyramid_sloped_terrain", "pyramid_stairs_terrain",
+              "discrete_obstacles_terrain", "stepping_stones_terrain", "convert_heightfield_to_trimesh"):
+        setattr(tu, k, getattr(ours, k))
+    from mini_gym.utils.terrain import Terrain
+    out = {}
+    for name, kw, seed in (("curriculum", {}, 3), ("random", dict(curriculum=False, num_rows=2, num_cols=3), 7)):
+        np.random.seed(seed)
+        c = _terrain_cfg(**kw)
+        t = Terrain(c, 64)
+        out[name + "_hf"] = t.height_field_raw
+        out[name + "_origins"] = c.env_origins
+        out[name + "_seed"] = np.array(seed)
+        if name == "curriculum":
+            out["curriculum_ntri"] = np.array(len(t.triangles))
+            out["curriculum_vsum"] = np.array(t.vertices.astype(np.float64).sum(0))
+    np.savez_compressed(os.path.join(HERE, "terrain.npz"), **out)
+    print("terrain:", {k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     gens = dict(post_physics_mc=lambda: gen_post_physics("mc"), post_physics_go1=lambda: gen_post_physics("go1"),
-                curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint)
+                curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint, terrain=gen_terrain)
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()
