@@ -56,7 +56,8 @@ extern "C" {
 #define LRL_MAX_SPHERES 40
 #define LRL_NUM_DOF 12
 #define LRL_NUM_LEGS 4
-#define LRL_MAX_OBS 64
+#define LRL_MAX_OBS 256       /* 42 + a 17 x 11 height scan (legged_robot_config.py:46-47) fits */
+#define LRL_MAX_HEIGHT_POINTS 192
 #define LRL_MAX_REWARD_TERMS 24
 #define LRL_NUM_PRIV 18
 
@@ -153,6 +154,19 @@ typedef struct lrl_env_params {
   int32_t num_history; /* HistoryWrapper length (15) */
   int32_t auto_reset;  /* 0 = fork semantics (no resets inside step, Q2); 1 = upstream */
   int32_t max_episode_length;
+  /* terrain (legged_robot.py:419-441 create_sim, :1112-1160 ground / heightfield / trimesh,
+   * :1453-1503 height scan).  terrain_mesh 0: ground plane z = 0 (plane, or a trimesh whose height
+   * field is all zero); 1: contacts against the triangle mesh given to lrl_sim_set_terrain. */
+  int32_t terrain_mesh;
+  float border_size, horizontal_scale, vertical_scale;
+  int32_t measure_heights;    /* _get_heights every step, obs += clip(z - 0.5 - h, -1, 1) * scale */
+  int32_t num_height_points;  /* 17 x 11 = 187 */
+  float height_points[LRL_MAX_HEIGHT_POINTS][2]; /* base-frame (x, y), meshgrid(x, y) order (:1453-1467) */
+  float obs_scale_height;
+  /* envs with index >= num_train_envs (the eval group, base_task.py:43-50) teleport with the eval tiles' x
+   * offset (legged_robot.py:772 under _call_train_eval) */
+  int32_t num_train_envs;
+  float teleport_x_offset_eval;
 } lrl_env_params;
 
 /* ------------------------------------------------------------------------------------------
@@ -201,6 +215,7 @@ enum lrl_tensor_id {
   LRL_T_ENV_ORIGINS,     /* [N,3] */
   LRL_T_BASE_LIN_VEL, LRL_T_BASE_ANG_VEL, LRL_T_PROJECTED_GRAVITY, /* [N,3] body frame */
   LRL_T_JOINT_POS_TARGET,/* [N,12] */
+  LRL_T_MEASURED_HEIGHTS,/* [N,num_height_points] (_get_heights, written by lrl_sim_step when measure_heights) */
   LRL_T_NUM
 };
 
@@ -246,6 +261,13 @@ int32_t lrl_sim_set_root_state_indexed(lrl_sim* sim, const float* root /*[N,13] 
 int32_t lrl_sim_set_dof_state_indexed(lrl_sim* sim, const float* dof_pos, const float* dof_vel,
                                       const int32_t* env_ids, int32_t n, void* stream);
 int32_t lrl_sim_refresh_rigid_body_state(lrl_sim* sim, void* stream);
+/* Terrain mesh for params->terrain_mesh == 1 (gym.add_triangle_mesh / add_heightfield, legged_robot.py:
+ * 1122-1160): `vertices` host [rows*cols][3] in the terrain frame (the Terrain class's trimesh vertices, or
+ * the unmoved grid for a heightfield), placed at (-border_size, -border_size, 0) like tm_params.transform;
+ * triangles follow the grid (cell (i, j): (v(i,j), v(i+1,j+1), v(i,j+1)) and (v(i,j), v(i+1,j), v(i+1,j+1))).
+ * `height_samples` host int16 [rows*cols] (Terrain.heightsamples) feed the height scan. */
+int32_t lrl_sim_set_terrain(lrl_sim* sim, const float* vertices, const int16_t* height_samples, int32_t rows,
+                            int32_t cols);
 /* HistoryWrapper.get_observations side effect (history_wrapper.py:26-30) */
 int32_t lrl_sim_shift_history(lrl_sim* sim, void* stream);
 

@@ -40,7 +40,7 @@ ENV_FIELDS = ["root", "dof_pos", "dof_vel", "contact", "torques", "actions", "la
               "last_root_vel", "commands", "obs", "priv", "hist", "rew", "reset", "last_contacts", "episode_length",
               "episode_sums", "command_sums", "feet_air_time", "friction", "restitution", "payload", "com",
               "motor_strength", "kp", "kd", "base_lin_vel", "base_ang_vel", "projected_gravity",
-              "joint_pos_target"]
+              "joint_pos_target", "heights"]
 
 
 class _Env(C.Structure):
@@ -51,7 +51,7 @@ def _dtype(f):
     return {"reset": np.uint8, "last_contacts": np.uint8, "episode_length": np.int32}.get(f, np.float32)
 
 
-def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs):
+def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs, num_height_points=0):
     """Zero-initialised logical-layout host state."""
     shp = dict(root=(n, 13), dof_pos=(n, 12), dof_vel=(n, 12), contact=(n, num_bodies, 3), torques=(n, 12),
                actions=(n, 12), last_actions=(n, 12), last_dof_vel=(n, 12), last_root_vel=(n, 6),
@@ -59,7 +59,8 @@ def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs):
                reset=(n,), last_contacts=(n, 4), episode_length=(n,), episode_sums=(n_es, n),
                command_sums=(n_cs, n), feet_air_time=(n, 4), friction=(n,), restitution=(n,), payload=(n,),
                com=(n, 3), motor_strength=(n, 12), kp=(n, 12), kd=(n, 12), base_lin_vel=(n, 3),
-               base_ang_vel=(n, 3), projected_gravity=(n, 3), joint_pos_target=(n, 12))
+               base_ang_vel=(n, 3), projected_gravity=(n, 3), joint_pos_target=(n, 12),
+               heights=(n, max(num_height_points, 1)))
     st = {k: np.zeros(v, _dtype(k)) for k, v in shp.items()}
     st["root"][:, 6] = 1.0
     st["motor_strength"][:] = 1
@@ -87,6 +88,38 @@ def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_
     if rc != 0:
         raise RuntimeError("oracle env_step failed (non-SPD mass matrix)")
     return state
+
+
+_terrain_keep = None
+
+
+def set_terrain(vertices_world, heights_m):
+    """lrl_oracle.c:lrlo_set_terrain — the terrain mesh the oracle's contacts and height scan use (params
+    terrain_mesh = 1): vertices [rows, cols, 3] in the world frame, height samples [rows, cols] in metres."""
+    global _terrain_keep
+    v = np.ascontiguousarray(vertices_world, np.float32)
+    h = np.ascontiguousarray(heights_m, np.float32)
+    rows, cols = h.shape
+    assert v.shape == (rows, cols, 3)
+    _terrain_keep = (v, h)
+    lib().lrlo_set_terrain(v.ctypes.data_as(C.c_void_p), h.ctypes.data_as(C.c_void_p), C.c_int(rows), C.c_int(cols))
+
+
+def terrain_query(params, p, r):
+    """lrl_oracle.c:terrain_query — (separation, world normal) of a sphere against the terrain mesh."""
+    L = lib()
+    L.lrlo_terrain_query.restype = C.c_double
+    pp = np.ascontiguousarray(p, np.float64).reshape(3)
+    n = np.zeros(3, np.float64)
+    sep = L.lrlo_terrain_query(C.byref(params), pp.ctypes.data_as(C.c_void_p), C.c_double(r),
+                               n.ctypes.data_as(C.c_void_p))
+    return sep, n
+
+
+def height_sample(params, root, k):
+    lib().lrlo_height_sample.restype = C.c_float
+    r = np.ascontiguousarray(root, np.float32).reshape(13)
+    return lib().lrlo_height_sample(C.byref(params), r.ctypes.data_as(C.c_void_p), C.c_int(k))
 
 
 def physics_substep(model, params, root, q, qd, tau, friction, restitution, payload, com):

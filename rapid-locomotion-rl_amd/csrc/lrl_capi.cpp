@@ -26,7 +26,7 @@ extern "C" int lrl_set_error(int code, const char* msg) { return fail(code, "%s"
   } while (0)
 
 extern "C" {
-hipError_t lrl_launch_env_step(const KParams*, const KState*, int, const float*, uint32_t, int64_t, hipStream_t);
+hipError_t lrl_launch_env_step(const KParams*, const KState*, int, const float*, uint32_t, int64_t, int, hipStream_t);
 hipError_t lrl_launch_observe(const KParams*, const KState*, const int32_t*, int32_t, uint32_t, int64_t, hipStream_t);
 hipError_t lrl_env_kernel_setup(int lds_bytes);
 hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, int64_t,
@@ -54,6 +54,7 @@ struct lrl_sim {
   int32_t* d_body_leg = nullptr;
   int32_t* d_body_link = nullptr;
   float* d_foot_xyz = nullptr;
+  void* terr = nullptr;  // terrain mesh buffers (lrl_sim_set_terrain)
 };
 
 static void quat_to_rowmajor(const float* q, float* R) {
@@ -73,7 +74,11 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
   if (p->num_reward_terms < 0 || p->num_reward_terms > LRL_MAX_REWARD_TERMS) return fail(LRL_E_INVALID, "reward terms");
   for (int t = 0; t < p->num_reward_terms; ++t)
     if (p->reward_term[t] < 0 || p->reward_term[t] >= LRL_R_NUM_TERMS) return fail(LRL_E_INVALID, "reward term id");
-  int obs_expected = 3 + (p->observe_command ? 3 : 0) + 36 + (p->observe_vel ? 6 : 0);
+  if (p->measure_heights && (p->num_height_points <= 0 || p->num_height_points > LRL_MAX_HEIGHT_POINTS))
+    return fail(LRL_E_INVALID, "num_height_points %d", p->num_height_points);
+  if (p->terrain_mesh && p->horizontal_scale <= 0.f) return fail(LRL_E_INVALID, "horizontal_scale");
+  int obs_expected = 3 + (p->observe_command ? 3 : 0) + 36 + (p->observe_vel ? 6 : 0) +
+                     (p->measure_heights ? p->num_height_points : 0);
   if (obs_expected != p->num_obs) return fail(LRL_E_INVALID, "obs layout %d != num_obs %d", obs_expected, p->num_obs);
   for (int l = 0; l < 4; ++l)
     for (int j = 0; j < 3; ++j) {
@@ -186,6 +191,8 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   addf(&S.motor_strength, 12ull * N); addf(&S.kp, 12ull * N); addf(&S.kd, 12ull * N); addf(&S.env_origins, 3ull * N);
   addf(&S.base_lin_vel, 3ull * N); addf(&S.base_ang_vel, 3ull * N); addf(&S.projected_gravity, 3ull * N);
   addf(&S.joint_pos_target, 12ull * N);
+  const int NP = params->measure_heights ? params->num_height_points : 0;
+  addf(&S.heights, (size_t)(NP > 0 ? NP : 1) * N);
   size_t total = 0;
   for (auto& f : fields) total += (f.bytes + 255) / 256 * 256;
   void* arena = nullptr;
@@ -262,7 +269,59 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   soa2(LRL_T_BASE_ANG_VEL, S.base_ang_vel, 3, LRL_F32);
   soa2(LRL_T_PROJECTED_GRAVITY, S.projected_gravity, 3, LRL_F32);
   soa2(LRL_T_JOINT_POS_TARGET, S.joint_pos_target, 12, LRL_F32);
+  soa2(LRL_T_MEASURED_HEIGHTS, S.heights, NP, LRL_F32);
   *out = s;
+  return 0;
+}
+
+int32_t lrl_sim_set_terrain(lrl_sim* s, const float* vertices, const int16_t* height_samples, int32_t rows,
+                            int32_t cols) {
+  if (!s || !vertices || !height_samples || rows < 2 || cols < 2) return fail(LRL_E_INVALID, "bad terrain arguments");
+  if (!s->hk.p.terrain_mesh) return fail(LRL_E_INVALID, "params.terrain_mesh is 0 (plane ground)");
+  const size_t nv = (size_t)rows * cols;
+  const float bs = s->hk.p.border_size, vs = s->hk.p.vertical_scale;
+  // vertex grid in the world frame (tm_params.transform.p = (-border, -border, 0), legged_robot.py:1152-1154)
+  std::vector<float> vtx(4 * nv), h(nv), hmax(nv, 0.f), rowmax(nv);
+  for (size_t v = 0; v < nv; ++v) {
+    vtx[4 * v] = vertices[3 * v] - bs;
+    vtx[4 * v + 1] = vertices[3 * v + 1] - bs;
+    vtx[4 * v + 2] = vertices[3 * v + 2];
+    vtx[4 * v + 3] = 0.f;
+    h[v] = (float)height_samples[v] * vs;  // torch: int16 tensor * python float -> float32
+  }
+  // a query at cell (i, j) reads vertices [i-1, i+2] x [j-1, j+2]: separable max filter of the vertex z
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) {
+      float m = -3.0e38f;
+      for (int jj = j - 1; jj <= j + 2; ++jj)
+        if (jj >= 0 && jj < cols) m = fmaxf(m, vtx[4 * ((size_t)i * cols + jj) + 2]);
+      rowmax[(size_t)i * cols + j] = m;
+    }
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) {
+      float m = -3.0e38f;
+      for (int ii = i - 1; ii <= i + 2; ++ii)
+        if (ii >= 0 && ii < rows) m = fmaxf(m, rowmax[(size_t)ii * cols + j]);
+      hmax[(size_t)i * cols + j] = m;
+    }
+  HIPCHECK(hipSetDevice(s->device));
+  (void)hipFree(s->terr);
+  s->terr = nullptr;
+  const size_t bytes = nv * 4 * sizeof(float) + 2 * nv * sizeof(float);
+  if (hipMalloc(&s->terr, bytes) != hipSuccess) return fail(LRL_E_NOMEM, "hipMalloc %zu bytes (terrain)", bytes);
+  float* dv = (float*)s->terr;
+  float* dmax = dv + 4 * nv;
+  float* dh = dmax + nv;
+  HIPCHECK(hipMemcpy(dv, vtx.data(), nv * 16, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dmax, hmax.data(), nv * 4, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dh, h.data(), nv * 4, hipMemcpyHostToDevice));
+  s->hk.terr_vtx = dv;
+  s->hk.terr_hmax = dmax;
+  s->hk.terr_h = dh;
+  s->hk.terr_rows = rows;
+  s->hk.terr_cols = cols;
+  s->hk.terr_inv_hs = 1.f / s->hk.p.horizontal_scale;
+  HIPCHECK(hipMemcpy(s->dk, &s->hk, sizeof(KParams), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -274,6 +333,7 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->d_body_leg);
   (void)hipFree(s->d_body_link);
   (void)hipFree(s->d_foot_xyz);
+  (void)hipFree(s->terr);
   delete s;
   return 0;
 }
@@ -295,8 +355,10 @@ int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* str
   if (!s || !actions) return fail(LRL_E_INVALID, "null argument");
   if ((flags & LRL_STEP_INJECT_UNIFORM) && (!s->S.inj_noise || !s->S.inj_dr))
     return fail(LRL_E_INVALID, "injected uniforms not set");
+  if (s->hk.p.terrain_mesh && !s->hk.terr_vtx) return fail(LRL_E_INVALID, "terrain_mesh set but no lrl_sim_set_terrain");
   s->step_counter += 1;  // common_step_counter (legged_robot.py:153)
-  HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, (hipStream_t)stream));
+  HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, s->hk.p.terrain_mesh,
+                               (hipStream_t)stream));
   return 0;
 }
 

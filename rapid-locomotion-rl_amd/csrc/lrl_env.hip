@@ -280,6 +280,100 @@ __device__ __forceinline__ V3 leg_qd(const Lds& M, int L, const float* vb) {
   return v3(q[0], q[1], q[2]);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Terrain mesh contact (own model; PhysX's trimesh / heightfield collision is closed): the sphere centre p
+// is tested against the 18 triangles of the 3x3 grid cells around it (vertex moves of the slope-corrected
+// trimesh are at most one cell, so every triangle within a cell of p is among them); the triangle whose
+// closest point is nearest wins (ties: first in cell order).  Inside its face region, or with p below its
+// plane, the contact normal is the face normal and the separation the signed plane distance minus r;
+// against an edge or vertex from outside, the normal points from the closest point to p and the separation
+// is the distance minus r.  A conservative max-height map skips the test for spheres clear of the terrain.
+// ------------------------------------------------------------------------------------------------
+struct THit {
+  float sep;
+  V3 n;  // world frame
+};
+__device__ __forceinline__ V3 terr_v(const float* __restrict__ vtx, int idx) {
+  const float4 v = reinterpret_cast<const float4*>(vtx)[idx];
+  return v3(v.x, v.y, v.z);
+}
+// closest point of triangle (a, b, c) to p (Voronoi regions, Ericson 5.1.5); face = p projects inside
+__device__ __forceinline__ V3 closest_on_tri(V3 p, V3 a, V3 b, V3 c, bool& face) {
+  face = false;
+  const V3 ab = b - a, ac = c - a, ap = p - a;
+  const float d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) return a;
+  const V3 bp = p - b;
+  const float d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) return b;
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + (d1 / (d1 - d3)) * ab;
+  const V3 cp = p - c;
+  const float d5 = dot(ab, cp), d6 = dot(ac, cp);
+  if (d6 >= 0.f && d5 <= d6) return c;
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + (d2 / (d2 - d6)) * ac;
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + ((d4 - d3) / ((d4 - d3) + (d5 - d6))) * (c - b);
+  face = true;
+  const float dn = 1.f / (va + vb + vc);
+  return a + (vb * dn) * ab + (vc * dn) * ac;
+}
+__device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, float margin) {
+  THit h;
+  h.sep = 1e30f;
+  h.n = v3(0.f, 0.f, 1.f);
+  const int R = K->terr_rows, Cn = K->terr_cols;
+  const float bs = K->p.border_size, ih = K->terr_inv_hs;
+  const int ci = min(max((int)floorf((p.x + bs) * ih), 0), R - 2);
+  const int cj = min(max((int)floorf((p.y + bs) * ih), 0), Cn - 2);
+  if (p.z - r - margin > K->terr_hmax[ci * Cn + cj]) return h;
+  const float* __restrict__ vtx = K->terr_vtx;
+  float best = 3.0e38f;
+  V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
+  bool bface = true;
+  for (int i = max(ci - 1, 0); i <= min(ci + 1, R - 2); ++i) {
+    for (int j = max(cj - 1, 0); j <= min(cj + 1, Cn - 2); ++j) {
+      const int i0 = i * Cn + j;
+      const V3 va = terr_v(vtx, i0), vb = terr_v(vtx, i0 + 1), vc = terr_v(vtx, i0 + Cn), vd = terr_v(vtx, i0 + Cn + 1);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        // triangles of convert_heightfield_to_trimesh: (v(i,j), v(i+1,j+1), v(i,j+1)), (v(i,j), v(i+1,j), v(i+1,j+1))
+        const V3 b = t == 0 ? vd : vc, c = t == 0 ? vb : vd;
+        const V3 nf = cross(b - va, c - va);
+        const float a2 = dot(nf, nf);
+        if (a2 < 1e-12f) continue;  // collapsed by the slope correction
+        bool face;
+        const V3 q = closest_on_tri(p, va, b, c, face);
+        const V3 dq = p - q;
+        const float d2 = dot(dq, dq);
+        if (d2 < best) {
+          best = d2;
+          bc = q;
+          bn = rsqrtf(a2) * nf;
+          ba = va;
+          bface = face;
+        }
+      }
+    }
+  }
+  const float dist = sqrtf(best), sd = dot(bn, p - ba);
+  if (!bface && dist > 1e-6f && sd > 0.f) {
+    h.n = (1.f / dist) * (p - bc);
+    h.sep = dist - r;
+  } else {
+    h.n = bn;
+    h.sep = sd - r;
+  }
+  return h;
+}
+// tangents of a contact normal: t1 = x (or y when n is close to x) made orthogonal to n, t2 = n x t1
+__device__ __forceinline__ void contact_frame(V3 n, V3& t1, V3& t2) {
+  const V3 t = fabsf(n.x) < 0.9f ? v3(1.f - n.x * n.x, -n.x * n.y, -n.x * n.z) : v3(-n.y * n.x, 1.f - n.y * n.y, -n.y * n.z);
+  t1 = rsqrtf(dot(t, t)) * t;
+  t2 = cross(n, t1);
+}
+
 // Contact-row field map (NSF floats per sphere, LDS [field][env slot]):
 //   0..2 contact point x (base frame)   3 1/W_nn   4 W_t1n   5 W_t2n   6..8 (W_tt)^-1 (11, 12, 22)
 //   9 velocity target   10..12 impulse (n, t1, t2)
@@ -308,15 +402,33 @@ __device__ __forceinline__ void apply_impulse(const Lds& M, int s, int lsel, flo
 }
 
 // One contact sphere's solver rows: g_d, h_d, z_d, e_d and the 3x3 Delassus block W_de = g_d . z_e + h_d . e_e
+// Terrain contacts (TERR): detection leaves the world normal n in fields 3..5 (free until the Delassus values
+// land there); contact_setup builds the frame (n, t1, t2) from it and parks n in fields 0..2 (the contact point
+// is dead after the rows are built) for the contact-force pass.  Flat ground: n = z, t1 = x, t2 = y.
+template <bool TERR>
 __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, const M3& R, int s, int lsel, int link) {
   const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
   V3 c[3] = {v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f)};
   if (lsel >= 0) leg_dirs(M, lsel, link, x, c);
   float g[3][6], z[3][6];
   V3 h[3], ev[3];
+  V3 fr[3];  // contact frame in base coordinates
+  V3 nw = v3(0.f, 0.f, 1.f);
+  if constexpr (TERR) {
+    nw = v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5));
+    V3 t1, t2;
+    contact_frame(nw, t1, t2);
+    fr[0] = mulT(R, nw);
+    fr[1] = mulT(R, t1);
+    fr[2] = mulT(R, t2);
+  } else {
+    fr[0] = v3(R.m[6], R.m[7], R.m[8]);
+    fr[1] = v3(R.m[0], R.m[1], R.m[2]);
+    fr[2] = v3(R.m[3], R.m[4], R.m[5]);
+  }
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const V3 nd = d == 0 ? v3(R.m[6], R.m[7], R.m[8]) : d == 1 ? v3(R.m[0], R.m[1], R.m[2]) : v3(R.m[3], R.m[4], R.m[5]);
+    const V3 nd = fr[d];
     const V3 xn = cross(x, nd);
     g[d][0] = xn.x; g[d][1] = xn.y; g[d][2] = xn.z; g[d][3] = nd.x; g[d][4] = nd.y; g[d][5] = nd.z;
     h[d] = v3(dot(c[0], nd), dot(c[1], nd), dot(c[2], nd));
@@ -355,6 +467,11 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
   M.sph(s, 6) = W[2][2] * id;  // (W_tt)^-1: 11, 12, 22
   M.sph(s, 7) = -W[1][2] * id;
   M.sph(s, 8) = W[1][1] * id;
+  if constexpr (TERR) {
+    M.sph(s, 0) = nw.x;
+    M.sph(s, 1) = nw.y;
+    M.sph(s, 2) = nw.z;
+  }
 }
 
 // One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone).
@@ -446,6 +563,7 @@ __device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
   return l;
 }
 
+template <bool TERR>
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau3, float mb, const float* Ib, V3 cb,
                         float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
                         unsigned long long* prof) {
@@ -482,7 +600,20 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 
   // contact detection helper: separation, restitution/speculative target (needs nu at sub-step start)
   auto detect = [&](int s, V3 x, int lsel, int link) {
-    float sep = pz + dot(Rz, x) - K->sph_rad[s];
+    float sep;
+    V3 nb = Rz;  // contact normal in base coordinates
+    if constexpr (TERR) {
+      const THit th = terrain_query(K, v3(st.pos[0], st.pos[1], pz) + mul(R, x), K->sph_rad[s], P.contact_offset);
+      sep = th.sep;
+      if (sep < P.contact_offset) {
+        M.sph(s, 3) = th.n.x;
+        M.sph(s, 4) = th.n.y;
+        M.sph(s, 5) = th.n.z;
+        nb = mulT(R, th.n);
+      }
+    } else {
+      sep = pz + dot(Rz, x) - K->sph_rad[s];
+    }
     if (sep < P.contact_offset) {
       active |= (1ull << s);
       M.sph(s, 0) = x.x;
@@ -495,7 +626,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #pragma unroll
         for (int j = 0; j < 3; ++j) u = u + pick12(st.qd, 3 * lsel + j) * c[j];
       }
-      const float u0 = dot(Rz, u);
+      const float u0 = dot(nb, u);
       float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
       if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
       M.sph(s, 9) = tgt;
@@ -654,7 +785,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     if (m) {
       const int s = __builtin_ctzll(m);
       m &= m - 1ull;
-      contact_setup(M, Sch, R, s, sph_leg_of(SL, s), K->sph_link[s]);
+      contact_setup<TERR>(M, Sch, R, s, sph_leg_of(SL, s), K->sph_link[s]);
     }
   }
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
@@ -757,6 +888,28 @@ __device__ __forceinline__ V3 quat_rotate_inverse(const float* q, V3 v) {
 __device__ __forceinline__ float sq(float x) { return x * x; }
 __device__ __forceinline__ float nrm3(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
 
+// _get_heights for scan point k (legged_robot.py:1469-1503, quat_apply_yaw math_utils.py:12-16), in torch's
+// float32 op order: yaw-only quaternion normalised, rotated point + root position, + border, / horizontal
+// scale, truncation, clip to the sample grid, min of three samples (already in metres)
+__device__ __forceinline__ float height_sample(const KParams* __restrict__ K, const float* pos, const float* quat, int k) {
+  const lrl_env_params& P = K->p;
+  if (!P.terrain_mesh) return 0.f;  // plane: zeros (:1482-1483)
+  const float qz = quat[2], qw = quat[3];
+  const float nrm = fmaxf(sqrtf(qz * qz + qw * qw), 1e-9f);
+  const float z = qz / nrm, w = qw / nrm;
+  const float px = P.height_points[k][0], py = P.height_points[k][1];
+  const float t0 = (0.f * 0.f - z * py) * 2.f, t1 = (z * px - 0.f * 0.f) * 2.f;
+  const float rx = (px + w * t0) + (0.f * 0.f - z * t1);
+  const float ry = (py + w * t1) + (z * t0 - 0.f * 0.f);
+  float x = rx + pos[0], y = ry + pos[1];
+  x = (x + P.border_size) / P.horizontal_scale;
+  y = (y + P.border_size) / P.horizontal_scale;
+  const int R = K->terr_rows, Cn = K->terr_cols;
+  const int ix = min(max((int)x, 0), R - 2), iy = min(max((int)y, 0), Cn - 2);
+  const float* __restrict__ H = K->terr_h;
+  return fminf(fminf(H[ix * Cn + iy], H[(ix + 1) * Cn + iy]), H[ix * Cn + iy + 1]);
+}
+
 // ------------------------------------------------------------------------------------------------
 // the fused step kernel
 // ------------------------------------------------------------------------------------------------
@@ -818,6 +971,7 @@ __device__ __forceinline__ void priv_row(const lrl_env_params& P, const KState& 
   for (int i = 0; i < LRL_NUM_PRIV; ++i) pr[i] = fminf(fmaxf(pr[i], -P.clip_obs), P.clip_obs);
 }
 
+template <bool TERR>
 __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
                                                         const float* __restrict__ actions_in, uint32_t flags,
                                                         int64_t step_counter) {
@@ -899,7 +1053,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
       tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
     }
     LRL_PROF(8)  // PD torques
-    if (physics) substep(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, prof);
+    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, prof);
 #ifdef LRL_ENV_PROFILE
     prof_t = clock64();
 #endif
@@ -943,9 +1097,19 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
     if (physics) {
       for (int s = K->body_sph_begin[b]; s < K->body_sph_end[b]; ++s)
         if ((active >> s) & 1ull) {
-          fx += M.sph(s, 11);
-          fy += M.sph(s, 12);
-          fz += M.sph(s, 10);
+          if constexpr (TERR) {  // impulse (n, t1, t2) in the sphere's contact frame -> world
+            const V3 nw = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
+            V3 t1, t2;
+            contact_frame(nw, t1, t2);
+            const float ln = M.sph(s, 10), l1 = M.sph(s, 11), l2 = M.sph(s, 12);
+            fx += ln * nw.x + l1 * t1.x + l2 * t2.x;
+            fy += ln * nw.y + l1 * t1.y + l2 * t2.y;
+            fz += ln * nw.z + l1 * t1.z + l2 * t2.z;
+          } else {
+            fx += M.sph(s, 11);
+            fy += M.sph(s, 12);
+            fz += M.sph(s, 10);
+          }
         }
       fx *= inv_dt;
       fy *= inv_dt;
@@ -978,6 +1142,29 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   const int NO = P.num_obs;
   float* otile = lds;                    // [ENVS][NO]
   float* ptile = lds + ENVS * NO;        // [ENVS][18]
+  // _teleport_robots (legged_robot.py:768-791), in every lane of the env (the height scan below needs it)
+  if (P.teleport) {
+    float th = P.teleport_thresh;
+    float xo = (float)(int)(e < P.num_train_envs ? P.teleport_x_offset : P.teleport_x_offset_eval);
+    if (st.pos[0] < th + xo) st.pos[0] += P.terrain_length * (float)(P.terrain_rows - 1);
+    if (st.pos[0] > P.terrain_length * (float)P.terrain_rows - th + xo) st.pos[0] -= P.terrain_length * (float)(P.terrain_rows - 1);
+    if (st.pos[1] < th) st.pos[1] += P.terrain_width * (float)(P.terrain_cols - 1);
+    if (st.pos[1] > P.terrain_width * (float)P.terrain_cols - th) st.pos[1] -= P.terrain_width * (float)(P.terrain_cols - 1);
+  }
+  // _get_heights (legged_robot.py:1469-1503) after the teleport (:575-585): the scan points spread over the
+  // env's 4 lanes, written to measured_heights and to the height entries of the obs row (:386-389)
+  float hsum = 0.f;
+  if (P.measure_heights) {
+    const int NP = P.num_height_points, NB = NO - NP;
+    float* orow = otile + es * NO + NB;
+    for (int k = ql; k < NP; k += QL) {
+      const float hk = height_sample(K, st.pos, st.quat, k);
+      if (valid) S.heights[k * N + e] = hk;
+      hsum += st.pos[2] - hk;
+      orow[k] = fminf(fmaxf(st.pos[2] - 0.5f - hk, -1.f), 1.f) * P.obs_scale_height;
+    }
+    hsum = quad_sum(hsum);
+  }
   // post-physics, observations and the state write-back: lane 0 of each env
   if (ql == 0) {
 
@@ -987,13 +1174,6 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   V3 blv = quat_rotate_inverse(quat, v3(st.V[0], st.V[1], st.V[2]));
   V3 bav = quat_rotate_inverse(quat, v3(st.W[0], st.W[1], st.W[2]));
   V3 pg = quat_rotate_inverse(quat, v3(0.f, 0.f, -1.f));
-  if (P.teleport) {
-    float th = P.teleport_thresh, xo = (float)(int)P.teleport_x_offset;
-    if (st.pos[0] < th + xo) st.pos[0] += P.terrain_length * (float)(P.terrain_rows - 1);
-    if (st.pos[0] > P.terrain_length * (float)P.terrain_rows - th + xo) st.pos[0] -= P.terrain_length * (float)(P.terrain_rows - 1);
-    if (st.pos[1] < th) st.pos[1] += P.terrain_width * (float)(P.terrain_cols - 1);
-    if (st.pos[1] > P.terrain_width * (float)P.terrain_cols - th) st.pos[1] -= P.terrain_width * (float)(P.terrain_cols - 1);
-  }
   const bool inject = flags & LRL_STEP_INJECT_UNIFORM;
   float ms_e[12];
 #pragma unroll
@@ -1042,7 +1222,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
       case LRL_R_LIN_VEL_Z: r = sq(blv.z); break;
       case LRL_R_ANG_VEL_XY: r = sq(bav.x) + sq(bav.y); break;
       case LRL_R_ORIENTATION: r = sq(pg.x) + sq(pg.y); break;
-      case LRL_R_BASE_HEIGHT: r = sq(st.pos[2] - P.base_height_target); break;
+      case LRL_R_BASE_HEIGHT:  // mean(z - measured_heights) (:1518-1521); measured_heights = 0 without a scan
+        r = sq((P.measure_heights ? hsum / (float)P.num_height_points : st.pos[2]) - P.base_height_target);
+        break;
       case LRL_R_TORQUES:
 #pragma unroll
         for (int j = 0; j < 12; ++j) r += sq(tau[j]);
@@ -1290,7 +1472,11 @@ extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
 }
 
 extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
-  return hipFuncSetAttribute((const void*)lrl::env_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  hipError_t e = hipFuncSetAttribute((const void*)lrl::env_step_kernel<false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)lrl::env_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             lds_bytes);
 }
 
 namespace lrl {
@@ -1332,6 +1518,12 @@ __global__ void observe_kernel(const KParams* __restrict__ K, KState S, const in
   S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
   float* ob = S.obs + (size_t)e * NO;
   obs_values(P, blv, bav, pg, cmd, q, qd, act, ob);
+  if (P.measure_heights) {  // the step's measured_heights (taken before the reset) against the new base height
+    const int NP = P.num_height_points, NB = NO - NP;
+    const float z = S.root[2 * N + e];
+    for (int k = 0; k < NP; ++k)
+      ob[NB + k] = fminf(fmaxf(z - 0.5f - S.heights[k * N + e], -1.f), 1.f) * P.obs_scale_height;
+  }
   obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, ob, 0, 1);
   priv_row(P, S, e, S.payload[e], v3(S.com[e], S.com[N + e], S.com[2 * N + e]), ms, S.priv + (size_t)e * LRL_NUM_PRIV);
   if (flags & LRL_STEP_HISTORY) {
@@ -1353,10 +1545,14 @@ __global__ void observe_kernel(const KParams* __restrict__ K, KState S, const in
 }  // namespace lrl
 
 extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int lds_bytes, const float* actions,
-                                          uint32_t flags, int64_t step_counter, hipStream_t stream) {
+                                          uint32_t flags, int64_t step_counter, int terrain_mesh, hipStream_t stream) {
   int blocks = S->stride / ENVS;
-  hipLaunchKernelGGL(lrl::env_step_kernel, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
-                     step_counter);
+  if (terrain_mesh)
+    hipLaunchKernelGGL(lrl::env_step_kernel<true>, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
+                       step_counter);
+  else
+    hipLaunchKernelGGL(lrl::env_step_kernel<false>, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions,
+                       flags, step_counter);
   return hipGetLastError();
 }
 

@@ -30,6 +30,14 @@ struct KParams {
   int32_t body_foot[LRL_MAX_BODIES];  // foot slot 0..3 or -1
   int32_t num_history;
   int32_t n_es, n_cs;                 // rows of episode_sums / command_sums
+  // terrain mesh (p.terrain_mesh == 1, lrl_sim_set_terrain): vertex grid [rows][cols] as (x, y, z, 0) in the
+  // world frame, the max vertex z over the 4x4 vertices a contact query at cell (i, j) reads, and the height
+  // samples in metres for the height scan
+  const float* terr_vtx;
+  const float* terr_hmax;
+  const float* terr_h;
+  int32_t terr_rows, terr_cols;
+  float terr_inv_hs;
 };
 
 // SoA device buffers of a sim (each [.][N] with N = padded env count unless noted).
@@ -44,5 +52,6 @@ struct KState {
   int32_t* episode_length;
   float *episode_sums, *command_sums, *feet_air_time, *friction, *restitution, *payload, *com, *motor_strength,
       *kp, *kd, *env_origins, *base_lin_vel, *base_ang_vel, *projected_gravity, *joint_pos_target;
+  float* heights;  // measured_heights [num_height_points][N]
   const float *inj_noise, *inj_dr;
 };

@@ -10,7 +10,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # LRL_LIB overrides the library path (instrumented development builds); the default is the in-tree build
 LIB_PATH = os.environ.get("LRL_LIB") or os.path.join(os.path.dirname(_HERE), "csrc", "liblrl.so")
 
-MAX_BODIES, MAX_SPHERES, NUM_DOF, NUM_LEGS, MAX_OBS, MAX_REWARD_TERMS, NUM_PRIV = 20, 40, 12, 4, 64, 24, 18
+MAX_BODIES, MAX_SPHERES, NUM_DOF, NUM_LEGS, MAX_OBS, MAX_REWARD_TERMS, NUM_PRIV = 20, 40, 12, 4, 256, 24, 18
+MAX_HEIGHT_POINTS = 192
 f32, i32, u32 = C.c_float, C.c_int32, C.c_uint32
 
 REWARD_TERMS = ["lin_vel_z", "ang_vel_xy", "orientation", "base_height", "torques", "energy",
@@ -24,7 +25,7 @@ STEP_PHYSICS, STEP_HISTORY, STEP_INJECT_UNIFORM = 1, 2, 4
  T_LAST_DOF_VEL, T_LAST_ROOT_VEL, T_COMMANDS, T_OBS, T_PRIV_OBS, T_OBS_HISTORY, T_REWARD, T_RESET, T_TIME_OUT,
  T_EPISODE_LENGTH, T_EPISODE_SUMS, T_COMMAND_SUMS, T_FEET_AIR_TIME, T_LAST_CONTACTS, T_FRICTION, T_RESTITUTION,
  T_PAYLOAD, T_COM_DISPLACEMENT, T_MOTOR_STRENGTH, T_KP_FACTOR, T_KD_FACTOR, T_ENV_ORIGINS, T_BASE_LIN_VEL,
- T_BASE_ANG_VEL, T_PROJECTED_GRAVITY, T_JOINT_POS_TARGET, T_NUM) = range(35)
+ T_BASE_ANG_VEL, T_PROJECTED_GRAVITY, T_JOINT_POS_TARGET, T_MEASURED_HEIGHTS, T_NUM) = range(36)
 
 
 class LrlModel(C.Structure):
@@ -67,6 +68,9 @@ class LrlEnvParams(C.Structure):
         ("teleport", i32), ("teleport_thresh", f32), ("teleport_x_offset", f32), ("terrain_length", f32),
         ("terrain_width", f32), ("terrain_rows", i32), ("terrain_cols", i32),
         ("base_init_state", f32 * 13), ("num_history", i32), ("auto_reset", i32), ("max_episode_length", i32),
+        ("terrain_mesh", i32), ("border_size", f32), ("horizontal_scale", f32), ("vertical_scale", f32),
+        ("measure_heights", i32), ("num_height_points", i32), ("height_points", f32 * 2 * MAX_HEIGHT_POINTS),
+        ("obs_scale_height", f32), ("num_train_envs", i32), ("teleport_x_offset_eval", f32),
     ]
 
 
@@ -142,7 +146,7 @@ def lib():
                      "lrl_ppo_act", "lrl_abi_version", "lrl_device_count", "lrl_gae_partial", "lrl_adv_normalize",
                      "lrl_sim_reset_idx_ex", "lrl_sim_observe_idx", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
-                     "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student"]:
+                     "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student", "lrl_sim_set_terrain"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_ppo_workspace_bytes.restype = C.c_int64
         L.lrl_ppo_act_workspace_bytes.restype = C.c_int64

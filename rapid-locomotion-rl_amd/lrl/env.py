@@ -24,6 +24,7 @@ from . import params as lparams
 from .config import Section
 from .curriculum import RewardThresholdCurriculum
 from .robot import load_robot
+from .terrain import Terrain, convert_heightfield_to_trimesh
 
 MINI_GYM_ROOT_DIR = "/root/reference"  # only used to format Cfg.asset.file; tables ship in lrl/robots
 
@@ -98,17 +99,22 @@ class LeggedRobotEnv:
         self.dof_names = self.robot["dof_names"]
         self.body_names = self.robot["body_names"]
         self.custom_origins = cfg.terrain.mesh_type in ("heightfield", "trimesh")
+        self.terrain = None
+        terrain_mesh = 0
         if self.custom_origins:
-            self._flat_terrain()
+            terrain_mesh = self._create_terrain()
         self._P = lparams.build_params(cfg, self.robot, auto_reset=not self.legacy_fork,
-                                       solver_iterations=solver_iterations)
+                                       solver_iterations=solver_iterations, terrain_mesh=terrain_mesh)
         if eval_cfg is not None:
             # one kernel parameter block serves both groups: the eval cfg may differ from the train cfg only in
             # what the host applies per group (command ranges / curriculum, reset logging)
-            if eval_cfg.terrain.mesh_type in ("heightfield", "trimesh"):
-                eval_cfg.terrain.x_offset = 0  # flat-terrain bookkeeping, as for the train cfg
             Pe = lparams.build_params(eval_cfg, self.robot, auto_reset=not self.legacy_fork,
-                                      solver_iterations=solver_iterations)
+                                      solver_iterations=solver_iterations, terrain_mesh=terrain_mesh)
+            # the eval tiles' teleport x offset is the one per-group kernel parameter
+            self._P.num_train_envs = self.num_train_envs
+            self._P.teleport_x_offset_eval = Pe.teleport_x_offset
+            Pe.teleport_x_offset, Pe.teleport_x_offset_eval = self._P.teleport_x_offset, Pe.teleport_x_offset
+            Pe.num_train_envs = self._P.num_train_envs
             def differs(f):
                 a, b = getattr(self._P, f), getattr(Pe, f)
                 return bytes(a) != bytes(b) if isinstance(a, C.Array) else a != b
@@ -138,6 +144,19 @@ class LeggedRobotEnv:
                                     C.c_int64(env_offset), C.c_uint64(self.seed), C.c_int32(dev_index),
                                     C.byref(self._sim)))
         self._dev_index = dev_index
+        if terrain_mesh:  # gym.add_triangle_mesh / add_heightfield (legged_robot.py:1122-1160)
+            t = self.terrain
+            if cfg.terrain.mesh_type == "trimesh":
+                vtx = t.vertices
+            else:  # PhysX height field: the unmoved grid
+                vtx, _ = convert_heightfield_to_trimesh(t.height_field_raw, cfg.terrain.horizontal_scale,
+                                                        cfg.terrain.vertical_scale, None)
+            vtx = np.ascontiguousarray(vtx, np.float32)
+            hs = np.ascontiguousarray(t.heightsamples, np.int16)
+            _abi.check(L.lrl_sim_set_terrain(self._sim, vtx.ctypes.data_as(C.c_void_p), hs.ctypes.data_as(C.c_void_p),
+                                             C.c_int32(hs.shape[0]), C.c_int32(hs.shape[1])))
+        self.height_samples = (torch.tensor(self.terrain.heightsamples).to(self.device)
+                               if self.terrain is not None else None)
         T = self._tensor
         self.root_states = self.all_root_states = T(_abi.T_ROOT_STATE)
         self.dof_pos = T(_abi.T_DOF_POS)
@@ -189,7 +208,11 @@ class LeggedRobotEnv:
                                            torch.tensor(self._P.soft_dof_pos_upper[:])], 1).to(self.device)
         self.base_init_state = torch.tensor(self._P.base_init_state[:], device=self.device)
         self.default_body_mass = self.robot["base_mass"]
-        self.measured_heights = 0
+        # _get_heights runs inside the step kernel (legged_robot.py:584-585); 0 without a scan (:979)
+        self.measured_heights = T(_abi.T_MEASURED_HEIGHTS) if cfg.terrain.measure_heights else 0
+        if cfg.terrain.measure_heights:
+            self.height_points = torch.zeros(self.num_envs, len(lparams.height_points(cfg)), 3, device=self.device)
+            self.height_points[:, :, :2] = torch.tensor(lparams.height_points(cfg), device=self.device)
         self.common_step_counter = 0
         self.extras = _LazyExtras(self)
         self.record_now = False
@@ -215,6 +238,7 @@ class LeggedRobotEnv:
         self._init_command_distribution()
         self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
         self._ids_all = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
+        self.init_done = True
 
     # -------------------------------------------------------------------------------- plumbing
     def _tensor(self, tid):
@@ -250,34 +274,50 @@ class LeggedRobotEnv:
         return self._last_contacts_u8.bool()
 
     # -------------------------------------------------------------------------------- terrain
-    def _flat_terrain(self):
-        """Terrain bookkeeping for the flat trimesh the Mini Cheetah preset uses (terrain.py:12-184 with
-        terrain_noise_magnitude 0: every sub-terrain is flat at z = 0)."""
-        t = self.cfg.terrain
-        if any(p > 0 for p in t.terrain_proportions[:8]) or t.terrain_noise_magnitude != 0:
-            raise NotImplementedError("rough terrain generation is a next-row item (SURVEY.md §8(f) rank 1)")
-        t.x_offset = 0
-        t.rows_offset = 0
-        t.env_length, t.env_width = t.terrain_length, t.terrain_width
-        origins = np.zeros((t.num_rows, t.num_cols, 3))
-        for i in range(t.num_rows):
-            for j in range(t.num_cols):
-                origins[i, j] = [(i + 0.5) * t.terrain_length, (j + 0.5) * t.terrain_width, 0.0]
-        t.env_origins = origins
+    def _create_terrain(self):
+        """create_sim's terrain (legged_robot.py:426-441): the Terrain tiles of the train cfg (and the eval cfg's
+        tiles below them), generated with numpy's global RNG seeded by the env seed so every rank builds the
+        same map.  Returns 1 when the ground is a mesh (some height is non-zero), 0 when it is the plane z = 0
+        (the Mini Cheetah preset's all-flat trimesh), which keeps the plane contact path."""
+        et = self.eval_cfg.terrain if self.eval_cfg is not None else None
+        state = np.random.get_state()
+        np.random.seed(self.seed)
+        try:
+            self.terrain = Terrain(self.cfg.terrain, self.num_train_envs, et, self.num_eval_envs)
+        finally:
+            np.random.set_state(state)
+        return int(np.any(self.terrain.height_field_raw != 0))
+
+    def _groups(self, env_ids=None):
+        """_call_train_eval (legged_robot.py:456-469): (ids, cfg) of the train and eval envs among env_ids."""
+        ids = torch.arange(self.num_envs, device=self.device) if env_ids is None else env_ids
+        out = [(ids[ids < self.num_train_envs], self.cfg)]
+        if self.eval_cfg is not None:
+            out.append((ids[ids >= self.num_train_envs], self.eval_cfg))
+        return [(i, c) for i, c in out if len(i)]
 
     def _set_env_origins(self):
-        """legged_robot.py:1385-1415"""
+        """_get_env_origins (legged_robot.py:1385-1415), per train / eval group"""
         cfg, n = self.cfg, self.num_envs
         if self.custom_origins:
-            t = cfg.terrain
-            max_l = t.num_rows - 1 if not t.curriculum else t.max_init_terrain_level
-            min_l = 0 if not t.curriculum else t.min_init_terrain_level
             g = torch.Generator().manual_seed(self.seed)
-            self.terrain_levels = torch.randint(min_l, max_l + 1, (n,), generator=g).to(self.device)
-            self.terrain_types = torch.div(torch.arange(n), (n / t.num_cols), rounding_mode="floor").long().to(self.device)
-            t.max_terrain_level = t.num_rows
-            t.terrain_origins = torch.from_numpy(t.env_origins).to(self.device).float()
-            self.env_origins[:] = t.terrain_origins[self.terrain_levels, self.terrain_types]
+            self.terrain_levels = torch.zeros(n, dtype=torch.long, device=self.device)
+            self.terrain_types = torch.zeros(n, dtype=torch.long, device=self.device)
+            for ids, c in self._groups():
+                t = c.terrain
+                max_l = t.num_rows - 1 if not t.curriculum else t.max_init_terrain_level
+                min_l = 0 if not t.curriculum else t.min_init_terrain_level
+                if not 0 <= min_l <= max_l < t.num_rows:  # the reference would index terrain_origins out of range
+                    raise IndexError(f"initial terrain levels [{min_l}, {max_l}] outside the {t.num_rows} terrain rows "
+                                     "(Cfg.terrain.max_init_terrain_level)")
+                k = len(ids)
+                self.terrain_levels[ids] = torch.randint(min_l, max_l + 1, (k,), generator=g).to(self.device)
+                self.terrain_types[ids] = torch.div(torch.arange(k), (k / t.num_cols),
+                                                    rounding_mode="floor").long().to(self.device)
+                t.max_terrain_level = t.num_rows
+                t.terrain_origins = torch.from_numpy(t.env_origins).to(self.device).float()
+                self.env_origins[ids] = t.terrain_origins[self.terrain_levels[ids], self.terrain_types[ids]]
+            self._level_gen = torch.Generator(device=self.device).manual_seed(self.seed + 1)
         else:
             num_cols = np.floor(np.sqrt(n))
             num_rows = np.ceil(n / num_cols)
@@ -395,6 +435,9 @@ class LeggedRobotEnv:
             tr, ev = env_ids[env_ids < n_tr], env_ids[env_ids >= n_tr]
         else:
             tr, ev = env_ids, env_ids[:0]
+        if self.custom_origins:
+            for ids, c in self._groups(env_ids):
+                self._update_terrain_curriculum(ids, c)
         if len(tr):
             self.update_command_curriculum(tr, self.cfg)
         if len(ev):
@@ -426,12 +469,34 @@ class LeggedRobotEnv:
         ep = self.extras.get("train/episode")
         if ep is None:
             ep = self.extras["train/episode"] = {}
+        if self.cfg.terrain.curriculum:  # :278-280
+            ep["terrain_level"] = torch.mean(self.terrain_levels[:self.num_train_envs].float())
         if self.cfg.commands.command_curriculum:
             self.env_command_bins_t = torch.tensor(self.env_command_bins, dtype=torch.float, device=self.device)
             self.extras["env_bins"] = self.env_command_bins_t[:self.num_train_envs]
             ep["command_area"] = np.sum(self.curriculum.weights) / self.curriculum.weights.shape[0]
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self.time_out_buf[:self.num_train_envs]
+
+    def _rand_levels(self, like, high):
+        """torch.randint_like(levels, high) of _update_terrain_curriculum (seeded device generator here;
+        tests replace it to inject the reference's draws)."""
+        return torch.randint(0, high, like.shape, generator=self._level_gen, device=self.device, dtype=like.dtype)
+
+    def _update_terrain_curriculum(self, env_ids, cfg):
+        """legged_robot.py:793-818: robots that walked past half a tile move a level up, those that covered less
+        than half of their commanded distance move down (not both); past the last level a random level."""
+        if not cfg.terrain.curriculum or not getattr(self, "init_done", False):
+            return
+        t = cfg.terrain
+        distance = torch.norm(self.root_states[env_ids, :2] - self.env_origins[env_ids, :2], dim=1)
+        move_up = distance > t.env_length / 2
+        move_down = (distance < torch.norm(self.commands[env_ids, :2], dim=1) * cfg.env.episode_length_s * 0.5) * ~move_up
+        self.terrain_levels[env_ids] += 1 * move_up - 1 * move_down
+        lv = self.terrain_levels[env_ids]
+        self.terrain_levels[env_ids] = torch.where(lv >= t.max_terrain_level, self._rand_levels(lv, t.max_terrain_level),
+                                                   torch.clip(lv, 0))
+        self.env_origins[env_ids] = t.terrain_origins[self.terrain_levels[env_ids], self.terrain_types[env_ids]]
 
     def update_command_curriculum(self, env_ids, cfg, episode_sums=None):
         """_update_command_curriculum_uniform (legged_robot.py:851-880)."""

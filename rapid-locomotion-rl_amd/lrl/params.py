@@ -59,7 +59,17 @@ def noise_vec(cfg):
     if cfg.env.observe_command:
         parts += [0.0] * 3
     parts += [ns.dof_pos * lvl * s.dof_pos] * 12 + [ns.dof_vel * lvl * s.dof_vel] * 12 + [0.0] * 12
+    if cfg.terrain.measure_heights:  # :924-927
+        parts += [ns.height_measurements * lvl * s.height_measurements] * len(height_points(cfg))
     return np.array(parts, np.float32)
+
+
+def height_points(cfg):
+    """_init_height_points (legged_robot.py:1453-1467): meshgrid(x, y) ('ij'), flattened -> [(x, y)]."""
+    t = cfg.terrain
+    gx, gy = np.meshgrid(np.array(t.measured_points_x, np.float32), np.array(t.measured_points_y, np.float32),
+                         indexing="ij")
+    return np.stack([gx.ravel(), gy.ravel()], -1)
 
 
 def build_model(robot):
@@ -85,7 +95,9 @@ def body_sets(cfg, robot):
     return feet, pen, term
 
 
-def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte=0.2):
+def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte=0.2, terrain_mesh=0):
+    """terrain_mesh: 1 when the sim collides with a generated height field / trimesh (lrl_sim_set_terrain),
+    0 for the plane z = 0 (mesh_type 'plane', or a trimesh whose heights are all zero)."""
     dt = derived(cfg)
     P = _abi.LrlEnvParams()
     dof_names = robot["dof_names"]
@@ -129,8 +141,13 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
     for flag in ("observe_only_ang_vel", "observe_only_lin_vel", "observe_yaw"):
         if getattr(cfg.env, flag):
             raise ValueError(f"Cfg.env.{flag} is not implemented by the fused kernel")
-    if cfg.terrain.measure_heights:
-        raise ValueError("height measurements (rough terrain) are not implemented yet")
+    mt = cfg.terrain.mesh_type
+    if cfg.terrain.measure_heights and mt == "none":
+        raise NameError("Can't measure height with terrain mesh type 'none'")  # :1484-1485
+    hp = height_points(cfg) if cfg.terrain.measure_heights else np.zeros((0, 2), np.float32)
+    if len(hp) > _abi.MAX_HEIGHT_POINTS:
+        raise ValueError(f"{len(hp)} height points exceed liblrl's {_abi.MAX_HEIGHT_POINTS}")
+    cfg.env.num_height_points = len(hp)
     if cfg.control.control_type != "P":
         raise ValueError("only control_type 'P' is implemented")
     if cfg.domain_rand.push_robots:  # off in config_mini_cheetah / config_go1 (mini_cheetah_config.py:90)
@@ -181,5 +198,10 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         terrain_rows=cfg.terrain.num_rows, terrain_cols=cfg.terrain.num_cols, base_init_state=init,
         num_history=cfg.env.num_observation_history, auto_reset=int(auto_reset),
         max_episode_length=int(cfg.env.max_episode_length),
+        terrain_mesh=int(terrain_mesh), border_size=cfg.terrain.border_size,
+        horizontal_scale=cfg.terrain.horizontal_scale, vertical_scale=cfg.terrain.vertical_scale,
+        measure_heights=int(cfg.terrain.measure_heights), num_height_points=len(hp),
+        height_points=hp.tolist(), obs_scale_height=s.height_measurements, num_train_envs=2 ** 30,
+        teleport_x_offset_eval=float(getattr(cfg.terrain, "x_offset", 0)) * cfg.terrain.horizontal_scale,
     )
     return P

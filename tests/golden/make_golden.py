@@ -133,9 +133,11 @@ URDF_LIMITS = {
 }
 
 
-def make_env(robot, n, seed):
+def make_env(robot, n, seed, tweak=None):
     rng = np.random.default_rng(seed)
     cfg = fresh_cfg(robot)
+    if tweak is not None:
+        tweak(cfg)
     env = object.__new__(LeggedRobot)
     env.cfg = cfg
     env.eval_cfg = None
@@ -586,8 +588,106 @@ def gen_terrain():
     print("terrain:", {k: v.shape for k, v in out.items()})
 
 
+def _ref_terrain(seed=3):
+    """A small curriculum terrain (3 levels x 10 types, 2 m border) built by the reference's Terrain class."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "rapid-locomotion-rl_amd"))
+    from lrl import terrain as ours
+    tu = sys.modules["isaacgym.terrain_utils"]
+    for k in ("SubTerrain", "random_uniform_terrain", "pyramid_sloped_terrain", "pyramid_stairs_terrain",
+              "discrete_obstacles_terrain", "stepping_stones_terrain", "convert_heightfield_to_trimesh"):
+        setattr(tu, k, getattr(ours, k))
+    from mini_gym.utils.terrain import Terrain
+    np.random.seed(seed)
+    c = _terrain_cfg()
+    return Terrain(c, 64), c
+
+
+def _rough_tweak(cfg):
+    cfg.terrain.mesh_type = "trimesh"
+    cfg.terrain.measure_heights = True
+    cfg.terrain.curriculum = True
+    cfg.env.num_height_points = len(cfg.terrain.measured_points_x) * len(cfg.terrain.measured_points_y)
+    cfg.env.num_observations = 42 + cfg.env.num_height_points
+
+
+def gen_heights(n=96, seed=11):
+    """_get_heights (legged_robot.py:1469-1503, quat_apply_yaw math_utils.py:12-16) and the height entries
+    of compute_observations (:386-389, noise :924-927) on the reference's Terrain, for random base poses
+    (some outside the map, to hit the index clipping)."""
+    t, tc = _ref_terrain()
+    env, rng = make_env("go1", n, seed, _rough_tweak)
+    env.terrain = t
+    rows, cols = t.heightsamples.shape
+    env.height_samples = torch.tensor(t.heightsamples).view(rows, cols)
+    env.height_points = env._init_height_points(torch.arange(n), env.cfg)
+    root = np.zeros((n, 13), np.float32)
+    root[:, 0] = rng.uniform(-tc.border_size - 1.0, rows * tc.horizontal_scale - tc.border_size + 1.0, n)
+    root[:, 1] = rng.uniform(-tc.border_size - 1.0, cols * tc.horizontal_scale - tc.border_size + 1.0, n)
+    root[:, 2] = rng.uniform(0.1, 0.8, n)
+    root[:, 3:7] = rand_quat(rng, n, tilt=3.0)
+    env.root_states[:] = torch.tensor(root)
+    env.base_quat[:] = env.root_states[:, 3:7]
+    heights = env._get_heights(torch.arange(n), env.cfg)
+    env.measured_heights = heights
+    env.projected_gravity = torch.zeros(n, 3)
+    noise_u = torch.tensor(rng.random((n, env.num_obs)), dtype=torch.float)
+    with InjectRand(noise_u, rng):
+        env.compute_observations()
+    out = dict(hf=t.heightsamples, border_size=np.array(tc.border_size), horizontal_scale=np.array(tc.horizontal_scale),
+               vertical_scale=np.array(tc.vertical_scale), root=root, heights=heights.numpy(),
+               obs_heights=env.obs_buf[:, 42:].numpy(), noise_u=noise_u.numpy(),
+               noise_vec=env.noise_scale_vec.numpy())
+    np.savez_compressed(os.path.join(HERE, "heights.npz"), **out)
+    print("heights:", {k: v.shape for k, v in out.items()})
+
+
+def gen_terrain_curriculum(n=64, seed=13):
+    """_update_terrain_curriculum (legged_robot.py:793-818) on the reference's terrain origins, with the
+    randint_like draws of envs past the last level injected and recorded."""
+    t, tc = _ref_terrain()
+    env, rng = make_env("go1", n, seed, _rough_tweak)
+    cfg = env.cfg
+    cfg.terrain.num_rows, cfg.terrain.num_cols = tc.num_rows, tc.num_cols
+    cfg.terrain.env_length = tc.env_length
+    cfg.terrain.max_terrain_level = tc.num_rows
+    cfg.terrain.terrain_origins = torch.from_numpy(tc.env_origins).to(torch.float)
+    env.terrain_levels = torch.tensor(rng.integers(0, tc.num_rows, n), dtype=torch.long)
+    env.terrain_levels[:6] = tc.num_rows - 1  # envs that will walk off the last level
+    env.terrain_types = torch.tensor(rng.integers(0, tc.num_cols, n), dtype=torch.long)
+    env.env_origins = cfg.terrain.terrain_origins[env.terrain_levels, env.terrain_types].clone()
+    disp = rng.uniform(-6.0, 6.0, (n, 2)).astype(np.float32)
+    disp[:6] = 5.0
+    env.root_states[:, :2] = env.env_origins[:, :2] + torch.tensor(disp)
+    env.commands[:, :2] = torch.tensor(rng.uniform(-0.6, 0.6, (n, 2)), dtype=torch.float)
+    env.commands[8:12, :2] = 0.0
+    levels_in, origins_in = env.terrain_levels.clone(), env.env_origins.clone()
+    ids = torch.tensor(np.sort(rng.choice(n, 40, replace=False)), dtype=torch.long)
+    ids[:6] = torch.arange(6)
+    draws = []
+    _ril = torch.randint_like
+
+    def randint_like(x, high):
+        d = torch.tensor(rng.integers(0, high, tuple(x.shape)), dtype=x.dtype)
+        draws.append(d.clone())
+        return d
+    torch.randint_like = randint_like
+    try:
+        env._update_terrain_curriculum(ids, cfg)
+    finally:
+        torch.randint_like = _ril
+    out = dict(origins_table=tc.env_origins.astype(np.float32), levels_in=levels_in.numpy(),
+               types=env.terrain_types.numpy(), env_origins_in=origins_in.numpy(),
+               root_xy=env.root_states[:, :2].numpy().copy(), commands_xy=env.commands[:, :2].numpy().copy(),
+               ids=ids.numpy(), draws=draws[0].numpy(), levels_out=env.terrain_levels.numpy(),
+               env_origins_out=env.env_origins.numpy(), env_length=np.array(tc.env_length),
+               episode_length_s=np.array(cfg.env.episode_length_s), num_rows=np.array(tc.num_rows))
+    np.savez_compressed(os.path.join(HERE, "terrain_curriculum.npz"), **out)
+    print("terrain_curriculum:", {k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     gens = dict(post_physics_mc=lambda: gen_post_physics("mc"), post_physics_go1=lambda: gen_post_physics("go1"),
-                curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint, terrain=gen_terrain)
+                curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint, terrain=gen_terrain,
+                heights=gen_heights, terrain_curriculum=gen_terrain_curriculum)
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()
