@@ -74,12 +74,47 @@ def cpu_baseline(seconds=12.0):
                        "the reference's Isaac Gym CPU pipeline is proprietary and absent (BASELINE.md §3)")
 
 
+def bench_go1_rough(dev, iters=3, warmup=1):
+    """Secondary line, BASELINE configs[2]: 4096 Go1 envs on the curriculum trimesh (stairs, slopes, obstacles,
+    stepping stones; terrain curriculum) with the upstream reset path (legacy_fork=False: time-outs, reset_idx
+    inside step, grid-adaptive command curriculum) — full PPO iterations, same timing rules as the headline."""
+    from lrl import config as lcfg
+    from lrl.env import LeggedRobotEnv
+    from lrl.history import HistoryWrapper
+    from lrl.ppo import runner as R
+    cfg = lcfg.make_cfg()
+    lcfg.config_go1(cfg)
+    cfg.env.num_envs = ENVS_PER_GPU
+    cfg.terrain.mesh_type = "trimesh"
+    cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]  # legged_robot_config.py:57
+    cfg.terrain.curriculum = True
+    env = HistoryWrapper(LeggedRobotEnv(dev, cfg=cfg, seed=4321, legacy_fork=False))
+    runner = R.Runner(env, device=dev, seed=4321)
+    runner.learn(warmup, init_at_random_ep_len=True)
+    timer = []
+    env.env.kernel_timer = timer
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.learn(iters)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    env.env.kernel_timer = None
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in timer]))
+    out = {"workload": "4096 Go1 envs, trimesh rough terrain (curriculum tiles) + terrain curriculum + upstream resets "
+                       "with the grid-adaptive command curriculum (BASELINE configs[2])",
+           "env_steps_per_s": round(ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env * iters / dt, 1),
+           "ppo_iters_per_s": round(iters / dt, 3), "env_step_kernel_ms": round(k_ms, 4), "steps": iters}
+    env.env.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the Go1 rough-terrain line (configs[2])")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -189,6 +224,9 @@ def main():
             "reference_context": {"upstream_example_run_env_steps_per_s": 41176, "upstream_ppo_iters_per_s": 0.429,
                                   "hardware": "unspecified NVIDIA GPU, 4000 envs (BASELINE.md §1)"},
         }
+        if world == 1 and not args.no_secondary:
+            env.env.close()
+            out["secondary"] = bench_go1_rough(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

@@ -27,6 +27,7 @@ GOLDEN_TERRAIN = {"terrain.num_rows": 3, "terrain.num_cols": 10, "terrain.terrai
 
 def _rough_cfg(n, border_size=2.0, **over):
     over = dict({"terrain.mesh_type": "trimesh", "terrain.measure_heights": True, "terrain.curriculum": True,
+                 "terrain.terrain_proportions": [0.1, 0.1, 0.35, 0.25, 0.2],  # legged_robot_config.py:57
                  "terrain.border_size": border_size, "terrain.teleport_robots": False,
                  "env.num_observations": 42 + 187}, **over)
     cfg = lcfg.make_cfg()
@@ -179,8 +180,12 @@ def test_rough_terrain_standing_and_curriculum():
     root = _np(env.root_states)
     assert np.isfinite(root).all()
     h = _np(env.measured_heights)
-    above = root[:, 2] - h.max(1)
-    assert np.mean(above > 0.05) > 0.9, np.sort(above)[:10]
+    centre = 8 * 11 + 5  # scan point (0, 0): meshgrid(x 17, y 11) 'ij' order
+    above = root[:, 2] - h[:, centre]
+    # supported by the mesh (no tunnelling): the base stays above the ground under it; robots dropped from the tile
+    # origin height (the tile's highest point, terrain.py:182-184) into pits may lie on their side
+    assert np.mean(above > 0.02) > 0.97, np.sort(above)[:10]
+    assert np.mean(above > 0.1) > 0.75, np.sort(above)[:10]
     lv0 = env.terrain_levels.clone()
     ids = torch.arange(0, n, 2, device="cuda:0")
     env.root_states[ids, 0] = env.env_origins[ids, 0] + 5.0  # walked more than env_length / 2
