@@ -221,6 +221,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   HIPCHECK(hipMemcpy(s->d_foot_xyz, model->foot_xyz, sizeof(float) * 12, hipMemcpyHostToDevice));
   // env step kernel LDS: 16 envs per workgroup (4 lanes each): leg blocks + contact rows, or the obs tiles
   int lds_contacts = (4 * 51 + model->num_spheres * 67) * 16 * 4;  // LEGF, NSF of lrl_env.hip
+  if (params->terrain_mesh) lds_contacts += 16 * 64 * 16;  // terrain query vertex block, float4 [16][64 lanes]
   int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * 16 * 4;  // obs / priv tiles + reward rows
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
   if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);
@@ -289,6 +290,20 @@ int32_t lrl_sim_set_terrain(lrl_sim* s, const float* vertices, const int16_t* he
     vtx[4 * v + 3] = 0.f;
     h[v] = (float)height_samples[v] * vs;  // torch: int16 tensor * python float -> float32
   }
+  // reach of the model: largest distance of a sphere surface from the base origin (chain of joint offsets)
+  const KParams& k = s->hk;
+  float reach = 0.f;
+  for (int q = 0; q < k.num_spheres; ++q) {
+    float d = sqrtf(k.sph_pos[q][0] * k.sph_pos[q][0] + k.sph_pos[q][1] * k.sph_pos[q][1] +
+                    k.sph_pos[q][2] * k.sph_pos[q][2]) + k.sph_rad[q];
+    const int l = k.sph_leg[q];
+    if (l >= 0)
+      for (int j = 0; j < 3; ++j)
+        d += sqrtf(k.leg[l].xyz[j][0] * k.leg[l].xyz[j][0] + k.leg[l].xyz[j][1] * k.leg[l].xyz[j][1] +
+                   k.leg[l].xyz[j][2] * k.leg[l].xyz[j][2]);
+    reach = fmaxf(reach, d);
+  }
+  const int W = (int)ceilf(reach / s->hk.p.horizontal_scale) + 2;
   // a query at cell (i, j) reads vertices [i-1, i+2] x [j-1, j+2]: separable max filter of the vertex z
   for (int i = 0; i < rows; ++i)
     for (int j = 0; j < cols; ++j) {
@@ -304,17 +319,36 @@ int32_t lrl_sim_set_terrain(lrl_sim* s, const float* vertices, const int16_t* he
         if (ii >= 0 && ii < rows) m = fmaxf(m, rowmax[(size_t)ii * cols + j]);
       hmax[(size_t)i * cols + j] = m;
     }
+  // window max around a base cell: [i-W, i+W] x [j-W, j+W] (terrain_window_max), two sliding passes
+  std::vector<float> wmax(nv);
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) {
+      float m = -3.0e38f;
+      for (int jj = (j - W > 0 ? j - W : 0); jj <= (j + W < cols - 1 ? j + W : cols - 1); ++jj)
+        m = fmaxf(m, vtx[4 * ((size_t)i * cols + jj) + 2]);
+      rowmax[(size_t)i * cols + j] = m;
+    }
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < cols; ++j) {
+      float m = -3.0e38f;
+      for (int ii = (i - W > 0 ? i - W : 0); ii <= (i + W < rows - 1 ? i + W : rows - 1); ++ii)
+        m = fmaxf(m, rowmax[(size_t)ii * cols + j]);
+      wmax[(size_t)i * cols + j] = m;
+    }
   HIPCHECK(hipSetDevice(s->device));
   (void)hipFree(s->terr);
   s->terr = nullptr;
-  const size_t bytes = nv * 4 * sizeof(float) + 2 * nv * sizeof(float);
+  const size_t bytes = nv * 4 * sizeof(float) + 3 * nv * sizeof(float);
   if (hipMalloc(&s->terr, bytes) != hipSuccess) return fail(LRL_E_NOMEM, "hipMalloc %zu bytes (terrain)", bytes);
   float* dv = (float*)s->terr;
   float* dmax = dv + 4 * nv;
   float* dh = dmax + nv;
+  float* dw = dh + nv;
   HIPCHECK(hipMemcpy(dv, vtx.data(), nv * 16, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(dmax, hmax.data(), nv * 4, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(dh, h.data(), nv * 4, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(dw, wmax.data(), nv * 4, hipMemcpyHostToDevice));
+  s->hk.terr_wmax = dw;
   s->hk.terr_vtx = dv;
   s->hk.terr_hmax = dmax;
   s->hk.terr_h = dh;

@@ -287,7 +287,9 @@ __device__ __forceinline__ V3 leg_qd(const Lds& M, int L, const float* vb) {
 // closest point is nearest wins (ties: first in cell order).  Inside its face region, or with p below its
 // plane, the contact normal is the face normal and the separation the signed plane distance minus r;
 // against an edge or vertex from outside, the normal points from the closest point to p and the separation
-// is the distance minus r.  A conservative max-height map skips the test for spheres clear of the terrain.
+// is the distance minus r.  Triangles whose xy bounding box, grown by r + contact_offset, does not hold p's xy
+// are skipped (part of the model: the oracle applies the same rule); a conservative max-height map skips the
+// test for spheres clear of the terrain.
 // ------------------------------------------------------------------------------------------------
 struct THit {
   float sep;
@@ -319,7 +321,8 @@ __device__ __forceinline__ V3 closest_on_tri(V3 p, V3 a, V3 b, V3 c, bool& face)
   const float dn = 1.f / (va + vb + vc);
   return a + (vb * dn) * ab + (vc * dn) * ac;
 }
-__device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, float margin) {
+// tv: this wave's LDS scratch for the 4 x 4 vertex block, [vertex][lane] float4 (conflict-free b128 accesses)
+__device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, float margin, float4* tv, int lane) {
   THit h;
   h.sep = 1e30f;
   h.n = v3(0.f, 0.f, 1.f);
@@ -327,24 +330,59 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   const float bs = K->p.border_size, ih = K->terr_inv_hs;
   const int ci = min(max((int)floorf((p.x + bs) * ih), 0), R - 2);
   const int cj = min(max((int)floorf((p.y + bs) * ih), 0), Cn - 2);
-  if (p.z - r - margin > K->terr_hmax[ci * Cn + cj]) return h;
-  const float* __restrict__ vtx = K->terr_vtx;
+  const float g = r + margin;
+  // the max-height word and the 4 x 4 vertices of the 3 x 3 cells in one memory round trip (rows / columns
+  // clamped for the load; cells off the grid are never marked), staged in LDS for the triangle walk
+  const float4* __restrict__ vtx = reinterpret_cast<const float4*>(K->terr_vtx);
+  const float hmax = K->terr_hmax[ci * Cn + cj];
+  float4 V[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int vi = min(max(ci - 1 + a, 0), R - 1);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) V[a][b] = vtx[vi * Cn + min(max(cj - 1 + b, 0), Cn - 1)];
+  }
+  if (p.z - r - margin > hmax) return h;
+  // triangles (bit 2 * (3 di + dj) + t) whose xy bounding box grown by g holds p's xy: a triangle under / over p
+  // always qualifies, so penetrating spheres keep the triangle they are in
+  uint32_t tris = 0;
+#pragma unroll
+  for (int di = 0; di < 3; ++di)
+#pragma unroll
+    for (int dj = 0; dj < 3; ++dj) {
+      const int i = ci - 1 + di, j = cj - 1 + dj;
+      const bool cell = i >= 0 && i <= R - 2 && j >= 0 && j <= Cn - 2;
+      const float4 A = V[di][dj], B = V[di][dj + 1], Cc = V[di + 1][dj], D = V[di + 1][dj + 1];
+      // t = 0: (v(i,j), v(i+1,j+1), v(i,j+1)) = (A, D, B);  t = 1: (v(i,j), v(i+1,j), v(i+1,j+1)) = (A, Cc, D)
+      const bool t0 = cell && p.x >= fminf(fminf(A.x, D.x), B.x) - g && p.x <= fmaxf(fmaxf(A.x, D.x), B.x) + g &&
+                      p.y >= fminf(fminf(A.y, D.y), B.y) - g && p.y <= fmaxf(fmaxf(A.y, D.y), B.y) + g;
+      const bool t1 = cell && p.x >= fminf(fminf(A.x, Cc.x), D.x) - g && p.x <= fmaxf(fmaxf(A.x, Cc.x), D.x) + g &&
+                      p.y >= fminf(fminf(A.y, Cc.y), D.y) - g && p.y <= fmaxf(fmaxf(A.y, Cc.y), D.y) + g;
+      const int k = 2 * (3 * di + dj);
+      tris |= (t0 ? 1u << k : 0u) | (t1 ? 2u << k : 0u);
+    }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) tv[(4 * a + b) * WAVE + lane] = V[a][b];
   float best = 3.0e38f;
   V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
   bool bface = true;
-  for (int i = max(ci - 1, 0); i <= min(ci + 1, R - 2); ++i) {
-    for (int j = max(cj - 1, 0); j <= min(cj + 1, Cn - 2); ++j) {
-      const int i0 = i * Cn + j;
-      const V3 va = terr_v(vtx, i0), vb = terr_v(vtx, i0 + 1), vc = terr_v(vtx, i0 + Cn), vd = terr_v(vtx, i0 + Cn + 1);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        // triangles of convert_heightfield_to_trimesh: (v(i,j), v(i+1,j+1), v(i,j+1)), (v(i,j), v(i+1,j), v(i+1,j+1))
-        const V3 b = t == 0 ? vd : vc, c = t == 0 ? vb : vd;
-        const V3 nf = cross(b - va, c - va);
-        const float a2 = dot(nf, nf);
-        if (a2 < 1e-12f) continue;  // collapsed by the slope correction
+  // each lane walks its own marked triangles in order (the wave runs max-over-lanes triangles, not 18)
+  while (__any((int)(tris != 0u))) {
+    if (tris) {
+      const int k = __builtin_ctz(tris);
+      tris &= tris - 1u;
+      const int c = k >> 1, di = c / 3, dj = c - 3 * di;
+      const int ia = 4 * di + dj;  // v(i,j) in the block
+      const int ib = (k & 1) ? ia + 4 : ia + 5, ic = (k & 1) ? ia + 5 : ia + 1;
+      const float4 fa = tv[ia * WAVE + lane], fb = tv[ib * WAVE + lane], fc = tv[ic * WAVE + lane];
+      const V3 va = v3(fa.x, fa.y, fa.z), b = v3(fb.x, fb.y, fb.z), cv = v3(fc.x, fc.y, fc.z);
+      const V3 nf = cross(b - va, cv - va);
+      const float a2 = dot(nf, nf);
+      if (a2 >= 1e-12f) {  // (zero area: collapsed by the slope correction)
         bool face;
-        const V3 q = closest_on_tri(p, va, b, c, face);
+        const V3 q = closest_on_tri(p, va, b, cv, face);
         const V3 dq = p - q;
         const float d2 = dot(dq, dq);
         if (d2 < best) {
@@ -366,6 +404,15 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
     h.sep = sd - r;
   }
   return h;
+}
+// max terrain height over the vertex window around the base's cell (lrl_sim_set_terrain: +-(ceil(reach / h) + 2)
+// rows / columns, reach = the model's largest xy distance of a sphere surface from the base origin), so every
+// vertex a query of one of the env's spheres can read is inside it; a sphere above it cannot touch the terrain
+__device__ __forceinline__ float terrain_window_max(const KParams* __restrict__ K, const float* pos) {
+  const float bs = K->p.border_size, ih = K->terr_inv_hs;
+  const int ci = min(max((int)floorf((pos[0] + bs) * ih), 0), K->terr_rows - 2);
+  const int cj = min(max((int)floorf((pos[1] + bs) * ih), 0), K->terr_cols - 2);
+  return K->terr_wmax[ci * K->terr_cols + cj];
 }
 // tangents of a contact normal: t1 = x (or y when n is close to x) made orthogonal to n, t2 = n x t1
 __device__ __forceinline__ void contact_frame(V3 n, V3& t1, V3& t2) {
@@ -599,21 +646,43 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   active = 0;
 
   // contact detection helper: separation, restitution/speculative target (needs nu at sub-step start)
-  auto detect = [&](int s, V3 x, int lsel, int link) {
-    float sep;
-    V3 nb = Rz;  // contact normal in base coordinates
-    if constexpr (TERR) {
-      const THit th = terrain_query(K, v3(st.pos[0], st.pos[1], pz) + mul(R, x), K->sph_rad[s], P.contact_offset);
-      sep = th.sep;
-      if (sep < P.contact_offset) {
-        M.sph(s, 3) = th.n.x;
-        M.sph(s, 4) = th.n.y;
-        M.sph(s, 5) = th.n.z;
-        nb = mulT(R, th.n);
-      }
-    } else {
-      sep = pz + dot(Rz, x) - K->sph_rad[s];
+  // contact activation: velocity target (restitution / speculative / Baumgarte) along the normal nb (base frame)
+  auto activate = [&](int s, V3 x, int lsel, int link, float sep, V3 nb) {
+    active |= (1ull << s);
+    M.sph(s, 0) = x.x;
+    M.sph(s, 1) = x.y;
+    M.sph(s, 2) = x.z;
+    V3 u = cross(wb, x) + vb;
+    if (lsel >= 0) {
+      V3 c[3];
+      leg_dirs(M, lsel, link, x, c);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) u = u + pick12(st.qd, 3 * lsel + j) * c[j];
     }
+    const float u0 = dot(nb, u);
+    float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+    if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
+    M.sph(s, 9) = tgt;
+  };
+  // TERR: spheres are only recorded here (contact point, world centre in the rows' free fields 6..8); those not
+  // clear of the terrain window around the base (one load) are queried after the leg pass, each lane walking its
+  // own list, so a wave pays max-over-lanes queries instead of every sphere of the model
+  uint64_t cand = 0;
+  float hwin = 0.f;
+  if constexpr (TERR) hwin = terrain_window_max(K, st.pos);
+  auto detect = [&](int s, V3 x, int lsel, int link) {
+    if constexpr (TERR) {
+      const V3 pw = v3(st.pos[0], st.pos[1], pz) + mul(R, x);
+      M.sph(s, 0) = x.x;
+      M.sph(s, 1) = x.y;
+      M.sph(s, 2) = x.z;
+      M.sph(s, 6) = pw.x;
+      M.sph(s, 7) = pw.y;
+      M.sph(s, 8) = pw.z;
+      if (pw.z - K->sph_rad[s] - P.contact_offset <= hwin) cand |= 1ull << s;
+      return;
+    }
+    const float sep = pz + dot(Rz, x) - K->sph_rad[s];
     if (sep < P.contact_offset) {
       active |= (1ull << s);
       M.sph(s, 0) = x.x;
@@ -626,7 +695,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #pragma unroll
         for (int j = 0; j < 3; ++j) u = u + pick12(st.qd, 3 * lsel + j) * c[j];
       }
-      const float u0 = dot(nb, u);
+      const float u0 = dot(Rz, u);
       float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
       if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
       M.sph(s, 9) = tgt;
@@ -706,6 +775,33 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     M.leg(l, 43) = sdot(S[1], Fc1);
     M.leg(l, 44) = sdot(S[2], Fc2);
     Cleg = Fc0;
+  }
+  if constexpr (TERR) {  // terrain queries of the recorded spheres (the leg frames are in LDS now)
+#ifdef LRL_ENV_PROFILE
+    const unsigned long long tq0 = clock64();
+#endif
+    for (uint64_t m = cand; __any((int)(m != 0ull));) {
+      if (m) {
+        const int s = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const THit th = terrain_query(K, v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8)), K->sph_rad[s], P.contact_offset,
+                                      reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS),
+                                      (int)threadIdx.x);
+        if (th.sep < P.contact_offset) {
+          M.sph(s, 3) = th.n.x;
+          M.sph(s, 4) = th.n.y;
+          M.sph(s, 5) = th.n.z;
+          activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), K->sph_link[s], th.sep,
+                   mulT(R, th.n));
+        }
+#ifdef LRL_ENV_PROFILE
+        prof[15] += 1;
+#endif
+      }
+    }
+#ifdef LRL_ENV_PROFILE
+    prof[14] += clock64() - tq0;  // terrain queries (part of kin+dyn+detect)
+#endif
   }
   // ---- quad reductions: legs -> base ----
 #pragma unroll
@@ -1027,7 +1123,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
   for (int s = 0; s < K->num_spheres; ++s)
     if (sph_owner(K, s) == ql) own |= 1ull << s;
-  unsigned long long prof[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   LRL_PROF_DECL
 #ifdef LRL_ENV_PROFILE
   prof_t = kt0;
@@ -1450,7 +1546,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 #ifdef LRL_ENV_PROFILE
   prof[9] = clock64() - kt0;  // the wave's whole lifetime (the phases above should sum to it)
   if (lane == 0)
-    for (int i = 0; i < 14; ++i) atomicAdd(&g_env_prof[i], prof[i]);
+    for (int i = 0; i < 16; ++i) atomicAdd(&g_env_prof[i], prof[i]);
 #endif
 }
 
@@ -1458,12 +1554,12 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 
 extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
 #ifdef LRL_ENV_PROFILE
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 14) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -2;
   if (reset) {
     unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
   }
-  return 14;
+  return 16;
 #else
   (void)out;
   (void)reset;

@@ -36,6 +36,7 @@ struct KParams {
   const float* terr_vtx;
   const float* terr_hmax;
   const float* terr_h;
+  const float* terr_wmax;  // max vertex z over the window around a base cell (terrain_window_max)
   int32_t terr_rows, terr_cols;
   float terr_inv_hs;
 };

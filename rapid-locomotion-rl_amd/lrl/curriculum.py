@@ -40,8 +40,12 @@ class GridCurriculum:
         return self.rng.uniform(centroids + half, centroids - half)
 
     def sample(self, batch_size):
+        """One ``uniform`` call over the [batch, 3] cell bounds: RandomState draws one double per element in C
+        order, i.e. exactly the per-row calls of curriculum.py:66-68 (np.stack over rows) in sequence."""
         cents, inds = self.sample_bins(batch_size)
-        return np.stack([self.sample_uniform_from_cell(c) for c in cents]), inds
+        if len(cents) == 0:
+            raise ValueError("need at least one array to stack")  # as np.stack([]) in the reference
+        return self.sample_uniform_from_cell(cents), inds
 
 
 class RewardThresholdCurriculum(GridCurriculum):

@@ -238,6 +238,7 @@ class LeggedRobotEnv:
         self._init_command_distribution()
         self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
         self._ids_all = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
+        self._due_next = None  # (episode_length_buf version, env ids due for command resampling next step)
         self.init_done = True
 
     # -------------------------------------------------------------------------------- plumbing
@@ -291,6 +292,8 @@ class LeggedRobotEnv:
     def _groups(self, env_ids=None):
         """_call_train_eval (legged_robot.py:456-469): (ids, cfg) of the train and eval envs among env_ids."""
         ids = torch.arange(self.num_envs, device=self.device) if env_ids is None else env_ids
+        if self.eval_cfg is None:
+            return [(ids, self.cfg)] if len(ids) else []
         out = [(ids[ids < self.num_train_envs], self.cfg)]
         if self.eval_cfg is not None:
             out.append((ids[ids >= self.num_train_envs], self.eval_cfg))
@@ -339,24 +342,31 @@ class LeggedRobotEnv:
         high = np.array([c.lin_vel_x[1], c.lin_vel_y[1], c.ang_vel_yaw[1]])
         self.curriculum.set_to(low=low, high=high)
 
-    def resample_commands(self, env_ids):
-        """_resample_commands (legged_robot.py:595-626); disconnected in the fork (Q3), callable here."""
+    def resample_commands(self, env_ids, _ids_host=None):
+        """_resample_commands (legged_robot.py:595-626); disconnected in the fork (Q3), callable here.
+        ``_ids_host``: the same ids as a numpy array when the caller already has them on the host."""
         if len(env_ids) == 0:
             return
         ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
-        ids_np = ids.cpu().numpy()
         timesteps = int(self.cfg.commands.resampling_time / self.dt)
         ep_len = min(self.cfg.env.max_episode_length, timesteps)
-        lin = (self.command_sums["tracking_lin_vel"][ids] / ep_len).cpu().numpy()
-        ang = (self.command_sums["tracking_ang_vel"][ids] / ep_len).cpu().numpy()
+        # both tracking sums in one device->host copy (float32 division on the device, as torch does)
+        keys = list(self.reward_scales)
+        rows = [keys.index("tracking_lin_vel"), keys.index("tracking_ang_vel")]
+        lin, ang = (self._command_sums[rows][:, ids] / ep_len).cpu().numpy()
+        ids_np = ids.cpu().numpy() if _ids_host is None else _ids_host
         lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
         ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
         old_bins = self.env_command_bins[ids_np]
         self.curriculum.update(old_bins, lin, ang, lin_thr, ang_thr, local_range=0.5)
         new_cmds, new_bins = self.curriculum.sample(batch_size=len(ids_np))
         self.env_command_bins[ids_np] = new_bins
-        self.commands[ids, :3] = torch.tensor(new_cmds, dtype=torch.float, device=self.device)
-        self.commands[ids, :2] *= (torch.norm(self.commands[ids, :2], dim=1) > 0.2).unsqueeze(1)
+        # commands[:, :3] = float32(cmds); commands[:, :2] *= (norm(commands[:, :2]) > 0.2): float32 on the host
+        c = new_cmds.astype(np.float32)
+        keep = (np.sqrt(c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]) > np.float32(0.2)).astype(np.float32)
+        c[:, 0] *= keep
+        c[:, 1] *= keep
+        self.commands[ids, :3] = torch.from_numpy(c).to(self.device)
         self._command_sums[:, ids] = 0.0
 
     # -------------------------------------------------------------------------------- API
@@ -370,7 +380,11 @@ class LeggedRobotEnv:
         if not self.legacy_fork:  # _post_physics_step_callback resampling (legged_robot.py:578-581): the
             # envs whose episode length reaches a multiple of resampling_time in this step, before its rewards
             interval = int(self.cfg.commands.resampling_time / self.dt)
-            due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
+            cached = self._due_next
+            if cached is not None and cached[0] == self.episode_length_buf._version:
+                due = cached[1]  # known from the previous step's single device->host copy
+            else:  # first step, or episode_length_buf written by a caller since
+                due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
             if len(due):
                 self.resample_commands(due)
         timer = self.kernel_timer
@@ -383,12 +397,22 @@ class LeggedRobotEnv:
             timer.append((ev0, ev1))
         self.common_step_counter += 1
         if not self.legacy_fork:  # reset_idx of the terminated / timed-out envs, then their observations
-            ids = self._reset_u8.nonzero(as_tuple=False).flatten()
-            if len(ids):
-                self.reset_idx(ids)
+            # one device->host copy per step: bit 0 = reset now, bit 1 = due for resampling next step (episode
+            # length after this step's resets: 0 for the reset envs)
+            eplen = self.episode_length_buf
+            nxt = ((eplen + 1) % interval == 0) if interval != 1 else torch.ones_like(self._reset_u8, dtype=torch.bool)
+            code = (self._reset_u8 | (nxt.to(torch.uint8) << 1)) if interval != 1 else (self._reset_u8 | 2)
+            code = code.cpu().numpy()
+            rst = code & 1
+            ids_np = np.flatnonzero(rst)
+            due_np = np.flatnonzero((code >> 1) & ((rst == 0) | (interval == 1)))
+            if len(ids_np):
+                ids = torch.from_numpy(ids_np).to(self.device)
+                self.reset_idx(ids, ids_np)
                 ids32 = ids.to(torch.int32).contiguous()
                 _abi.check(self._L.lrl_sim_observe_idx(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
                                                        C.c_uint32(flags), self._stream()))
+            self._due_next = (eplen._version, torch.from_numpy(due_np).to(self.device))
         ex = self.extras
         ex["privileged_obs"] = self.privileged_obs_buf
         ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())
@@ -424,12 +448,13 @@ class LeggedRobotEnv:
         obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
         return obs
 
-    def reset_idx(self, env_ids):
+    def reset_idx(self, env_ids, _ids_host=None):
         """legged_robot.py:227-290; train and eval envs (env id >= num_train_envs) go through their own cfg
         for the command curriculum (_call_train_eval, :456-469) and their own episode logging."""
         env_ids = torch.as_tensor(env_ids, device=self.device).long()
         if len(env_ids) == 0:
             return
+        self._due_next = None  # episode lengths change: the next step re-derives its resampling set
         n_tr = self.num_train_envs
         if self.num_eval_envs:
             tr, ev = env_ids[env_ids < n_tr], env_ids[env_ids >= n_tr]
@@ -443,7 +468,7 @@ class LeggedRobotEnv:
         if len(ev):
             self.update_command_curriculum(ev, self.eval_cfg)
         if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
-            self.resample_commands(env_ids)
+            self.resample_commands(env_ids, _ids_host)
         ids32 = env_ids.to(torch.int32).contiguous()
         xo = yo = 0.0
         if self.custom_origins:  # torch_rand_float(x_init_range, y_init_range) == constant (Q8)

@@ -1,5 +1,6 @@
 """Phase breakdown of the env step kernel (build: -DLRL_ENV_PROFILE, see csrc/lrl_env.hip; run with
-LRL_LIB=<that build>).  4096 Mini Cheetah envs, random actions."""
+LRL_LIB=<that build>, e.g. `make -C rapid-locomotion-rl_amd/csrc liblrl_prof.so`).  4096 envs, random actions;
+argv: [n] [mc | go1 | go1_rough]."""
 import ctypes as C
 import os
 import sys
@@ -12,12 +13,17 @@ from lrl import config as lcfg  # noqa: E402
 from lrl.env import LeggedRobotEnv  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+which = sys.argv[2] if len(sys.argv) > 2 else "mc"
 cfg = lcfg.make_cfg()
-lcfg.config_mini_cheetah(cfg)
+(lcfg.config_mini_cheetah if which == "mc" else lcfg.config_go1)(cfg)
+if which == "go1_rough":
+    cfg.terrain.mesh_type = "trimesh"
+    cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]
+    cfg.terrain.curriculum = True
 env = LeggedRobotEnv("cuda:0", cfg=cfg, num_envs=n)
 env.reset()
 L = _abi.lib()
-buf = (C.c_ulonglong * 14)()
+buf = (C.c_ulonglong * 16)()
 g = torch.Generator(device="cuda:0").manual_seed(0)
 for _ in range(50):
     env.step(0.5 * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
@@ -27,7 +33,7 @@ K = 100
 for _ in range(K):
     env.step(0.5 * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
 torch.cuda.synchronize()
-assert L.lrl_debug_env_profile(buf, 0) == 14, "library built without LRL_ENV_PROFILE"
+assert L.lrl_debug_env_profile(buf, 0) == 16, "library built without LRL_ENV_PROFILE"
 waves = (n + 15) // 16  # quad layout: 16 envs per wave
 names = ["kin+dyn+detect", "schur+free acc", "delassus+warm", "PGS", "integrate", "start+state load", "post-physics",
          "tiles+history", "PD torques"]
@@ -36,5 +42,8 @@ for i, nm in enumerate(names[:9]):
     print(f"{nm:16s} {buf[i] / waves / K:10.0f} cycles/wave/step  {100 * buf[i] / tot:5.1f}%")
 for i, nm in zip(range(10, 14), ["  contact forces", "  loads/teleport/DR", "  rewards+sums", "  obs/priv rows"]):
     print(f"{nm:16s} {buf[i] / waves / K:10.0f} cycles/wave/step  (part of post-physics)")
+if buf[15]:
+    print(f"  terrain queries {buf[14] / waves / K:10.0f} cycles/wave/step  ({buf[15] / waves / K:.1f} per lane, "
+          f"{buf[14] / buf[15]:.0f} cycles each; part of kin+dyn+detect)")
 print(f"total {tot / waves / K:.0f} cycles/wave/step (wave lifetime {buf[9] / waves / K:.0f}); "
       f"resets/step {env._reset_u8.float().mean().item():.3f}")

@@ -132,8 +132,10 @@ def test_oracle_terrain_contact_geometry():
     r = 0.02
     sep, n = oracle.terrain_query(P, [0.5, 1.0, 0.05], r)  # above the floor
     np.testing.assert_allclose([sep, *n], [0.03, 0, 0, 1], atol=1e-7)
-    sep, n = oracle.terrain_query(P, [0.97, 1.0, 0.1], r)  # in front of the wall (x = 1.0 after the move)
-    np.testing.assert_allclose([sep, *n], [0.01, -1, 0, 0], atol=1e-7)
+    sep, n = oracle.terrain_query(P, [0.985, 1.0, 0.1], r)  # touching the wall (x = 1.0 after the move)
+    np.testing.assert_allclose([sep, *n], [-0.005, -1, 0, 0], atol=1e-7)
+    sep, n = oracle.terrain_query(P, [0.95, 1.0, 0.1], r)  # wall beyond r + contact_offset in xy: the floor
+    np.testing.assert_allclose([sep, *n], [0.08, 0, 0, 1], atol=1e-7)
     sep, n = oracle.terrain_query(P, [1.5, 1.0, 0.23], r)  # on the step top
     np.testing.assert_allclose([sep, *n], [0.01, 0, 0, 1], atol=1e-7)
     sep, n = oracle.terrain_query(P, [0.98, 1.0, 0.22], r)  # past the convex edge: distance to the edge
