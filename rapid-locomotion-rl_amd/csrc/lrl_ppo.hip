@@ -642,7 +642,12 @@ struct Plan {
   int64_t bytes;
 };
 
-constexpr int XS = 64;      // X row pitch (obs + latent <= 64)
+// X = [obs | latent] row pitch: 64 for the blind policies (42 + 18), else rounded up to 16 floats (a height-scan
+// policy: 235 + 18 -> 256).  Columns nx..XS-1 are zero.
+static int xs_of(const lrl_ppo_net& n) {
+  const int nx = n.num_obs + n.latent;
+  return nx <= 64 ? 64 : (nx + 15) / 16 * 16;
+}
 constexpr int LATS = 32;    // latent-wide buffers pitch
 constexpr int HD2S = 32;    // adaptation hidden-2 pitch
 
@@ -663,7 +668,7 @@ static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
     return r;
   };
   const int64_t Bl = B;
-  p.xa = take(Bl * XS);
+  p.xa = take(Bl * xs_of(n));
   p.he1 = take(Bl * n.enc_h0);
   p.he2 = take(Bl * n.enc_h1);
   p.h1 = take(Bl * 2 * n.ac_h0);
@@ -699,7 +704,6 @@ static int check_net(const lrl_ppo_net* n) {
   if (n->ac_h2 != HEAD_W) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: last actor/critic hidden width must be 128");
   if (n->num_actions != HEAD_NA) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: num_actions must be 12");
   if (n->latent > MAX_LAT || n->ad_h1 > MAX_LAT) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: latent/adaptation widths > 32");
-  if (n->num_obs + n->latent > XS) return lrl_set_error(LRL_E_INVALID, "lrl_ppo: obs + latent > 64");
   return 0;
 }
 
@@ -813,7 +817,7 @@ static ActPlan make_act_plan(const lrl_ppo_net& n, int rows, char* base) {
     return r;
   };
   const int64_t R = rows;
-  p.xa = take(R * XS);
+  p.xa = take(R * xs_of(n));
   p.he1 = take(R * n.enc_h0);
   p.he2 = take(R * n.enc_h1);
   p.h1 = take(R * 2 * n.ac_h0);
@@ -843,7 +847,7 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   hipStream_t st = static_cast<hipStream_t>(stream);
   G g{st, nullptr};
   const float* w = params;
-  const int nx = nt.num_obs + nt.latent;
+  const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
   hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
                      (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
@@ -880,7 +884,7 @@ static StudentPlan make_student_plan(const lrl_ppo_net& n, int rows, char* base)
     return r;
   };
   const int64_t R = rows;
-  p.xa = take(R * XS);
+  p.xa = take(R * xs_of(n));
   p.hd1 = take(R * n.ad_h0);
   p.hd2 = take(R * HD2S);
   p.h1 = take(R * n.ac_h0);
@@ -909,7 +913,7 @@ extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* para
   hipStream_t st = static_cast<hipStream_t>(stream);
   G g{st, nullptr};
   const float* w = params;
-  const int nx = nt.num_obs + nt.latent;
+  const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
   hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
                      (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   if (hld >= hpad && hld % 4 == 0 && ((uintptr_t)hist & 15) == 0 && hpad != nt.num_hist) {
@@ -953,14 +957,14 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   hipStream_t st = static_cast<hipStream_t>(stream);
   G g{st, P.part + P.part_floats};
   const float* w = params;
-  const int nx = n.num_obs + n.latent;
+  const int nx = n.num_obs + n.latent, XS = xs_of(n);
   // ---- forward ----
   hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)B * XS + 255) / 256)), dim3(256), 0, st, bt->obs,
                      bt->rows, B, n.num_obs, XS, P.xa);
   g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
   g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
   g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.xa + n.num_obs, XS, w + n.e3b, B, n.latent, n.enc_h1, false);
-  // k runs over all XS = 64 columns of X: columns nx..63 are zero, so the extra products (with the next
+  // k runs over all XS columns of X: columns nx..XS-1 are zero, so the extra products (with the next
   // row's first weights, or the first biases after the last row — finite values) add exactly 0, and the
   // product takes the unguarded float4 path
   g.nt(P.xa, XS, nullptr, w + n.w1, nx, P.h1, 2 * n.ac_h0, w + n.b1, B, 2 * n.ac_h0, XS, true);

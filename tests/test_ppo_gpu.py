@@ -43,15 +43,16 @@ def test_gae_matches_reference():
     np.testing.assert_allclose(adv.cpu().numpy(), g["advantages"], rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("n", [37, 4096])
-def test_fused_policy_act_matches_torch(n):
+@pytest.mark.parametrize("n,no", [(37, 42), (4096, 42), (300, 235)])
+def test_fused_policy_act_matches_torch(n, no):
+    """no = 235: the base config's perceptive policy (observe_vel + 17 x 11 height scan, X pitch 256)."""
     from lrl.ppo.actor_critic import ActorCritic
-    ac = ActorCritic(42, 18, 630, 12).cuda()
+    ac = ActorCritic(no, 18, 15 * no, 12).cuda()
     init_params(ac)
     with torch.no_grad():
         ac.std.copy_(torch.linspace(0.5, 1.5, 12))
     g = torch.Generator(device="cuda:0").manual_seed(3)
-    obs = torch.randn(n, 42, device="cuda:0", generator=g)
+    obs = torch.randn(n, no, device="cuda:0", generator=g)
     priv = torch.randn(n, 18, device="cuda:0", generator=g)
     eps = torch.randn(n, 12, device="cuda:0", generator=g)
     a, mu, v, lp = ac.act_fused(obs, priv, eps=eps)
@@ -189,8 +190,8 @@ def _random_storage(alg, N, T, seed=1):
         st.actions_log_prob.copy_(-11.0 + torch.randn(st.values.shape, device="cuda:0", generator=g))
 
 
-@pytest.mark.parametrize("padded_hist", [True, False])
-def test_native_minibatch_gradients_match_autograd(padded_hist):
+@pytest.mark.parametrize("padded_hist,no", [(True, 42), (False, 42), (True, 235)])
+def test_native_minibatch_gradients_match_autograd(padded_hist, no):
     """One minibatch of lrl_ppo_forward_backward / lrl_ppo_adaptation_forward_backward against torch
     autograd of the reference's loss (ppo.py:98-147, 157-166): every parameter's gradient, the KL mean,
     the losses.  History rows either at the storage's padded pitch (640: the float4 / zero-k-padding
@@ -200,10 +201,11 @@ def test_native_minibatch_gradients_match_autograd(padded_hist):
     from lrl.ppo.actor_critic import ActorCritic
     from lrl.ppo.ppo import PPO, PPO_Args
     N, T = 256, 24
-    ac = ActorCritic(42, 18, 630, 12)
+    nh = 15 * no
+    ac = ActorCritic(no, 18, nh, 12)
     init_params(ac)
     alg = PPO(ac.cuda(), device="cuda:0", fused=True)
-    alg.init_storage(N, T, [42], [18], [630], [12])
+    alg.init_storage(N, T, [no], [18], [nh], [12])
     _random_storage(alg, N, T)
     mb = N * T // 4
     rows = torch.randperm(N * T, device="cuda:0")[:mb].contiguous()
@@ -221,7 +223,7 @@ def test_native_minibatch_gradients_match_autograd(padded_hist):
     if not padded_hist:
         hist_flat = hist_flat.contiguous()
         batch.hist = hist_flat.data_ptr()
-    assert hist_flat.stride(0) == (640 if padded_hist else 630)
+    assert hist_flat.stride(0) == ((nh + 15) // 16 * 16 if padded_hist else nh)
     batch.hist_ld = hist_flat.stride(0)
     p = lambda t: C.c_void_p(t.data_ptr())
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -203,3 +203,28 @@ def test_rough_terrain_standing_and_curriculum():
     np.testing.assert_allclose(_np(env.root_states[ids, 2]), _np(org[:, 2]) + cfg.init_state.pos[2], atol=1e-5)
     assert "terrain_level" in env.extras["train/episode"]
     env.close()
+
+
+def test_perceptive_policy_trains_on_rough_terrain():
+    """The base config's perceptive layout (observe_vel + 17 x 11 height scan = 235 observations, history
+    15 x 235) end to end: upstream resets on the curriculum trimesh, one Runner.learn iteration through the
+    native act / update (X pitch 256) — finite losses, heights in the observations."""
+    from lrl.env import LeggedRobotEnv
+    from lrl.history import HistoryWrapper
+    from lrl.ppo import runner as R
+    n = 256
+    cfg = _rough_cfg(n, 3.0, **{"terrain.num_rows": 4, "terrain.num_cols": 4, "env.observe_vel": True,
+                                "env.num_observations": 48 + 187})
+    R.RunnerArgs.save_interval = 0
+    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=2, legacy_fork=False))
+    assert env.num_obs == 235 and env.num_obs_history == 15 * 235
+    runner = R.Runner(env, device="cuda:0", seed=2)
+    runner.learn(1, init_at_random_ep_len=True)
+    torch.cuda.synchronize()
+    obs = _np(env.env.obs_buf)
+    assert np.isfinite(obs).all() and np.abs(obs[:, 48:]).max() > 0  # the scan reaches the policy
+    st = runner.alg.storage
+    assert torch.isfinite(st.values).all() and torch.isfinite(st.actions).all()
+    p = runner.alg.actor_critic._flat
+    assert torch.isfinite(p).all()
+    env.env.close()
