@@ -189,7 +189,7 @@ def main():
     value = steps_total / elapsed
     if rank == 0:
         achieved = B_ENV * ENVS_PER_GPU / (k_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic("lrl::env_step_kernel")
+        traffic, traffic_src = pmc_traffic("lrl::env_step_kernel<false>", "lrl::env_step_kernel")
         # update's largest product: actor/critic layer-2 weight gradient, 2 x (256 x 512) over the minibatch rows
         mb_rows = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env // 4
         gemm_flop = 2.0 * 2 * 256 * 512 * mb_rows
@@ -208,7 +208,7 @@ def main():
             "ppo_iters_per_s": round(args.steps / elapsed, 3),
             "env_only_env_steps_per_s_per_gpu": round(env_only, 1),
             "env_step_kernel_ms": round(k_ms, 4),
-            "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel", "achieved": round(achieved, 3),
+            "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel<false> (plane ground)", "achieved": round(achieved, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (the fused history "

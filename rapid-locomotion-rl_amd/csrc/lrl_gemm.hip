@@ -4,6 +4,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "../../include/lrl.h"
 #include "lrl_gemm.h"
@@ -913,6 +915,10 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   p.groups = groups;
   dim3 grid(((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * groups * p.splits);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  static const bool trace = getenv("LRL_GEMM_TRACE") != nullptr;  // shape log for profiling runs
+  if (trace)
+    fprintf(stderr, "gemm layout=%d epi=%d M=%d N=%d K=%d groups=%d splits=%d avec=%d bvec=%d arows=%d brows=%d\n",
+            layout, epi, p.M, p.N, p.K, groups, p.splits, p.avec, p.bvec, p.a_rows != nullptr, p.b_rows != nullptr);
   // LDS-DMA path: batch-major product, every tile interior, float4-aligned operands, single split
   if (layout != GEMM_TN && p.splits == 1 && p.M % 64 == 0 && p.N % 64 == 0 && p.K % 16 == 0 && p.K >= 32 &&
       p.avec == 4 && p.bvec == 4 && epi != EPI_PARTIAL && (layout == GEMM_NT || layout == GEMM_NN)) {

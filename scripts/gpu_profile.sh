@@ -10,14 +10,14 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 rm -rf /tmp/lrlprof && mkdir -p /tmp/lrlprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/lrlprof/trace -o run -- \
-  python3 "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline > "$OUT/trace.log" 2>&1
+  python3 "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/trace.log" 2>&1
 find /tmp/lrlprof/trace -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 KT=$(find /tmp/lrlprof/trace -name "*kernel_trace.csv" | head -n 1)
 python3 "$ROOT/scripts/trace_reduce.py" "$KT" > "$OUT/kernel_by_grid.csv"
 [ "${NO_PMC:-0}" = 1 ] && exit 0
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d /tmp/lrlprof/$C -o run -- \
-    python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$C.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-secondary > "$OUT/pmc_$C.log" 2>&1
   F=$(find /tmp/lrlprof/$C -name "*counter_collection.csv" | head -n 1)
   python3 "$ROOT/scripts/pmc_reduce.py" "$F" "$C" > "$OUT/pmc_$C.csv"
   timeout -k 10 120 rocprofv3 --pmc $C --output-format csv -d /tmp/lrlprof/cal_$C -o run -- \
