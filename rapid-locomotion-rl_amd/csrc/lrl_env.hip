@@ -571,19 +571,78 @@ struct Body {  // per-lane env state during the step
 // One physics sub-step.  Contact impulses of the sub-step stay in the LDS rows (fields 10..12).
 // ------------------------------------------------------------------------------------------------
 // sum of a value over the 4 lanes of an env (xor-shuffles inside the quad)
+// quad exchanges through DPP quad_perm (a VALU operand modifier, no LDS crossbar round trip):
+// xor 1 = [1,0,3,2] (0xB1), xor 2 = [2,3,0,1] (0x4E), broadcast of quad lane l = [l,l,l,l] (l * 0x55)
+template <int CTRL>
+__device__ __forceinline__ int qperm(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float qperm(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// sum over the quad: every lane gets (v0 + v1) + (v2 + v3) with the operands of each add swapped at most, so
+// the four lanes hold bitwise the same value
 __device__ __forceinline__ float quad_sum(float v) {
-  v += __shfl_xor(v, 1, WAVE);
-  v += __shfl_xor(v, 2, WAVE);
+  v += qperm<0xB1>(v);
+  v += qperm<0x4E>(v);
   return v;
 }
-__device__ __forceinline__ uint64_t quad_or(uint64_t v) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  lo |= __shfl_xor(lo, 1, WAVE);
-  hi |= __shfl_xor(hi, 1, WAVE);
-  lo |= __shfl_xor(lo, 2, WAVE);
-  hi |= __shfl_xor(hi, 2, WAVE);
-  return ((uint64_t)hi << 32) | lo;
+// value of quad lane l
+__device__ __forceinline__ float quad_bcast(float v, int l) {
+  switch (l) {
+    case 0: return qperm<0x00>(v);
+    case 1: return qperm<0x55>(v);
+    case 2: return qperm<0xAA>(v);
+    default: return qperm<0xFF>(v);
+  }
 }
+__device__ __forceinline__ uint64_t quad_or(uint64_t v) {
+  int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+  lo |= qperm<0xB1>(lo);
+  hi |= qperm<0xB1>(hi);
+  lo |= qperm<0x4E>(lo);
+  hi |= qperm<0x4E>(hi);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// The Gauss-Seidel update with the base velocity spread over the env's quad: lane q holds v_b[q] (vo0) and, for
+// q < 2, v_b[q + 4] (vo1, 0 in lanes 2 and 3), and owns component q < 3 of the leg accumulators Y_L.  Each lane
+// forms its part of the three contact-velocity rows, one quad sum gives every lane the same u, the cone
+// projection runs in all four lanes, and each lane updates only what it owns — a quarter of the row reads and
+// fused multiply-adds of the redundant form, and no lane reads what another lane writes (no barrier).
+__device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, float mu, int q, float& vo0, float& vo1) {
+  const int L = lsel < 0 ? 0 : lsel;
+  const bool hj = q < 3;
+  // lane 3 reads finite neighbouring fields and zeroes them by selection (no divergent branches)
+  const float yq = hj ? M.leg(L, 45 + q) + M.leg(L, 48 + q) : 0.f;
+  float u[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float a = M.sph(s, SF_G + 6 * d + q) * vo0 + M.sph(s, SF_G + 6 * d + q + 4) * vo1;
+    a += (hj ? M.sph(s, SF_H + 3 * d + q) : 0.f) * yq;
+    u[d] = quad_sum(a);
+  }
+  const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
+  const float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
+  const float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
+  const float ln = fmaxf(ln0 - (u[0] - b) * iWnn, 0.f);
+  const float dn = ln - ln0;
+  const float ut1 = u[1] + Wt1n * dn, ut2 = u[2] + Wt2n * dn;
+  float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
+  const float lim = mu * ln, nt2 = lt1 * lt1 + lt2 * lt2;
+  const float sc = nt2 > lim * lim ? (nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f) : 1.f;
+  lt1 *= sc;
+  lt2 *= sc;
+  M.sph(s, 10) = ln;
+  M.sph(s, 11) = lt1;
+  M.sph(s, 12) = lt2;
+  const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
+  vo0 += dn * M.sph(s, SF_Z + q) + dt1 * M.sph(s, SF_Z + 6 + q) + dt2 * M.sph(s, SF_Z + 12 + q);
+  const float d1 = dn * M.sph(s, SF_Z + q + 4) + dt1 * M.sph(s, SF_Z + 10 + q) + dt2 * M.sph(s, SF_Z + 16 + q);
+  vo1 = q < 2 ? vo1 + d1 : 0.f;
+  if (hj) M.leg(L, 48 + q) += dn * M.sph(s, SF_E + q) + dt1 * M.sph(s, SF_E + 3 + q) + dt2 * M.sph(s, SF_E + 6 + q);
+}
+
 // lane of the quad that owns sphere s: its leg, or round-robin for the base spheres
 __device__ __forceinline__ int sph_owner(const KParams* __restrict__ K, int s) {
   const int l = K->sph_leg[s];
@@ -909,14 +968,25 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   // projected Gauss-Seidel, sphere order = model order (base, legs 0..3)
   // (each env walks its own active spheres in model order; the wave runs max-over-envs sphere updates,
   // not the union of the 16 envs' contact sets)
-  for (int it = 0; it < P.solver_iterations; ++it)
-    for (uint64_t m = active; __any((int)(m != 0ull));) {
-      if (m) {
-        const int s = __builtin_ctzll(m);
-        m &= m - 1ull;
-        contact_pgs(M, s, sph_leg_of(SL, s), mu, vbc);
+  {
+    float vo0 = vbc[0], vo1 = vbc[4];
+#pragma unroll
+    for (int r = 1; r < 4; ++r) vo0 = ql == r ? vbc[r] : vo0;
+    vo1 = ql == 1 ? vbc[5] : (ql == 0 ? vo1 : 0.f);
+    for (int it = 0; it < P.solver_iterations; ++it)
+      for (uint64_t m = active; __any((int)(m != 0ull));) {
+        if (m) {
+          const int s = __builtin_ctzll(m);
+          m &= m - 1ull;
+          contact_pgs_q(M, s, sph_leg_of(SL, s), mu, ql, vo0, vo1);
+        }
       }
-    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) vbc[r] = quad_bcast(vo0, r);
+    vbc[4] = quad_bcast(vo1, 0);
+    vbc[5] = quad_bcast(vo1, 1);
+  }
+  __syncthreads();  // the leg accumulators each lane owned are read by the whole quad below
   LRL_PROF(3)  // PGS iterations
   // materialise the lazily propagated joint rates
 #pragma unroll
@@ -1158,7 +1228,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
 #pragma unroll
   for (int l = 0; l < 4; ++l)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) tau[3 * l + j] = __shfl(tau3[j], (lane & ~3) | l, WAVE);
+    for (int j = 0; j < 3; ++j) tau[3 * l + j] = quad_bcast(tau3[j], l);
 #ifdef LRL_ENV_PROFILE
   prof_t = clock64();
 #endif
@@ -1226,8 +1296,8 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
     for (int f = 0; f < 4; ++f)
       if (fs == f) { ff[f][0] = fx; ff[f][1] = fy; ff[f][2] = fz; }
   }
-  rst |= __shfl_xor(rst, 1, WAVE);
-  rst |= __shfl_xor(rst, 2, WAVE);
+  rst |= qperm<0xB1>(rst);
+  rst |= qperm<0x4E>(rst);
   collision = quad_sum(collision);
 #pragma unroll
   for (int f = 0; f < 4; ++f)
