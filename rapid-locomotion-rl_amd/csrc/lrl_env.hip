@@ -521,46 +521,6 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
   }
 }
 
-// One projected Gauss-Seidel update of a contact (normal, then the friction pair inside the cone).
-// Branch-free over the sphere kind: a base sphere (lsel < 0) has h_d = e_d = 0 in its rows, so it reads and
-// writes leg 0's accumulators with exact-zero contributions, and the envs of a wave never split paths.
-__device__ __forceinline__ void contact_pgs(const Lds& M, int s, int lsel, float mu, float* vb) {
-  const int L = lsel < 0 ? 0 : lsel;
-  float u[3];
-  float yq[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) yq[j] = M.leg(L, 45 + j) + M.leg(L, 48 + j);
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    float a = 0.f;
-#pragma unroll
-    for (int r = 0; r < 6; ++r) a += M.sph(s, SF_G + 6 * d + r) * vb[r];
-    a += M.sph(s, SF_H + 3 * d) * yq[0] + M.sph(s, SF_H + 3 * d + 1) * yq[1] + M.sph(s, SF_H + 3 * d + 2) * yq[2];
-    u[d] = a;
-  }
-  const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
-  const float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
-  const float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
-  const float ln = fmaxf(ln0 - (u[0] - b) * iWnn, 0.f);
-  const float dn = ln - ln0;
-  const float ut1 = u[1] + Wt1n * dn, ut2 = u[2] + Wt2n * dn;
-  float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
-  const float lim = mu * ln, nt2 = lt1 * lt1 + lt2 * lt2;
-  const float sc = nt2 > lim * lim ? (nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f) : 1.f;
-  lt1 *= sc;
-  lt2 *= sc;
-  M.sph(s, 10) = ln;
-  M.sph(s, 11) = lt1;
-  M.sph(s, 12) = lt2;
-  const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-    vb[r] += dn * M.sph(s, SF_Z + r) + dt1 * M.sph(s, SF_Z + 6 + r) + dt2 * M.sph(s, SF_Z + 12 + r);
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-    M.leg(L, 48 + j) += dn * M.sph(s, SF_E + j) + dt1 * M.sph(s, SF_E + 3 + j) + dt2 * M.sph(s, SF_E + 6 + j);
-}
-
 struct Body {  // per-lane env state during the step
   float pos[3], quat[4], V[3], W[3];
   float q[12], qd[12];
