@@ -685,9 +685,54 @@ def gen_terrain_curriculum(n=64, seed=13):
     print("terrain_curriculum:", {k: v.shape for k, v in out.items()})
 
 
+def gen_high_level(n=32, T=40, seed=5):
+    """HighLevelControlWrapper (scripts/high_level_play.py:30-363) driven over the scripted low-level env of
+    fake_ll_env.py (the reference constructor's _load_env is replaced by it; its hard-coded cuda:0 tensors are
+    made on the CPU): observations, rewards, resets, episode logging and the commands handed down, per step."""
+    from fake_ll_env import FakeLowLevelEnv
+    import importlib
+    hlp = importlib.import_module("scripts.high_level_play")
+    W = hlp.HighLevelControlWrapper
+    fake = FakeLowLevelEnv(n, T, seed)
+    policy = lambda ob: torch.zeros(n, 12)
+    W._load_env = lambda self, num_envs, headless: (fake, policy)
+    z, o = torch.zeros, torch.ones
+
+    def cpu(fn):
+        def g(*a, **k):
+            k.pop("device", None)
+            return fn(*a, **k)
+        return g
+    torch.zeros, torch.ones = cpu(z), cpu(o)
+    try:
+        env = W(num_envs=n)
+        env.device = "cpu"
+        rng = np.random.default_rng(seed + 1)
+        acts = rng.uniform(-2.5, 2.5, (T, n, 3)).astype(np.float32)
+        acts[:, 8:12, :2] = 0.1  # below the 0.2 command threshold
+        rec = {k: [] for k in ("obs", "rew", "reset", "ep_total", "ep_distance", "ep_gs", "extra_total")}
+        for t in range(T):
+            obs, rew, reset, extras = env.step(torch.tensor(acts[t]))
+            rec["obs"].append(obs["obs"].numpy().copy())
+            rec["rew"].append(rew.numpy().copy())
+            rec["reset"].append(reset.numpy().copy())
+            rec["ep_total"].append(env.episode_sums["total"].numpy().copy())
+            rec["ep_distance"].append(env.episode_sums["distance"].numpy().copy())
+            rec["ep_gs"].append(env.episode_sums["terminal_distance_gs"].numpy().copy())
+            ep = extras.get("train/episode", {})
+            rec["extra_total"].append(np.float32(ep["rew_total"].item()) if "rew_total" in ep else np.float32(np.nan))
+    finally:
+        torch.zeros, torch.ones = z, o
+    out = {k: np.stack(v) for k, v in rec.items()}
+    out["actions"] = acts
+    out["commands"] = np.stack([c.numpy() for c in fake.commands_log])
+    np.savez_compressed(os.path.join(HERE, "high_level.npz"), **out)
+    print("high_level:", {k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     gens = dict(post_physics_mc=lambda: gen_post_physics("mc"), post_physics_go1=lambda: gen_post_physics("go1"),
                 curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint, terrain=gen_terrain,
-                heights=gen_heights, terrain_curriculum=gen_terrain_curriculum)
+                heights=gen_heights, terrain_curriculum=gen_terrain_curriculum, high_level=gen_high_level)
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()
