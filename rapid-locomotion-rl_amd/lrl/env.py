@@ -239,6 +239,10 @@ class LeggedRobotEnv:
         self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
         self._ids_all = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
         self._due_next = None  # (episode_length_buf version, env ids due for command resampling next step)
+        self._sums_host = None  # (command_sums version, host copy of the two tracking rows) between a step's sync
+        keys = list(self.reward_scales)  # and the resampling it feeds
+        self._track_rows = [keys.index("tracking_lin_vel"), keys.index("tracking_ang_vel")] \
+            if "tracking_lin_vel" in keys and "tracking_ang_vel" in keys else None
         self.init_done = True
 
     # -------------------------------------------------------------------------------- plumbing
@@ -351,10 +355,14 @@ class LeggedRobotEnv:
         timesteps = int(self.cfg.commands.resampling_time / self.dt)
         ep_len = min(self.cfg.env.max_episode_length, timesteps)
         # both tracking sums in one device->host copy (float32 division on the device, as torch does)
-        keys = list(self.reward_scales)
-        rows = [keys.index("tracking_lin_vel"), keys.index("tracking_ang_vel")]
-        lin, ang = (self._command_sums[rows][:, ids] / ep_len).cpu().numpy()
         ids_np = ids.cpu().numpy() if _ids_host is None else _ids_host
+        hs = self._sums_host
+        if hs is not None and _ids_host is not None and hs[0] == self._command_sums._version:
+            # the step's device->host copy (float32 sums / ep_len in float32, as torch divides on the device)
+            lin, ang = hs[1][:, ids_np] / np.float32(ep_len)
+            hs[1][:, ids_np] = 0.0  # mirrors the zeroing below
+        else:
+            lin, ang = (self._command_sums[self._track_rows][:, ids] / ep_len).cpu().numpy()
         lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
         ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
         old_bins = self.env_command_bins[ids_np]
@@ -368,6 +376,8 @@ class LeggedRobotEnv:
         c[:, 1] *= keep
         self.commands[ids, :3] = torch.from_numpy(c).to(self.device)
         self._command_sums[:, ids] = 0.0
+        if hs is not None and _ids_host is not None and hs[0] + 1 == self._command_sums._version:
+            self._sums_host = (self._command_sums._version, hs[1])  # the host copy was zeroed alike
 
     # -------------------------------------------------------------------------------- API
     def step(self, actions, _history=False):
@@ -386,7 +396,8 @@ class LeggedRobotEnv:
             else:  # first step, or episode_length_buf written by a caller since
                 due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
             if len(due):
-                self.resample_commands(due)
+                self.resample_commands(due, due.cpu().numpy() if cached is None else cached[2])
+        self._sums_host = None  # the kernel below changes the command sums
         timer = self.kernel_timer
         if timer is not None:  # HIP events on the launch stream around the fused kernel (bench.py)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -399,10 +410,17 @@ class LeggedRobotEnv:
         if not self.legacy_fork:  # reset_idx of the terminated / timed-out envs, then their observations
             # one device->host copy per step: bit 0 = reset now, bit 1 = due for resampling next step (episode
             # length after this step's resets: 0 for the reset envs)
+            # length after this step's resets: 0 for the reset envs), rows 1-2 = the tracking command sums the
+            # curriculum update of the envs resampled next (resets now, due ones before the next kernel) reads
             eplen = self.episode_length_buf
             nxt = ((eplen + 1) % interval == 0) if interval != 1 else torch.ones_like(self._reset_u8, dtype=torch.bool)
             code = (self._reset_u8 | (nxt.to(torch.uint8) << 1)) if interval != 1 else (self._reset_u8 | 2)
-            code = code.cpu().numpy()
+            if self._track_rows is not None:
+                pack = torch.cat([code.to(torch.float32).unsqueeze(0), self._command_sums[self._track_rows]]).cpu().numpy()
+                code = pack[0].astype(np.uint8)
+                self._sums_host = (self._command_sums._version, pack[1:3])
+            else:
+                code = code.cpu().numpy()
             rst = code & 1
             ids_np = np.flatnonzero(rst)
             due_np = np.flatnonzero((code >> 1) & ((rst == 0) | (interval == 1)))
@@ -412,7 +430,7 @@ class LeggedRobotEnv:
                 ids32 = ids.to(torch.int32).contiguous()
                 _abi.check(self._L.lrl_sim_observe_idx(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
                                                        C.c_uint32(flags), self._stream()))
-            self._due_next = (eplen._version, torch.from_numpy(due_np).to(self.device))
+            self._due_next = (eplen._version, torch.from_numpy(due_np).to(self.device), due_np)
         ex = self.extras
         ex["privileged_obs"] = self.privileged_obs_buf
         ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())

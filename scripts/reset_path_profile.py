@@ -1,5 +1,6 @@
 """Host-side cost of the upstream reset path (legacy_fork=False): cProfile of 100 env steps of 4096 Go1 envs
-on the curriculum trimesh with random actions (frequent terminations), wall time per step."""
+on the curriculum trimesh (or Mini Cheetah on its flat map: argv `mc`; fork semantics: argv `fork`) with random
+actions (frequent terminations), wall time per step."""
 import cProfile
 import os
 import pstats
@@ -15,13 +16,16 @@ from lrl.env import LeggedRobotEnv  # noqa: E402
 from lrl.history import HistoryWrapper  # noqa: E402
 
 N = 4096
+fork = "fork" in sys.argv[1:]
 cfg = lcfg.make_cfg()
-lcfg.config_go1(cfg)
+if "mc" in sys.argv[1:]:
+    lcfg.config_mini_cheetah(cfg)
+else:
+    lcfg.config_go1(cfg)
+    cfg.terrain.mesh_type = "trimesh"
+    cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]
+    cfg.terrain.curriculum = True
 cfg.env.num_envs = N
-cfg.terrain.mesh_type = "trimesh"
-cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]
-cfg.terrain.curriculum = True
-fork = len(sys.argv) > 1 and sys.argv[1] == "fork"
 env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=7, legacy_fork=fork))
 env.reset()
 a = torch.randn(N, 12, device="cuda:0") * 0.5
