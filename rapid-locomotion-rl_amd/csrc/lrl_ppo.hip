@@ -326,17 +326,20 @@ __device__ __forceinline__ void copy_rows(const float* __restrict__ src, int64_t
   }
 }
 
+// rollout head: ACT_ROWS rows per workgroup (4096 envs -> 512 workgroups: the storage row copies of the tile, the
+// bulk of the kernel's bytes, spread over every CU)
+constexpr int ACT_ROWS = 8, ACT_Q = HEAD_THREADS / ACT_ROWS;  // 32 thread groups per row
 __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
   constexpr int HP = 2 * HEAD_W + 1;
-  __shared__ float H[HEAD_ROWS][HP];
+  __shared__ float H[ACT_ROWS][HP];
   __shared__ float W4[MAX_ACT + 1][HEAD_W];
-  __shared__ float MU[HEAD_ROWS][MAX_ACT + 1];
-  __shared__ float VP[HEAD_ROWS][8];
+  __shared__ float MU[ACT_ROWS][MAX_ACT + 1];
+  __shared__ float VP[ACT_ROWS][ACT_Q];
   const int t = threadIdx.x, na = a.na;
-  const int r0 = blockIdx.x * HEAD_ROWS;
-  const int nrows = min(HEAD_ROWS, a.n - r0);
+  const int r0 = blockIdx.x * ACT_ROWS;
+  const int nrows = min(ACT_ROWS, a.n - r0);
   {
-    constexpr int NV = HEAD_ROWS * 2 * HEAD_W / 4 / HEAD_THREADS;
+    constexpr int NV = ACT_ROWS * 2 * HEAD_W / 4 / HEAD_THREADS;
     float4 v[NV];
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
@@ -356,14 +359,14 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
   }
   __syncthreads();
   {
-    const int r = t & (HEAD_ROWS - 1), q = t / HEAD_ROWS;
-    for (int j = q; j < na; j += 8) {
+    const int r = t & (ACT_ROWS - 1), q = t / ACT_ROWS;
+    for (int j = q; j < na; j += ACT_Q) {
       float s = 0.f;
       for (int k = 0; k < HEAD_W; ++k) s = fmaf(H[r][k], W4[j][k], s);
       MU[r][j] = s + a.b4a[j];
     }
     float s = 0.f;
-    for (int k = q * (HEAD_W / 8); k < (q + 1) * (HEAD_W / 8); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
+    for (int k = q * (HEAD_W / ACT_Q); k < (q + 1) * (HEAD_W / ACT_Q); ++k) s = fmaf(H[r][HEAD_W + k], W4[na][k], s);
     VP[r][q] = s;
   }
   __syncthreads();
@@ -399,8 +402,14 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
     const int g = r0 + t;
     float lp = 0.f;
     for (int j = 0; j < na; ++j) lp += MU[t][j];
-    const float v = (((VP[t][0] + VP[t][1]) + (VP[t][2] + VP[t][3])) + ((VP[t][4] + VP[t][5]) + (VP[t][6] + VP[t][7]))) +
-                    a.b4c[0];
+    float vs[ACT_Q];
+#pragma unroll
+    for (int q = 0; q < ACT_Q; ++q) vs[q] = VP[t][q];
+#pragma unroll
+    for (int w = ACT_Q / 2; w >= 1; w /= 2)  // pairwise tree, fixed order
+#pragma unroll
+      for (int q = 0; q < w; ++q) vs[q] = vs[2 * q] + vs[2 * q + 1];
+    const float v = vs[0] + a.b4c[0];
     if (a.values) a.values[g] = v;
     if (a.logp) a.logp[g] = lp;
     if (a.do_store) {
@@ -866,7 +875,7 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   ah.actions = actions; ah.mu = mu; ah.values = values; ah.logp = logp;
   if (store) ah.store = *store;
   ah.store_row = store_row; ah.do_store = store ? 1 : 0;
-  hipLaunchKernelGGL(act_head_kernel, dim3((n + HEAD_ROWS - 1) / HEAD_ROWS), dim3(HEAD_THREADS), 0, st, ah);
+  hipLaunchKernelGGL(act_head_kernel, dim3((n + ACT_ROWS - 1) / ACT_ROWS), dim3(HEAD_THREADS), 0, st, ah);
   return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act: launch failed");
 }
 
