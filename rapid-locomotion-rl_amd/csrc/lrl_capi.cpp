@@ -219,10 +219,12 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   HIPCHECK(hipMemcpy(s->d_body_leg, model->body_leg, sizeof(int32_t) * LRL_MAX_BODIES, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(s->d_body_link, model->body_link, sizeof(int32_t) * LRL_MAX_BODIES, hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy(s->d_foot_xyz, model->foot_xyz, sizeof(float) * 12, hipMemcpyHostToDevice));
-  // env step kernel LDS: 16 envs per workgroup (4 lanes each): leg blocks + contact rows, or the obs tiles
-  int lds_contacts = (4 * 51 + model->num_spheres * 67) * 16 * 4;  // LEGF, NSF of lrl_env.hip
-  if (params->terrain_mesh) lds_contacts += 16 * 64 * 16;  // terrain query vertex block, float4 [16][64 lanes]
-  int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * 16 * 4;  // obs / priv tiles + reward rows
+  // env step kernel LDS: LRL_ENV_LANES / 4 envs per workgroup (4 lanes each): leg blocks + contact rows, or the
+  // obs tiles
+  const int wg_envs = LRL_ENV_LANES / 4;
+  int lds_contacts = (4 * 51 + model->num_spheres * 67) * wg_envs * 4;  // LEGF, NSF of lrl_env.hip
+  if (params->terrain_mesh) lds_contacts += 16 * LRL_ENV_LANES * 16;  // terrain query vertex block, float4 [16][lanes]
+  int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * wg_envs * 4;  // obs / priv tiles + reward rows
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
   if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);
   HIPCHECK(lrl_env_kernel_setup(s->lds_bytes));

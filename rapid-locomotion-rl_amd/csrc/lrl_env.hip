@@ -25,14 +25,14 @@
 #include "../../include/lrl_philox.h"
 #include "lrl_kparams.h"
 
-#define WAVE 64
+#define BLOCK LRL_ENV_LANES  // lanes per workgroup (one wave; see lrl_kparams.h)
 // Quad layout: 4 lanes per env (lane & 3 = the leg it owns), 16 envs per single-wave workgroup.  The leg
 // work (kinematics, composite inertias, leg blocks, RNEA, contact detection and Delassus rows of the leg's
 // spheres, warm-start impulses) runs leg-parallel; the base quantities are summed over the 4 lanes with
 // cross-lane shuffles; the Gauss-Seidel sweep and the integration run redundantly in the 4 lanes (so
 // every lane holds the full env state); post-physics runs in lane 0 of each env.
 #define QL 4
-#define ENVS (WAVE / QL)
+#define ENVS (BLOCK / QL)
 #define NSF 67  // LDS fields per contact sphere (map above contact_setup)
 
 namespace lrl {
@@ -364,7 +364,7 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) tv[(4 * a + b) * WAVE + lane] = V[a][b];
+    for (int b = 0; b < 4; ++b) tv[(4 * a + b) * BLOCK + lane] = V[a][b];
   float best = 3.0e38f;
   V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
   bool bface = true;
@@ -376,7 +376,7 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
       const int c = k >> 1, di = c / 3, dj = c - 3 * di;
       const int ia = 4 * di + dj;  // v(i,j) in the block
       const int ib = (k & 1) ? ia + 4 : ia + 5, ic = (k & 1) ? ia + 5 : ia + 1;
-      const float4 fa = tv[ia * WAVE + lane], fb = tv[ib * WAVE + lane], fc = tv[ic * WAVE + lane];
+      const float4 fa = tv[ia * BLOCK + lane], fb = tv[ib * BLOCK + lane], fc = tv[ic * BLOCK + lane];
       const V3 va = v3(fa.x, fa.y, fa.z), b = v3(fb.x, fb.y, fb.z), cv = v3(fc.x, fc.y, fc.z);
       const V3 nf = cross(b - va, cv - va);
       const float a2 = dot(nf, nf);
@@ -573,18 +573,31 @@ __device__ __forceinline__ uint64_t quad_or(uint64_t v) {
 __device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, float mu, int q, float& vo0, float& vo1) {
   const int L = lsel < 0 ? 0 : lsel;
   const bool hj = q < 3;
-  // lane 3 reads finite neighbouring fields and zeroes them by selection (no divergent branches)
-  const float yq = hj ? M.leg(L, 45 + q) + M.leg(L, 48 + q) : 0.f;
-  float u[3];
+  const int qh = hj ? q : 2;  // lane 3 reads lane 2's fields and zeroes them by selection (no divergent branches)
+  // every read of the update is issued before any compute or store: one LDS round trip per update instead of
+  // one per row (a conditional read becomes an exec-masked branch with its own lgkmcnt(0) wait)
+  float g0[3], g1[3], hv[3], z0[3], z1[3], ev[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    float a = M.sph(s, SF_G + 6 * d + q) * vo0 + M.sph(s, SF_G + 6 * d + q + 4) * vo1;
-    a += (hj ? M.sph(s, SF_H + 3 * d + q) : 0.f) * yq;
-    u[d] = quad_sum(a);
+    g0[d] = M.sph(s, SF_G + 6 * d + q);
+    g1[d] = M.sph(s, SF_G + 6 * d + q + 4);
+    hv[d] = M.sph(s, SF_H + 3 * d + qh);
+    z0[d] = M.sph(s, SF_Z + 6 * d + q);
+    z1[d] = M.sph(s, SF_Z + 6 * d + q + 4);
+    ev[d] = M.sph(s, SF_E + 3 * d + qh);
   }
+  const float y45 = M.leg(L, 45 + qh), y48 = M.leg(L, 48 + qh);
   const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
   const float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
   const float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
+  const float yq = hj ? y45 + y48 : 0.f;
+  float u[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float a = g0[d] * vo0 + g1[d] * vo1;
+    a += (hj ? hv[d] : 0.f) * yq;
+    u[d] = quad_sum(a);
+  }
   const float ln = fmaxf(ln0 - (u[0] - b) * iWnn, 0.f);
   const float dn = ln - ln0;
   const float ut1 = u[1] + Wt1n * dn, ut2 = u[2] + Wt2n * dn;
@@ -597,10 +610,10 @@ __device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, flo
   M.sph(s, 11) = lt1;
   M.sph(s, 12) = lt2;
   const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
-  vo0 += dn * M.sph(s, SF_Z + q) + dt1 * M.sph(s, SF_Z + 6 + q) + dt2 * M.sph(s, SF_Z + 12 + q);
-  const float d1 = dn * M.sph(s, SF_Z + q + 4) + dt1 * M.sph(s, SF_Z + 10 + q) + dt2 * M.sph(s, SF_Z + 16 + q);
+  vo0 += dn * z0[0] + dt1 * z0[1] + dt2 * z0[2];
+  const float d1 = dn * z1[0] + dt1 * z1[1] + dt2 * z1[2];
   vo1 = q < 2 ? vo1 + d1 : 0.f;
-  if (hj) M.leg(L, 48 + q) += dn * M.sph(s, SF_E + q) + dt1 * M.sph(s, SF_E + 3 + q) + dt2 * M.sph(s, SF_E + 6 + q);
+  if (hj) M.leg(L, 48 + q) = y48 + (dn * ev[0] + dt1 * ev[1] + dt2 * ev[2]);
 }
 
 // lane of the quad that owns sphere s: its leg, or round-robin for the base spheres
@@ -1098,7 +1111,7 @@ __device__ __forceinline__ void priv_row(const lrl_env_params& P, const KState& 
 }
 
 template <bool TERR>
-__global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restrict__ K, KState S,
+__global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restrict__ K, KState S,
                                                         const float* __restrict__ actions_in, uint32_t flags,
                                                         int64_t step_counter) {
 #ifdef LRL_ENV_PROFILE
@@ -1535,9 +1548,9 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
   const size_t row0 = (size_t)blockIdx.x * ENVS;
   {
     float* og = S.obs + row0 * NO;
-    for (int i = lane; i < ENVS * NO; i += WAVE) og[i] = otile[i];
+    for (int i = lane; i < ENVS * NO; i += BLOCK) og[i] = otile[i];
     float* pgp = S.priv + row0 * LRL_NUM_PRIV;
-    for (int i = lane; i < ENVS * LRL_NUM_PRIV; i += WAVE) pgp[i] = ptile[i];
+    for (int i = lane; i < ENVS * LRL_NUM_PRIV; i += BLOCK) pgp[i] = ptile[i];
   }
   if (flags & LRL_STEP_HISTORY) {
     const int H = K->num_history * NO;
@@ -1549,7 +1562,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
       const int H2 = H >> 1, S2 = (H - NO) >> 1, NO2 = NO >> 1;
       float2* hg2 = reinterpret_cast<float2*>(S.hist + row0 * H);
       const float2* ot2 = reinterpret_cast<const float2*>(otile);
-      for (int c0 = 0; c0 < H2; c0 += WAVE) {
+      for (int c0 = 0; c0 < H2; c0 += BLOCK) {
         const int k2 = c0 + lane;
         float2 v[ENVS];
 #pragma unroll
@@ -1562,7 +1575,7 @@ __global__ __launch_bounds__(WAVE) void env_step_kernel(const KParams* __restric
       }
     } else {
       float* hg = S.hist + row0 * H;
-      for (int i0 = 0; i0 < ENVS * H; i0 += WAVE) {
+      for (int i0 = 0; i0 < ENVS * H; i0 += BLOCK) {
         const int i = i0 + lane;
         const int r = i / H, k = i - r * H;
         float v = 0.f;
@@ -1674,10 +1687,10 @@ extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int
                                           uint32_t flags, int64_t step_counter, int terrain_mesh, hipStream_t stream) {
   int blocks = S->stride / ENVS;
   if (terrain_mesh)
-    hipLaunchKernelGGL(lrl::env_step_kernel<true>, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions, flags,
+    hipLaunchKernelGGL(lrl::env_step_kernel<true>, dim3(blocks), dim3(BLOCK), lds_bytes, stream, K, *S, actions, flags,
                        step_counter);
   else
-    hipLaunchKernelGGL(lrl::env_step_kernel<false>, dim3(blocks), dim3(WAVE), lds_bytes, stream, K, *S, actions,
+    hipLaunchKernelGGL(lrl::env_step_kernel<false>, dim3(blocks), dim3(BLOCK), lds_bytes, stream, K, *S, actions,
                        flags, step_counter);
   return hipGetLastError();
 }

@@ -7,6 +7,14 @@
 
 #include "../../include/lrl.h"
 
+// Lanes per env-step workgroup (4 lanes per env).  A workgroup is one wave; with 4096 envs, 64 lanes give 256
+// waves (one per CU: three of each CU's four SIMDs idle), 32 lanes give 512 and 16 give 1024 (one per SIMD).
+// The kernel is bound by each env's dependent chain, and a wave's instruction stream costs the same whatever
+// its active-lane count, so fewer envs per wave spreads the same chains over more SIMDs.
+#ifndef LRL_ENV_LANES
+#define LRL_ENV_LANES 64
+#endif
+
 struct KLeg {
   float xyz[3][3];   // joint origin in the parent frame
   float rfix[3][9];  // fixed joint-origin rotation (row-major)

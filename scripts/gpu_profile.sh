@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 rm -rf /tmp/lrlprof && mkdir -p /tmp/lrlprof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/lrlprof/trace -o run -- \
-  python3 "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/trace.log" 2>&1
+  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-secondary > "$OUT/trace.log" 2>&1
 find /tmp/lrlprof/trace -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 KT=$(find /tmp/lrlprof/trace -name "*kernel_trace.csv" | head -n 1)
 python3 "$ROOT/scripts/trace_reduce.py" "$KT" > "$OUT/kernel_by_grid.csv"
