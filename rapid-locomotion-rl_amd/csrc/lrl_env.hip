@@ -435,16 +435,23 @@ __device__ __forceinline__ void contact_frame(V3 n, V3& t1, V3& t2) {
 #define SF_Z 40
 #define SF_E 58
 
-// apply a world-frame impulse change dl = (n, t1, t2) of sphere s (leg lsel) to v_b and Y_lsel
+// apply a world-frame impulse change dl = (n, t1, t2) of sphere s (leg lsel) to v_b and Y_lsel (every read
+// before the first store, so the rows arrive in one LDS round trip)
 __device__ __forceinline__ void apply_impulse(const Lds& M, int s, int lsel, float dn, float dt1, float dt2,
                                               float* vb) {
+  const int L = lsel < 0 ? 0 : lsel;
+  float z[18], ev[9], y[3];
 #pragma unroll
-  for (int r = 0; r < 6; ++r)
-    vb[r] += dn * M.sph(s, SF_Z + r) + dt1 * M.sph(s, SF_Z + 6 + r) + dt2 * M.sph(s, SF_Z + 12 + r);
+  for (int k = 0; k < 18; ++k) z[k] = M.sph(s, SF_Z + k);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) ev[k] = M.sph(s, SF_E + k);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) y[j] = M.leg(L, 48 + j);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) vb[r] += dn * z[r] + dt1 * z[6 + r] + dt2 * z[12 + r];
   if (lsel >= 0) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
-      M.leg(lsel, 48 + j) += dn * M.sph(s, SF_E + j) + dt1 * M.sph(s, SF_E + 3 + j) + dt2 * M.sph(s, SF_E + 6 + j);
+    for (int j = 0; j < 3; ++j) M.leg(lsel, 48 + j) = y[j] + (dn * ev[j] + dt1 * ev[3 + j] + dt2 * ev[6 + j]);
   }
 }
 
@@ -454,15 +461,31 @@ __device__ __forceinline__ void apply_impulse(const Lds& M, int s, int lsel, flo
 // is dead after the rows are built) for the contact-force pass.  Flat ground: n = z, t1 = x, t2 = y.
 template <bool TERR>
 __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, const M3& R, int s, int lsel, int link) {
+  // every LDS read up front (the point, the leg's joint axes / origins, K and D^-1; base spheres read leg 0's
+  // and discard them by selection), every store at the end: one round trip instead of one per dependent read
+  const int L = lsel < 0 ? 0 : lsel;
+  const bool onleg = lsel >= 0;
   const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
-  V3 c[3] = {v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f)};
-  if (lsel >= 0) leg_dirs(M, lsel, link, x, c);
+  V3 nw = v3(0.f, 0.f, 1.f);
+  if constexpr (TERR) nw = v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5));
+  V3 ax[3], og[3];
+  float kx[3][6], di[6];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    ax[j] = M.a(L, j);
+    og[j] = M.o(L, j);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) kx[j][r] = M.Kx(L, j, r);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) di[k] = M.Di(L, k);
+  V3 c[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) c[j] = (onleg && j <= link) ? cross(ax[j], x - og[j]) : v3(0.f, 0.f, 0.f);
   float g[3][6], z[3][6];
   V3 h[3], ev[3];
   V3 fr[3];  // contact frame in base coordinates
-  V3 nw = v3(0.f, 0.f, 1.f);
   if constexpr (TERR) {
-    nw = v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5));
     V3 t1, t2;
     contact_frame(nw, t1, t2);
     fr[0] = mulT(R, nw);
@@ -479,21 +502,14 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
     const V3 xn = cross(x, nd);
     g[d][0] = xn.x; g[d][1] = xn.y; g[d][2] = xn.z; g[d][3] = nd.x; g[d][4] = nd.y; g[d][5] = nd.z;
     h[d] = v3(dot(c[0], nd), dot(c[1], nd), dot(c[2], nd));
-    ev[d] = v3(0.f, 0.f, 0.f);
-    if (lsel >= 0) {
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-        g[d][r] -= M.Kx(lsel, 0, r) * h[d].x + M.Kx(lsel, 1, r) * h[d].y + M.Kx(lsel, 2, r) * h[d].z;
-      ev[d] = di_mul(M, lsel, h[d]);
-    }
-    sym6mul(Si, g[d], z[d]);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      M.sph(s, SF_G + 6 * d + r) = g[d][r];
-      M.sph(s, SF_Z + 6 * d + r) = z[d][r];
+      const float gk = g[d][r] - (kx[0][r] * h[d].x + kx[1][r] * h[d].y + kx[2][r] * h[d].z);
+      g[d][r] = onleg ? gk : g[d][r];
     }
-    M.sph(s, SF_H + 3 * d) = h[d].x; M.sph(s, SF_H + 3 * d + 1) = h[d].y; M.sph(s, SF_H + 3 * d + 2) = h[d].z;
-    M.sph(s, SF_E + 3 * d) = ev[d].x; M.sph(s, SF_E + 3 * d + 1) = ev[d].y; M.sph(s, SF_E + 3 * d + 2) = ev[d].z;
+    const V3 e = sym3mul(di[0], di[1], di[2], di[3], di[4], di[5], h[d]);
+    ev[d] = onleg ? e : v3(0.f, 0.f, 0.f);
+    sym6mul(Si, g[d], z[d]);
   }
   float W[3][3];
 #pragma unroll
@@ -508,6 +524,16 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
       W[e][d] = w;
     }
   const float id = 1.f / (W[1][1] * W[2][2] - W[1][2] * W[2][1]);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      M.sph(s, SF_G + 6 * d + r) = g[d][r];
+      M.sph(s, SF_Z + 6 * d + r) = z[d][r];
+    }
+    M.sph(s, SF_H + 3 * d) = h[d].x; M.sph(s, SF_H + 3 * d + 1) = h[d].y; M.sph(s, SF_H + 3 * d + 2) = h[d].z;
+    M.sph(s, SF_E + 3 * d) = ev[d].x; M.sph(s, SF_E + 3 * d + 1) = ev[d].y; M.sph(s, SF_E + 3 * d + 2) = ev[d].z;
+  }
   M.sph(s, 3) = 1.f / W[0][0];
   M.sph(s, 4) = W[1][0];
   M.sph(s, 5) = W[2][0];
@@ -702,7 +728,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   uint64_t cand = 0;
   float hwin = 0.f;
   if constexpr (TERR) hwin = terrain_window_max(K, st.pos);
-  auto detect = [&](int s, V3 x, int lsel, int link) {
+  // aa / oo: the carrying leg's joint axes / origins in registers (the leg pass has them; no LDS read-back)
+  auto detect = [&](int s, V3 x, int lsel, int link, const V3* aa, const V3* oo) {
     if constexpr (TERR) {
       const V3 pw = v3(st.pos[0], st.pos[1], pz) + mul(R, x);
       M.sph(s, 0) = x.x;
@@ -722,10 +749,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.sph(s, 2) = x.z;
       V3 u = cross(wb, x) + vb;
       if (lsel >= 0) {
-        V3 c[3];
-        leg_dirs(M, lsel, link, x, c);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) u = u + pick12(st.qd, 3 * lsel + j) * c[j];
+        for (int j = 0; j < 3; ++j)
+          if (j <= link) u = u + pick12(st.qd, 3 * lsel + j) * cross(aa[j], x - oo[j]);
       }
       const float u0 = dot(Rz, u);
       float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
@@ -734,7 +760,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     }
   };
   for (int s = ql; s < K->base_sph_end; s += QL)
-    detect(s, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2]), -1, 0);
+    detect(s, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2]), -1, 0, nullptr, nullptr);
 
   // ---- this lane's leg ----
   SI Aleg;     // composite inertia of the leg about the base origin
@@ -748,6 +774,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     V3 op = v3(0.f, 0.f, 0.f);
     SI Ij[3];
     SV S[3];
+    V3 aa[3], oo[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       M3 Rf;
@@ -760,11 +787,14 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.leg(l, 3 * j) = a.x; M.leg(l, 3 * j + 1) = a.y; M.leg(l, 3 * j + 2) = a.z;
       M.leg(l, 9 + 3 * j) = o.x; M.leg(l, 9 + 3 * j + 1) = o.y; M.leg(l, 9 + 3 * j + 2) = o.z;
       S[j] = SV{a, cross(o, a)};
+      aa[j] = a;
+      oo[j] = o;
       const V3 c = o + mul(Rj, v3(kl.com[j][0], kl.com[j][1], kl.com[j][2]));
       Ij[j] = make_si(kl.mass[j], c, Rj, kl.inertia[j]);
       // contact detection for this link's spheres (needs only a_j', o_j' for j' <= j, already in LDS)
       for (int s = K->leg_sph_begin[l]; s < K->leg_sph_end[l]; ++s)
-        if (K->sph_link[s] == j) detect(s, o + mul(Rj, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2])), l, j);
+        if (K->sph_link[s] == j)
+          detect(s, o + mul(Rj, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2])), l, j, aa, oo);
       Rp = Rj;
       op = o;
     }
