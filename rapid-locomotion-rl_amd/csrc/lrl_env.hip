@@ -1585,23 +1585,32 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   if (flags & LRL_STEP_HISTORY) {
     const int H = K->num_history * NO;
     // in place: new[r][k] = old[r][k + NO] (k < H - NO) else obs[r][k - (H - NO)].  The wave's 16 rows are
-    // contiguous; a pass covers one 64-wide column block of every row (one 8-B pair per lane and row, 16
-    // loads in flight), all its loads before any of its stores, and column blocks run left to right, so a
-    // pass only reads pairs no earlier pass has written.
+    // contiguous; a pass covers HCW 64-wide column blocks of every row (8-B pairs), all its loads before any
+    // of its stores, and passes run left to right, so a pass only reads pairs no earlier pass has written.
     if (((H | NO) & 1) == 0) {
       const int H2 = H >> 1, S2 = (H - NO) >> 1, NO2 = NO >> 1;
       float2* hg2 = reinterpret_cast<float2*>(S.hist + row0 * H);
       const float2* ot2 = reinterpret_cast<const float2*>(otile);
-      for (int c0 = 0; c0 < H2; c0 += BLOCK) {
-        const int k2 = c0 + lane;
-        float2 v[ENVS];
+      // HCW column blocks per pass: HCW x 16 pairs per lane in flight (the physics registers are dead here), so
+      // the 630-float history takes 2 passes instead of 5 (each pass pays one HBM round trip)
+      constexpr int HCW = 3;
+      for (int c0 = 0; c0 < H2; c0 += HCW * BLOCK) {
+        float2 v[HCW][ENVS];
 #pragma unroll
-        for (int r = 0; r < ENVS; ++r)
-          if (k2 < H2) v[r] = k2 < S2 ? hg2[r * H2 + k2 + NO2] : ot2[r * NO2 + (k2 - S2)];
+        for (int w = 0; w < HCW; ++w) {
+          const int k2 = c0 + w * BLOCK + lane;
+#pragma unroll
+          for (int r = 0; r < ENVS; ++r)
+            if (k2 < H2) v[w][r] = k2 < S2 ? hg2[r * H2 + k2 + NO2] : ot2[r * NO2 + (k2 - S2)];
+        }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < ENVS; ++r)
-          if (k2 < H2) hg2[r * H2 + k2] = v[r];
+        for (int w = 0; w < HCW; ++w) {
+          const int k2 = c0 + w * BLOCK + lane;
+#pragma unroll
+          for (int r = 0; r < ENVS; ++r)
+            if (k2 < H2) hg2[r * H2 + k2] = v[w][r];
+        }
       }
     } else {
       float* hg = S.hist + row0 * H;
