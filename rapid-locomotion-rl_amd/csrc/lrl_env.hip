@@ -1116,7 +1116,8 @@ __device__ __forceinline__ void obs_noise_clip(const lrl_env_params& P, const KS
       for (int k = 0; k < 4; ++k) {
         int i = i0 + k;
         if (i < NO) {
-          float u = inject ? S.inj_noise[(size_t)e * NO + i] : lrl_u01(r.v[k]);
+          // (padded env slots e >= n read no injected row: the injected buffers hold n rows)
+          float u = inject ? (e < S.n ? S.inj_noise[(size_t)e * NO + i] : 0.5f) : lrl_u01(r.v[k]);
           ob[i] += (2.f * u - 1.f) * P.noise_vec[i];
         }
       }
@@ -1352,7 +1353,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter, (LRL_RNG_DR << 16) ^ (uint32_t)(step_counter >> 32), 0,
                              S.seed);
     if (P.randomize_motor_strength) {
-      float u = inject ? S.inj_dr[e] : lrl_u01(r.v[k]);
+      float u = inject ? (valid ? S.inj_dr[e] : 0.5f) : lrl_u01(r.v[k]);
       k++;
       float v = u * (P.motor_strength_range[1] - P.motor_strength_range[0]) + P.motor_strength_range[0];
 #pragma unroll
