@@ -172,12 +172,17 @@ struct Lds {
   float* base;     // leg blocks, then contact rows: [field][env slot] columns shared by the env's 4 lanes
   int sph_off;     // field offset of the contact rows
   int es;          // env slot of this lane inside the workgroup
-  __device__ __forceinline__ float& leg(int l, int f) const { return base[(l * LEGF + f) * ENVS + es]; }
-  __device__ __forceinline__ float& sph(int s, int f) const { return base[(sph_off + s * NSF + f) * ENVS + es]; }
+  // field f of a row = row pointer + f * ENVS (a constant f folds into the ds_read / ds_write immediate offset)
+  __device__ __forceinline__ float& leg(int l, int f) const { return lp(l)[f * ENVS]; }
+  __device__ __forceinline__ float& sph(int s, int f) const { return sp(s)[f * ENVS]; }
   __device__ __forceinline__ V3 a(int l, int j) const { return v3(leg(l, 3 * j), leg(l, 3 * j + 1), leg(l, 3 * j + 2)); }
   __device__ __forceinline__ V3 o(int l, int j) const {
     return v3(leg(l, 9 + 3 * j), leg(l, 9 + 3 * j + 1), leg(l, 9 + 3 * j + 2));
   }
+  // column pointers: field f of the row is p[f * ENVS] (constant offsets fold into the ds_read / ds_write
+  // immediate instead of one address computation per field)
+  __device__ __forceinline__ float* sp(int s) const { return base + (sph_off + s * NSF) * ENVS + es; }
+  __device__ __forceinline__ float* lp(int l) const { return base + l * LEGF * ENVS + es; }
   __device__ __forceinline__ float Kx(int l, int j, int r) const { return leg(l, 18 + 6 * j + r); }
   __device__ __forceinline__ float Di(int l, int k) const { return leg(l, 36 + k); }
 };
@@ -601,21 +606,26 @@ __device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, flo
   const bool hj = q < 3;
   const int qh = hj ? q : 2;  // lane 3 reads lane 2's fields and zeroes them by selection (no divergent branches)
   // every read of the update is issued before any compute or store: one LDS round trip per update instead of
-  // one per row (a conditional read becomes an exec-masked branch with its own lgkmcnt(0) wait)
+  // one per row (a conditional read becomes an exec-masked branch with its own lgkmcnt(0) wait); the per-lane
+  // columns are addressed from three row pointers so the field offsets are instruction immediates
+  float* const rs = M.sp(s);
+  const float* const rq = rs + q * ENVS;
+  const float* const rh = rs + qh * ENVS;
+  float* const lg = M.lp(L) + qh * ENVS;
   float g0[3], g1[3], hv[3], z0[3], z1[3], ev[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    g0[d] = M.sph(s, SF_G + 6 * d + q);
-    g1[d] = M.sph(s, SF_G + 6 * d + q + 4);
-    hv[d] = M.sph(s, SF_H + 3 * d + qh);
-    z0[d] = M.sph(s, SF_Z + 6 * d + q);
-    z1[d] = M.sph(s, SF_Z + 6 * d + q + 4);
-    ev[d] = M.sph(s, SF_E + 3 * d + qh);
+    g0[d] = rq[(SF_G + 6 * d) * ENVS];
+    g1[d] = rq[(SF_G + 6 * d + 4) * ENVS];
+    hv[d] = rh[(SF_H + 3 * d) * ENVS];
+    z0[d] = rq[(SF_Z + 6 * d) * ENVS];
+    z1[d] = rq[(SF_Z + 6 * d + 4) * ENVS];
+    ev[d] = rh[(SF_E + 3 * d) * ENVS];
   }
-  const float y45 = M.leg(L, 45 + qh), y48 = M.leg(L, 48 + qh);
-  const float iWnn = M.sph(s, 3), Wt1n = M.sph(s, 4), Wt2n = M.sph(s, 5);
-  const float i11 = M.sph(s, 6), i12 = M.sph(s, 7), i22 = M.sph(s, 8), b = M.sph(s, 9);
-  const float ln0 = M.sph(s, 10), lt10 = M.sph(s, 11), lt20 = M.sph(s, 12);
+  const float y45 = lg[45 * ENVS], y48 = lg[48 * ENVS];
+  const float iWnn = rs[3 * ENVS], Wt1n = rs[4 * ENVS], Wt2n = rs[5 * ENVS];
+  const float i11 = rs[6 * ENVS], i12 = rs[7 * ENVS], i22 = rs[8 * ENVS], b = rs[9 * ENVS];
+  const float ln0 = rs[10 * ENVS], lt10 = rs[11 * ENVS], lt20 = rs[12 * ENVS];
   const float yq = hj ? y45 + y48 : 0.f;
   float u[3];
 #pragma unroll
@@ -632,14 +642,14 @@ __device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, flo
   const float sc = nt2 > lim * lim ? (nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f) : 1.f;
   lt1 *= sc;
   lt2 *= sc;
-  M.sph(s, 10) = ln;
-  M.sph(s, 11) = lt1;
-  M.sph(s, 12) = lt2;
+  rs[10 * ENVS] = ln;
+  rs[11 * ENVS] = lt1;
+  rs[12 * ENVS] = lt2;
   const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
   vo0 += dn * z0[0] + dt1 * z0[1] + dt2 * z0[2];
   const float d1 = dn * z1[0] + dt1 * z1[1] + dt2 * z1[2];
   vo1 = q < 2 ? vo1 + d1 : 0.f;
-  if (hj) M.leg(L, 48 + q) = y48 + (dn * ev[0] + dt1 * ev[1] + dt2 * ev[2]);
+  if (hj) lg[48 * ENVS] = y48 + (dn * ev[0] + dt1 * ev[1] + dt2 * ev[2]);
 }
 
 // lane of the quad that owns sphere s: its leg, or round-robin for the base spheres
