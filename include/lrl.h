@@ -254,6 +254,16 @@ int32_t lrl_sim_reset_idx_ex(lrl_sim* sim, const int32_t* env_ids, int32_t n, in
  * last_actions / last_dof_vel / last_root_vel as post_physics_step does after reset_idx (:182-184), and with
  * flags & LRL_STEP_HISTORY rewrite the newest history slot (the HistoryWrapper shift of that step). */
 int32_t lrl_sim_observe_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, uint32_t flags, void* stream);
+/* _update_terrain_curriculum (legged_robot.py:793-818) for the envs `env_ids` in one launch: distance = |root xy -
+ * env origin xy|; move up when distance > half_env_length, down when distance < |command xy| * episode_length_s *
+ * 0.5 and not up; a level >= max_level becomes rand_levels[t] (the caller's torch.randint_like draw, one per id),
+ * others are clipped at 0; the env origin becomes terrain_origins[level][type].  levels / types: int64 [num_envs]
+ * device arrays (the caller's terrain_levels / terrain_types), terrain_origins: f32 [rows][cols][3]; an index
+ * outside rows / cols is an error of the caller (clamped on the device: the kernel never reads out of bounds). */
+int32_t lrl_sim_terrain_curriculum(lrl_sim* sim, const int32_t* env_ids, int32_t n, int64_t* levels,
+                                   const int64_t* types, const int64_t* rand_levels, const float* terrain_origins,
+                                   int32_t rows, int32_t cols, float half_env_length, float episode_length_s,
+                                   int32_t max_level, void* stream);
 /* common_step_counter (legged_robot.py:153); lrl_sim_step increments it before the launch */
 int32_t lrl_sim_set_step_counter(lrl_sim* sim, int64_t counter);
 int32_t lrl_sim_set_root_state_indexed(lrl_sim* sim, const float* root /*[N,13] full tensor*/,

@@ -55,6 +55,32 @@ __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int3
   S.reset[e] = 1;
 }
 
+// _update_terrain_curriculum (legged_robot.py:793-818), one thread per reset env.  Float32 ops in torch's order
+// without contraction (torch.norm of a 2-vector: x0*x0 + x1*x1, then sqrt; the command term (|c| * T) * 0.5).
+__global__ void terrain_curriculum_kernel(KState S, const int32_t* __restrict__ ids, int32_t n, int64_t* levels,
+                                          const int64_t* __restrict__ types, const int64_t* __restrict__ rnd,
+                                          const float* __restrict__ torig, int32_t rows, int32_t cols, float half,
+                                          float ep_len_s, int32_t max_level) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int e = ids[t];
+  if (e < 0 || e >= S.n) return;
+  const int N = S.stride;
+  const float dx = __fsub_rn(S.root[e], S.env_origins[e]), dy = __fsub_rn(S.root[N + e], S.env_origins[N + e]);
+  const float dist = __fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+  const float c0 = S.commands[e], c1 = S.commands[N + e];
+  const float cn = __fsqrt_rn(__fadd_rn(__fmul_rn(c0, c0), __fmul_rn(c1, c1)));
+  const bool up = dist > half;
+  const bool down = dist < __fmul_rn(__fmul_rn(cn, ep_len_s), 0.5f) && !up;
+  int64_t lv = levels[e] + (up ? 1 : 0) - (down ? 1 : 0);
+  lv = lv >= max_level ? rnd[t] : (lv < 0 ? 0 : lv);
+  levels[e] = lv;
+  const int64_t li = lv < 0 ? 0 : (lv >= rows ? rows - 1 : lv);
+  const int64_t ty = types[e] < 0 ? 0 : (types[e] >= cols ? cols - 1 : types[e]);
+  const float* o = torig + (li * cols + ty) * 3;
+  for (int c = 0; c < 3; ++c) S.env_origins[c * N + e] = o[c];
+}
+
 // gym.set_actor_root_state_tensor_indexed: rows `ids` of an AoS [n,13] source
 __global__ void set_root_kernel(KState S, const float* __restrict__ src, const int32_t* __restrict__ ids, int32_t n) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -205,6 +231,14 @@ hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* id
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, root_mode, xo, yo,
                      counter);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_terrain_curriculum(const KState* S, const int32_t* ids, int32_t n, int64_t* levels,
+                                         const int64_t* types, const int64_t* rnd, const float* torig, int32_t rows,
+                                         int32_t cols, float half, float ep_len_s, int32_t max_level, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lrl::terrain_curriculum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, *S, ids, n, levels,
+                     types, rnd, torig, rows, cols, half, ep_len_s, max_level);
   return hipGetLastError();
 }
 hipError_t lrl_launch_set_root(const KState* S, const float* src, const int32_t* ids, int32_t n, hipStream_t st) {

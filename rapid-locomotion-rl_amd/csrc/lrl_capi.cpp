@@ -32,6 +32,9 @@ hipError_t lrl_env_kernel_setup(int lds_bytes);
 hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, int64_t,
                             hipStream_t);
 hipError_t lrl_launch_set_root(const KState*, const float*, const int32_t*, int32_t, hipStream_t);
+hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t, int64_t*, const int64_t*,
+                                         const int64_t*, const float*, int32_t, int32_t, float, float, int32_t,
+                                         hipStream_t);
 hipError_t lrl_launch_set_dof(const KState*, const float*, const float*, const int32_t*, int32_t, hipStream_t);
 hipError_t lrl_launch_rigid_body(const KParams*, const KState*, const int32_t*, const int32_t*, const float*,
                                  hipStream_t);
@@ -413,6 +416,18 @@ int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t 
   if (!s || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
   s->reset_counter += 1;
   HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, root_mode, xo, yo, s->reset_counter, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_terrain_curriculum(lrl_sim* s, const int32_t* ids, int32_t n, int64_t* levels, const int64_t* types,
+                                   const int64_t* rand_levels, const float* terrain_origins, int32_t rows,
+                                   int32_t cols, float half_env_length, float episode_length_s, int32_t max_level,
+                                   void* stream) {
+  if (!s || (n > 0 && (!ids || !levels || !types || !rand_levels || !terrain_origins)))
+    return fail(LRL_E_INVALID, "null argument");
+  if (n < 0 || rows <= 0 || cols <= 0) return fail(LRL_E_INVALID, "bad sizes");
+  HIPCHECK(lrl_launch_terrain_curriculum(&s->S, ids, n, levels, types, rand_levels, terrain_origins, rows, cols,
+                                         half_env_length, episode_length_s, max_level, (hipStream_t)stream));
   return 0;
 }
 

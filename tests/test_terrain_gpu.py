@@ -205,6 +205,33 @@ def test_rough_terrain_standing_and_curriculum():
     env.close()
 
 
+def test_native_terrain_curriculum_matches_reference():
+    """lrl_sim_terrain_curriculum (the one-launch _update_terrain_curriculum of a sim-backed env) on the
+    reference's fixture (tests/golden/terrain_curriculum.npz, the reference's randint_like draws injected):
+    levels and origins bit-exact, as the host torch form is in tests/test_terrain.py."""
+    import types
+    from lrl.env import LeggedRobotEnv
+    g = golden("terrain_curriculum.npz")
+    n = len(g["levels_in"])
+    env = LeggedRobotEnv("cuda:0", cfg=_rough_cfg(n, 2.0, **GOLDEN_TERRAIN), seed=5)
+    env.terrain_levels[:] = _dev(g["levels_in"], torch.long)
+    env.terrain_types[:] = _dev(g["types"], torch.long)
+    env.env_origins[:] = _dev(g["env_origins_in"])
+    env.root_states[:, :2] = _dev(g["root_xy"])
+    env.commands[:, :2] = _dev(g["commands_xy"])
+    draws = _dev(g["draws"], torch.long)
+    env._rand_levels = lambda like, high: draws[:len(like)]
+    cfg = types.SimpleNamespace(
+        terrain=types.SimpleNamespace(curriculum=True, env_length=float(g["env_length"]),
+                                      max_terrain_level=int(g["num_rows"]), terrain_origins=_dev(g["origins_table"])),
+        env=types.SimpleNamespace(episode_length_s=float(g["episode_length_s"])))
+    env._update_terrain_curriculum(_dev(g["ids"], torch.long), cfg)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(env.terrain_levels), g["levels_out"])
+    np.testing.assert_array_equal(_np(env.env_origins), g["env_origins_out"])
+    env.close()
+
+
 def test_perceptive_policy_trains_on_rough_terrain():
     """The base config's perceptive layout (observe_vel + 17 x 11 height scan = 235 observations, history
     15 x 235) end to end: upstream resets on the curriculum trimesh, one Runner.learn iteration through the
