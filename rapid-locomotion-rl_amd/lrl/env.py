@@ -78,6 +78,14 @@ class LeggedRobotEnv:
         # legacy_fork=False re-enables what the fork comments out: reset_idx inside step
         # for terminated / timed-out envs, command resampling every resampling_time and at resets
         self.legacy_fork = bool(legacy_fork)
+        # data-parallel ranks: with the upstream curricula reconnected, every rank applies the same
+        # command-curriculum update / sample to all ranks' reset envs (rank-major global order), so the replicas of
+        # the curriculum stay identical and a rank's envs draw what they would in one process holding every env
+        self._dist = None
+        if not self.legacy_fork:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                self._dist = dist
         self.device = torch.device(sim_device)
         if self.device.type != "cuda" or not torch.cuda.is_available():
             raise RuntimeError("LeggedRobotEnv runs on the GPU through liblrl.so; no CPU path exists")
@@ -346,10 +354,36 @@ class LeggedRobotEnv:
         high = np.array([c.lin_vel_x[1], c.lin_vel_y[1], c.ang_vel_yaw[1]])
         self.curriculum.set_to(low=low, high=high)
 
+    def _dist_count(self, k):
+        """Sum over ranks of a local count (one small all-reduce)."""
+        dist = self._dist
+        dev = self.device if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([k], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    def _dist_gather_rows(self, rows):
+        """All ranks' rows (float64 [k, m]) concatenated in rank order, and this rank's first row in it."""
+        dist = self._dist
+        dev = self.device if dist.get_backend() == "nccl" else "cpu"
+        world, rank = dist.get_world_size(), dist.get_rank()
+        cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        cnts = [int(c.item()) for c in cnts]
+        kmax = max(cnts)
+        if kmax == 0:
+            return rows[:0], 0
+        buf = torch.zeros(kmax, rows.shape[1], dtype=torch.float64, device=dev)
+        buf[:rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows, np.float64)).to(dev)
+        bufs = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(bufs, buf)
+        return np.concatenate([b[:c].cpu().numpy() for b, c in zip(bufs, cnts)]), sum(cnts[:rank])
+
     def resample_commands(self, env_ids, _ids_host=None):
         """_resample_commands (legged_robot.py:595-626); disconnected in the fork (Q3), callable here.
         ``_ids_host``: the same ids as a numpy array when the caller already has them on the host."""
-        if len(env_ids) == 0:
+        if len(env_ids) == 0 and self._dist is None:  # (ranks join the collective update with no envs of their own)
             return
         ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
         timesteps = int(self.cfg.commands.resampling_time / self.dt)
@@ -366,8 +400,18 @@ class LeggedRobotEnv:
         lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
         ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
         old_bins = self.env_command_bins[ids_np]
-        self.curriculum.update(old_bins, lin, ang, lin_thr, ang_thr, local_range=0.5)
-        new_cmds, new_bins = self.curriculum.sample(batch_size=len(ids_np))
+        if self._dist is None:
+            self.curriculum.update(old_bins, lin, ang, lin_thr, ang_thr, local_range=0.5)
+            new_cmds, new_bins = self.curriculum.sample(batch_size=len(ids_np))
+        else:  # the same update / draw on every rank over all ranks' envs, then this rank's rows
+            rows, off = self._dist_gather_rows(np.stack([old_bins.astype(np.float64), np.asarray(lin, np.float64),
+                                                         np.asarray(ang, np.float64)], 1))
+            if len(rows) == 0:
+                return
+            self.curriculum.update(rows[:, 0].astype(old_bins.dtype), rows[:, 1].astype(np.float32),
+                                   rows[:, 2].astype(np.float32), lin_thr, ang_thr, local_range=0.5)
+            new_cmds, new_bins = self.curriculum.sample(batch_size=len(rows))
+            new_cmds, new_bins = new_cmds[off:off + len(ids_np)], new_bins[off:off + len(ids_np)]
         self.env_command_bins[ids_np] = new_bins
         # commands[:, :3] = float32(cmds); commands[:, :2] *= (norm(commands[:, :2]) > 0.2): float32 on the host
         c = new_cmds.astype(np.float32)
@@ -395,7 +439,8 @@ class LeggedRobotEnv:
                 due = cached[1]  # known from the previous step's single device->host copy
             else:  # first step, or episode_length_buf written by a caller since
                 due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
-            if len(due):
+            # (with several ranks every rank takes part whenever any rank has envs to resample)
+            if (len(due) > 0) if self._dist is None else (self._dist_count(len(due)) > 0):
                 self.resample_commands(due, due.cpu().numpy() if cached is None else cached[2])
         self._sums_host = None  # the kernel below changes the command sums
         timer = self.kernel_timer
@@ -424,7 +469,7 @@ class LeggedRobotEnv:
             rst = code & 1
             ids_np = np.flatnonzero(rst)
             due_np = np.flatnonzero((code >> 1) & ((rst == 0) | (interval == 1)))
-            if len(ids_np):
+            if (len(ids_np) > 0) if self._dist is None else (self._dist_count(len(ids_np)) > 0):
                 ids = torch.from_numpy(ids_np).to(self.device)
                 self.reset_idx(ids, ids_np)
                 ids32 = ids.to(torch.int32).contiguous()
@@ -470,7 +515,7 @@ class LeggedRobotEnv:
         """legged_robot.py:227-290; train and eval envs (env id >= num_train_envs) go through their own cfg
         for the command curriculum (_call_train_eval, :456-469) and their own episode logging."""
         env_ids = torch.as_tensor(env_ids, device=self.device).long()
-        if len(env_ids) == 0:
+        if len(env_ids) == 0 and self._dist is None:  # (ranks join the collective curriculum steps with no envs)
             return
         self._due_next = None  # episode lengths change: the next step re-derives its resampling set
         n_tr = self.num_train_envs
@@ -481,9 +526,9 @@ class LeggedRobotEnv:
         if self.custom_origins:
             for ids, c in self._groups(env_ids):
                 self._update_terrain_curriculum(ids, c)
-        if len(tr):
+        if len(tr) or self._dist is not None:
             self.update_command_curriculum(tr, self.cfg)
-        if len(ev):
+        if len(ev) or (self._dist is not None and self.num_eval_envs):
             self.update_command_curriculum(ev, self.eval_cfg)
         if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
             self.resample_commands(env_ids, _ids_host)
@@ -551,12 +596,22 @@ class LeggedRobotEnv:
                                                    torch.clip(lv, 0))
         self.env_origins[env_ids] = t.terrain_origins[self.terrain_levels[env_ids], self.terrain_types[env_ids]]
 
+    def _ids_mean(self, values, env_ids):
+        """torch.mean(values[env_ids]); over all ranks' envs (sum and count all-reduced) with several ranks."""
+        if self._dist is None:
+            return torch.mean(values[env_ids])
+        dev = self.device if self._dist.get_backend() == "nccl" else "cpu"
+        t = torch.stack([values[env_ids].double().sum(), torch.tensor(float(len(env_ids)), dtype=torch.float64,
+                                                                       device=values.device)]).to(dev)
+        self._dist.all_reduce(t)
+        return (t[0] / t[1]).float().to(values.device)
+
     def update_command_curriculum(self, env_ids, cfg, episode_sums=None):
         """_update_command_curriculum_uniform (legged_robot.py:851-880)."""
         c = cfg.commands
         if c.command_curriculum and (self.common_step_counter % cfg.env.max_episode_length == 0):
             if self.reward_scales.get("tracking_lin_vel", 0) > 0:
-                m = torch.mean(self.episode_sums["tracking_lin_vel"][env_ids]) / cfg.env.max_episode_length
+                m = self._ids_mean(self.episode_sums["tracking_lin_vel"], env_ids) / cfg.env.max_episode_length
                 if m > c.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]:
                     cfg.command_ranges["lin_vel_x"][0] = np.clip(cfg.command_ranges["lin_vel_x"][0] - 0.2,
                                                                  -c.max_reverse_curriculum, 0.0)
@@ -564,7 +619,7 @@ class LeggedRobotEnv:
                                                                  c.max_forward_curriculum)
         if c.yaw_command_curriculum and (self.common_step_counter % cfg.env.max_episode_length == 0):
             if self.reward_scales.get("tracking_ang_vel", 0) > 0:
-                m = torch.mean(self.episode_sums["tracking_ang_vel"][env_ids]) / cfg.env.max_episode_length
+                m = self._ids_mean(self.episode_sums["tracking_ang_vel"], env_ids) / cfg.env.max_episode_length
                 if m > c.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]:
                     cfg.command_ranges["ang_vel_yaw"][0] = np.clip(cfg.command_ranges["ang_vel_yaw"][0] - 0.2,
                                                                    -c.max_yaw_curriculum, 0.0)

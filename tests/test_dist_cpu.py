@@ -89,3 +89,49 @@ def test_two_rank_update_keeps_replicas_identical():
     assert a[0] and b[0], "gradient all-reduce did not average"
     np.testing.assert_array_equal(a[1], b[1])  # identical replicas after 20 optimiser steps
     assert a[2] == b[2]                         # same adaptive learning rate on both ranks
+
+
+def _curriculum_rows_worker(rank, world, port, out):
+    import sys
+    import types
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "rapid-locomotion-rl_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lrl.env import LeggedRobotEnv
+    from lrl.curriculum import RewardThresholdCurriculum
+    stub = types.SimpleNamespace(_dist=dist, device="cpu")
+    counts = [3, 0, 5]  # a rank with no resampled envs still joins
+    k = counts[rank]
+    rows = np.stack([np.arange(k) + 10 * rank, np.full(k, 0.5 + rank), np.full(k, -1.0 - rank)], 1).astype(np.float64)
+    got, off = LeggedRobotEnv._dist_gather_rows(stub, rows)
+    total = LeggedRobotEnv._dist_count(stub, k)
+    # every rank then runs the same curriculum update / draw over the gathered rows and keeps its slice
+    cur = RewardThresholdCurriculum(seed=100, x_vel=(-1, 1, 5), y_vel=(-0.6, 0.6, 2), yaw_vel=(-1, 1, 5))
+    cur.weights[:] = 1.0
+    cmds, bins = cur.sample(batch_size=len(got))
+    out[rank] = (got, off, total, cmds[off:off + k], bins[off:off + k])
+    dist.destroy_process_group()
+
+
+def test_curriculum_rows_gathered_in_rank_order():
+    """LeggedRobotEnv._dist_gather_rows / _dist_count (the multi-rank command curriculum) over
+    gloo with 3 ranks of 3 / 0 / 5 rows: every rank sees all rows in rank order and its own offset, so slicing
+    one shared draw gives each rank the rows a single process would have drawn for its envs."""
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_curriculum_rows_worker, args=(world, _port(), out), nprocs=world, join=True)
+    want = np.concatenate([np.stack([np.arange(k) + 10 * r, np.full(k, 0.5 + r), np.full(k, -1.0 - r)], 1)
+                           for r, k in enumerate([3, 0, 5])])
+    offs = [0, 3, 3]
+    for r in range(world):
+        got, off, total, cmds, bins = out[r]
+        np.testing.assert_array_equal(got, want)
+        assert off == offs[r] and total == 8
+    allc = np.concatenate([out[r][3] for r in range(world)])
+    from lrl.curriculum import RewardThresholdCurriculum
+    cur = RewardThresholdCurriculum(seed=100, x_vel=(-1, 1, 5), y_vel=(-0.6, 0.6, 2), yaw_vel=(-1, 1, 5))
+    cur.weights[:] = 1.0
+    ref, _ = cur.sample(batch_size=8)
+    np.testing.assert_array_equal(allc, ref)

@@ -59,3 +59,59 @@ def test_two_rank_native_update_keeps_replicas_identical():
     assert np.isfinite(a[0]).all()
     np.testing.assert_array_equal(a[0], b[0])   # identical replicas after 20 optimiser steps
     assert a[1] == b[1] and len(a[1]) == 20     # identical device-side learning-rate schedule
+
+
+def _curriculum_cfg(n):
+    from lrl import config as lcfg
+    cfg = lcfg.make_cfg()
+    lcfg.config_go1(cfg)
+    cfg.env.num_envs = n
+    cfg.env.episode_length_s = 0.5        # time-outs every 25 steps: reset_idx inside step
+    cfg.commands.resampling_time = 0.14   # resampling every 7 steps between resets
+    return cfg
+
+
+def _run_curriculum_env(n, env_offset, steps=60):
+    from lrl.env import LeggedRobotEnv
+    env = LeggedRobotEnv("cuda:0", cfg=_curriculum_cfg(n), seed=9, env_offset=env_offset, legacy_fork=False)
+    env.reset()
+    zero = torch.zeros(n, 12, device="cuda:0")
+    for _ in range(steps):
+        env.step(zero)
+    torch.cuda.synchronize()
+    out = dict(commands=env.commands.cpu().numpy().copy(), bins=env.env_command_bins.copy(),
+               obs=env.obs_buf.cpu().numpy().copy(), dof_pos=env.dof_pos.cpu().numpy().copy(),
+               weights=env.curriculum.weights.copy())
+    env.close()
+    return out
+
+
+def _curriculum_worker(rank, world, port, n, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "rapid-locomotion-rl_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    out[rank] = _run_curriculum_env(n, rank * n)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_command_curriculum_matches_one_process():
+    """Upstream semantics (legacy_fork=False) split over two ranks: every rank applies the same
+    grid-curriculum update / draw over both ranks' resampled envs, so after time-outs and resamplings the two
+    64-env ranks hold exactly the commands, bins, curriculum weights and observations of one 128-env process."""
+    n, world = 64, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_curriculum_worker, args=(world, _port(), n, out), nprocs=world, join=True)
+    ref = _run_curriculum_env(n * world, 0)
+    for r in range(world):
+        part = slice(r * n, (r + 1) * n)
+        np.testing.assert_array_equal(out[r]["weights"], ref["weights"])
+        np.testing.assert_array_equal(out[r]["bins"], ref["bins"][part])
+        np.testing.assert_array_equal(out[r]["commands"], ref["commands"][part])
+        np.testing.assert_array_equal(out[r]["obs"], ref["obs"][part])
+        np.testing.assert_array_equal(out[r]["dof_pos"], ref["dof_pos"][part])
+    assert len(np.unique(ref["bins"])) > 1  # commands were drawn from the curriculum
