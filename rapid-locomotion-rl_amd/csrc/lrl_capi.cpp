@@ -227,6 +227,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   const int wg_envs = LRL_ENV_LANES / 4;
   int lds_contacts = (4 * 51 + model->num_spheres * 67) * wg_envs * 4;  // LEGF, NSF of lrl_env.hip
   if (params->terrain_mesh) lds_contacts += 16 * LRL_ENV_LANES * 16;  // terrain query vertex block, float4 [16][lanes]
+  lds_contacts += (4 * (int)(sizeof(KLeg) / 4) + 5 * model->num_spheres) * 4;  // staged model tables (Lds::ktab)
   int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * wg_envs * 4;  // obs / priv tiles + reward rows
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
   if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);

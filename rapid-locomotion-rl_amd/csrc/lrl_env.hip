@@ -168,10 +168,21 @@ __device__ __forceinline__ float sv_get(const SV& s, int r) {
 #define LEGF 51
 #define LI(r, c) ((r) * ((r) + 1) / 2 + (c))
 
+#define KLEGF ((int)(sizeof(KLeg) / sizeof(float)))  // floats of one leg's model table
 struct Lds {
   float* base;     // leg blocks, then contact rows: [field][env slot] columns shared by the env's 4 lanes
   int sph_off;     // field offset of the contact rows
   int es;          // env slot of this lane inside the workgroup
+  float* ktab;     // the model tables a lane reads at a lane-dependent index, staged once per launch:
+                   // K->leg[4], then per sphere (x, y, z, radius), then per sphere its link (int)
+  int nsph;
+  __device__ __forceinline__ const KLeg& kleg(int l) const { return reinterpret_cast<const KLeg*>(ktab)[l]; }
+  __device__ __forceinline__ float4 sph4(int s) const {
+    return reinterpret_cast<const float4*>(ktab + 4 * KLEGF)[s];
+  }
+  __device__ __forceinline__ int slink(int s) const {
+    return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 4 * nsph)[s];
+  }
   // field f of a row = row pointer + f * ENVS (a constant f folds into the ds_read / ds_write immediate offset)
   __device__ __forceinline__ float& leg(int l, int f) const { return lp(l)[f * ENVS]; }
   __device__ __forceinline__ float& sph(int s, int f) const { return sp(s)[f * ENVS]; }
@@ -739,7 +750,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   float hwin = 0.f;
   if constexpr (TERR) hwin = terrain_window_max(K, st.pos);
   // aa / oo: the carrying leg's joint axes / origins in registers (the leg pass has them; no LDS read-back)
-  auto detect = [&](int s, V3 x, int lsel, int link, const V3* aa, const V3* oo) {
+  auto detect = [&](int s, V3 x, float rad, int lsel, int link, const V3* aa, const V3* oo) {
     if constexpr (TERR) {
       const V3 pw = v3(st.pos[0], st.pos[1], pz) + mul(R, x);
       M.sph(s, 0) = x.x;
@@ -748,10 +759,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.sph(s, 6) = pw.x;
       M.sph(s, 7) = pw.y;
       M.sph(s, 8) = pw.z;
-      if (pw.z - K->sph_rad[s] - P.contact_offset <= hwin) cand |= 1ull << s;
+      if (pw.z - rad - P.contact_offset <= hwin) cand |= 1ull << s;
       return;
     }
-    const float sep = pz + dot(Rz, x) - K->sph_rad[s];
+    const float sep = pz + dot(Rz, x) - rad;
     if (sep < P.contact_offset) {
       active |= (1ull << s);
       M.sph(s, 0) = x.x;
@@ -770,14 +781,17 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     }
   };
   for (int s = ql; s < K->base_sph_end; s += QL)
-    detect(s, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2]), -1, 0, nullptr, nullptr);
+  {
+    const float4 sp = M.sph4(s);
+    detect(s, v3(sp.x, sp.y, sp.z), sp.w, -1, 0, nullptr, nullptr);
+  }
 
   // ---- this lane's leg ----
   SI Aleg;     // composite inertia of the leg about the base origin
   SV Cleg;     // its RNEA force on the base
   {
     const int l = ql;
-    const KLeg& kl = K->leg[l];
+    const KLeg& kl = M.kleg(l);  // (LDS copy: a per-lane global read here was one memory round trip per joint)
     M3 Rp;
 #pragma unroll
     for (int k = 0; k < 9; ++k) Rp.m[k] = (k % 4 == 0) ? 1.f : 0.f;
@@ -802,9 +816,13 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       const V3 c = o + mul(Rj, v3(kl.com[j][0], kl.com[j][1], kl.com[j][2]));
       Ij[j] = make_si(kl.mass[j], c, Rj, kl.inertia[j]);
       // contact detection for this link's spheres (needs only a_j', o_j' for j' <= j, already in LDS)
-      for (int s = K->leg_sph_begin[l]; s < K->leg_sph_end[l]; ++s)
-        if (K->sph_link[s] == j)
-          detect(s, o + mul(Rj, v3(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2])), l, j, aa, oo);
+      const int sb = l == 0 ? SL.b[0] : l == 1 ? SL.b[1] : l == 2 ? SL.b[2] : SL.b[3];
+      const int se = l == 0 ? SL.e[0] : l == 1 ? SL.e[1] : l == 2 ? SL.e[2] : SL.e[3];
+      for (int s = sb; s < se; ++s)
+        if (M.slink(s) == j) {
+          const float4 sp = M.sph4(s);
+          detect(s, o + mul(Rj, v3(sp.x, sp.y, sp.z)), sp.w, l, j, aa, oo);
+        }
       Rp = Rj;
       op = o;
     }
@@ -856,14 +874,14 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (m) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        const THit th = terrain_query(K, v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8)), K->sph_rad[s], P.contact_offset,
+        const THit th = terrain_query(K, v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8)), M.sph4(s).w, P.contact_offset,
                                       reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS),
                                       (int)threadIdx.x);
         if (th.sep < P.contact_offset) {
           M.sph(s, 3) = th.n.x;
           M.sph(s, 4) = th.n.y;
           M.sph(s, 5) = th.n.z;
-          activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), K->sph_link[s], th.sep,
+          activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), th.sep,
                    mulT(R, th.n));
         }
 #ifdef LRL_ENV_PROFILE
@@ -953,7 +971,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     if (m) {
       const int s = __builtin_ctzll(m);
       m &= m - 1ull;
-      contact_setup<TERR>(M, Sch, R, s, sph_leg_of(SL, s), K->sph_link[s]);
+      contact_setup<TERR>(M, Sch, R, s, sph_leg_of(SL, s), M.slink(s));
     }
   }
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
@@ -1190,7 +1208,20 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       act[j] = fminf(fmaxf(a, -c), c);
     }
   }
-  const Lds M{lds, 4 * LEGF, es};  // leg blocks first, then the contact rows
+  // leg blocks first, then the contact rows, (terrain: the query's vertex block), then the model tables
+  const int nsph = K->num_spheres;
+  const Lds M{lds, 4 * LEGF, es, lds + (4 * LEGF + nsph * NSF) * ENVS + (TERR ? 64 * BLOCK : 0), nsph};
+  {
+    const float* src = reinterpret_cast<const float*>(K->leg);
+    for (int i = lane; i < 4 * KLEGF; i += BLOCK) M.ktab[i] = src[i];
+    float4* s4 = reinterpret_cast<float4*>(M.ktab + 4 * KLEGF);
+    int* sl = reinterpret_cast<int*>(M.ktab + 4 * KLEGF + 4 * nsph);
+    for (int s = lane; s < nsph; s += BLOCK) {
+      s4[s] = make_float4(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2], K->sph_rad[s]);
+      sl[s] = K->sph_link[s];
+    }
+    __syncthreads();
+  }
   const float payload = S.payload[e];
   const V3 cb = v3(S.com[e], S.com[N + e], S.com[2 * N + e]);
   const float mb = K->base_mass + payload;
