@@ -1522,23 +1522,26 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   {  // episode_sums / command_sums rows of the terms (distinct rows), 8 terms' loads in flight per batch
     const int nt = P.num_reward_terms;
     for (int t0 = 0; t0 < nt; t0 += 8) {
-      float ev[8], cv[8];
+      // the batch's slots (scalar) and reward values (LDS) read up front and unconditionally (clamped index), so
+      // the scalar and LDS reads share one wait instead of one lgkmcnt(0) per term
+      int sl[8];
+      float rv[8], ev[8], cv[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int t = t0 + u;
-        if (t < nt) {
-          const int slot = P.reward_slot[t];
-          ev[u] = S.episode_sums[slot * N + e];
-          cv[u] = S.command_sums[slot * N + e];
-        }
+        const int t = min(t0 + u, nt - 1);
+        sl[u] = P.reward_slot[t];
+        rv[u] = rt[t];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int t = t0 + u;
-        if (t < nt) {
-          const int slot = P.reward_slot[t];
-          S.episode_sums[slot * N + e] = ev[u] + rt[t];
-          S.command_sums[slot * N + e] = cv[u] + rt[t];
+        ev[u] = S.episode_sums[sl[u] * N + e];
+        cv[u] = S.command_sums[sl[u] * N + e];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (t0 + u < nt) {
+          S.episode_sums[sl[u] * N + e] = ev[u] + rv[u];
+          S.command_sums[sl[u] * N + e] = cv[u] + rv[u];
         }
       }
     }
