@@ -542,8 +542,8 @@ class LeggedRobotEnv:
         if len(tr):
             ep = {}
             means = self._episode_sums[:, tr].mean(dim=1)
-            for i, k in enumerate(self.episode_sums):
-                ep["rew_" + k] = means[i]
+            for k, m in zip(self.episode_sums, means.unbind(0)):  # (one call for all the 0-d views)
+                ep["rew_" + k] = m
             self._episode_sums[:, tr] = 0.0
             self.extras["train/episode"] = ep
         if len(ev):
