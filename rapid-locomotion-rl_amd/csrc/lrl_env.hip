@@ -351,6 +351,7 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   // clamped for the load; cells off the grid are never marked), staged in LDS for the triangle walk
   const float4* __restrict__ vtx = reinterpret_cast<const float4*>(K->terr_vtx);
   const float hmax = K->terr_hmax[ci * Cn + cj];
+  if (p.z - r - margin > hmax) return h;  // (before the block: a lane that leaves here issues none of its 16 gathers)
   float4 V[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
@@ -358,7 +359,6 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
 #pragma unroll
     for (int b = 0; b < 4; ++b) V[a][b] = vtx[vi * Cn + min(max(cj - 1 + b, 0), Cn - 1)];
   }
-  if (p.z - r - margin > hmax) return h;
   // triangles (bit 2 * (3 di + dj) + t) whose xy bounding box grown by g holds p's xy: a triangle under / over p
   // always qualifies, so penetrating spheres keep the triangle they are in
   uint32_t tris = 0;
