@@ -232,6 +232,35 @@ def test_native_terrain_curriculum_matches_reference():
     env.close()
 
 
+def test_native_terrain_curriculum_matches_torch_form_on_random_inputs():
+    """The one-launch terrain curriculum against the host torch form (legged_robot.py:793-818 as written, on
+    CUDA tensors) over random positions, commands, levels and draws: levels and origins identical."""
+    import types
+    from lrl.env import LeggedRobotEnv
+    n, rows, cols = 512, 6, 4
+    cfg = _rough_cfg(n, 2.0, **{"terrain.num_rows": rows, "terrain.num_cols": cols})
+    env = LeggedRobotEnv("cuda:0", cfg=cfg, seed=6)
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    t = cfg.terrain
+    env.terrain_levels[:] = torch.randint(-1, rows + 1, (n,), generator=g, device="cuda:0")
+    env.terrain_types[:] = torch.randint(0, cols, (n,), generator=g, device="cuda:0")
+    env.root_states[:, :2] = env.env_origins[:, :2] + (torch.rand(n, 2, generator=g, device="cuda:0") - 0.5) * 12.0
+    env.commands[:, :2] = (torch.rand(n, 2, generator=g, device="cuda:0") - 0.5) * 2.0
+    ids = torch.randperm(n, generator=g, device="cuda:0")[:300].sort().values
+    draws = torch.randint(0, t.max_terrain_level, (len(ids),), generator=g, device="cuda:0")
+    stub = types.SimpleNamespace(init_done=True, terrain_levels=env.terrain_levels.clone(),
+                                 terrain_types=env.terrain_types.clone(), env_origins=env.env_origins.clone(),
+                                 root_states=env.root_states.clone(), commands=env.commands.clone(),
+                                 _rand_levels=lambda like, high: draws[:len(like)])
+    env._rand_levels = lambda like, high: draws[:len(like)]
+    LeggedRobotEnv._update_terrain_curriculum(stub, ids, cfg)   # torch form (no sim)
+    env._update_terrain_curriculum(ids, cfg)                      # native
+    torch.cuda.synchronize()
+    assert torch.equal(env.terrain_levels, stub.terrain_levels)
+    assert torch.equal(env.env_origins, stub.env_origins)
+    env.close()
+
+
 def test_perceptive_policy_trains_on_rough_terrain():
     """The base config's perceptive layout (observe_vel + 17 x 11 height scan = 235 observations, history
     15 x 235) end to end: upstream resets on the curriculum trimesh, one Runner.learn iteration through the
