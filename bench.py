@@ -108,6 +108,62 @@ def bench_go1_rough(dev, iters=3, warmup=1):
     return out
 
 
+WORKLOADS = {
+    "mc": lambda w: (f"{w * ENVS_PER_GPU} Mini Cheetah envs flat terrain ({ENVS_PER_GPU} per GPU), PPO teacher policy "
+                     f"(BASELINE configs[{1 if w == 1 else 3}])"),
+    "go1": lambda w: (f"{w * ENVS_PER_GPU} Go1 envs on the plane ({ENVS_PER_GPU} per GPU), teacher PPO + student "
+                      "(adaptation-module) distillation update (BASELINE configs[4] at 2 GPUs)"),
+}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """``--gpus N`` without a launcher: start N child processes of this script, one per GPU, with the
+    torch.distributed.run environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), relay their output and
+    exit with the worst return code.  The parent never touches the GPU (torch.cuda.device_count() does not
+    initialise it on this image), so no process that holds a GPU context is replaced or forked."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def init_world(args):
+    """Join (or skip) the process group; returns (world, rank, local_rank, backend).  Every rank asserts that the
+    world it joined has exactly ``--gpus`` ranks."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # one rank per GPU over RCCL ("nccl"); LRL_DIST_BACKEND=gloo rehearses the multi-rank path on CPU or with
+    # several ranks sharing one GPU (ranks then use devices round-robin)
+    backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
+        got = dist.get_world_size()
+        assert got == args.gpus, f"rank {rank}: process group has {got} ranks, --gpus {args.gpus}"
+    return world, rank, local, backend
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,21 +171,39 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the Go1 rough-terrain line (configs[2])")
+    ap.add_argument("--workload", choices=["mc", "go1"], default="mc",
+                    help="mc: 4096 Mini Cheetah envs per GPU, flat (configs[1] / [3]); go1: 4096 Go1 envs per GPU, "
+                         "plane, teacher + student update (configs[4] at --gpus 2)")
+    ap.add_argument("--world-check", action="store_true",
+                    help="join the process group, print the world every rank sees and exit (no GPU work)")
     args = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU over RCCL ("nccl"); LRL_DIST_BACKEND=gloo and more ranks than GPUs are for rehearsing
-    # the multi-rank path on a single-GPU box (ranks then share devices round-robin)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        ndev = torch.cuda.device_count()
+        if args.gpus > ndev:
+            print(f"bench.py: --gpus {args.gpus} requested but {ndev} GPU(s) visible", file=sys.stderr)
+            raise SystemExit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local, backend = init_world(args)
+    if args.world_check:
+        seen = torch.tensor([rank], dtype=torch.int64)
+        if world > 1:
+            ranks = [torch.zeros_like(seen) for _ in range(world)]
+            dist.all_gather(ranks, seen)
+            seen_ranks = sorted(int(t.item()) for t in ranks)
+        else:
+            seen_ranks = [0]
+        if rank == 0:
+            print(json.dumps({"world_size": world, "ranks": seen_ranks, "backend": backend if world > 1 else None,
+                              "parallelism": f"dp{world}"}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     ndev = max(1, torch.cuda.device_count())
     local_dev = local % ndev
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_dev}"))
-        else:
-            dist.init_process_group(backend)
     torch.cuda.set_device(local_dev)
     dev = f"cuda:{local_dev}"
 
@@ -139,7 +213,7 @@ def main():
     from lrl.ppo import runner as R
 
     cfg = lcfg.make_cfg()
-    lcfg.config_mini_cheetah(cfg)
+    (lcfg.config_go1 if args.workload == "go1" else lcfg.config_mini_cheetah)(cfg)
     cfg.env.num_envs = ENVS_PER_GPU
     R.RunnerArgs.save_interval = 0
     R.RunnerArgs.log_freq = 10 ** 9
@@ -202,9 +276,12 @@ def main():
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "4096 Mini Cheetah envs flat terrain, PPO teacher policy (BASELINE configs[1])",
-                       "envs_per_gpu": ENVS_PER_GPU, "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
-                       "parallelism": f"dp{world}", "policy": "ActorCritic 42/18/630->12, random init"},
+            "config": {"workload": WORKLOADS[args.workload](world),
+                       "envs_per_gpu": ENVS_PER_GPU, "global_envs": world * ENVS_PER_GPU,
+                       "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
+                       "parallelism": f"dp{world}", "world_size": dist.get_world_size() if world > 1 else 1,
+                       "backend": (backend if world > 1 else None),
+                       "policy": "ActorCritic 42/18/630->12, random init; teacher PPO + student adaptation update"},
             "ppo_iters_per_s": round(args.steps / elapsed, 3),
             "env_only_env_steps_per_s_per_gpu": round(env_only, 1),
             "env_step_kernel_ms": round(k_ms, 4),

@@ -167,6 +167,9 @@ typedef struct lrl_env_params {
    * offset (legged_robot.py:772 under _call_train_eval) */
   int32_t num_train_envs;
   float teleport_x_offset_eval;
+  /* float32(hi - lo) of motor_strength_range / kp_range / kd_range with the difference taken in double, as
+   * torch.rand(k) * (max - min) + min rounds the python-float difference once (legged_robot.py:544-560) */
+  float dr_span[3];
 } lrl_env_params;
 
 /* ------------------------------------------------------------------------------------------
@@ -244,10 +247,21 @@ int32_t lrl_sim_step(lrl_sim* sim, const float* actions, uint32_t flags, void* s
 int32_t lrl_sim_inject_uniforms(lrl_sim* sim, const float* noise_u, const float* dr_u);
 
 int32_t lrl_sim_reset_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, void* stream);
-/* reset_idx with the root-state policy made explicit: root_mode 0 leaves the root untouched (the
- * fork's custom-origin quirk), 1 writes base_init_state + env_origin + (xo, yo). */
-int32_t lrl_sim_reset_idx_ex(lrl_sim* sim, const int32_t* env_ids, int32_t n, int32_t root_mode, float xo, float yo,
-                             void* stream);
+/* reset_idx (legged_robot.py:227-290) with the root-state policy made explicit.
+ *   root_mode 0: the root is left untouched — the fork's custom-origin quirk (_reset_root_states
+ *                :724-741 writes the advanced-index copy `root_states` and pushes the unchanged all_root_states);
+ *   root_mode 1: base_init_state + env_origin (the plane path :736-737 / upstream);
+ *   root_mode 2: custom origins, upstream semantics (:725-732): ((base_init_state + env_origin) + (xy_span * u
+ *                + xy_lo)) + (x_off, y_off), one uniform u per env for x and one for y — torch_rand_float(
+ *                x_init_range, y_init_range, (k, 2)) with xy_lo = x_init_range and xy_span = float32(y_init_range -
+ *                x_init_range) rounded from the python-float difference — in that float32 order.
+ * The uniforms (motor-strength / Kp / Kd redraws of _randomize_dof_props :544-560, then x, y) come from the
+ * sim's counter RNG, or with flags & LRL_STEP_INJECT_UNIFORM from the lrl_sim_inject_reset_uniforms buffer. */
+int32_t lrl_sim_reset_idx_ex(lrl_sim* sim, const int32_t* env_ids, int32_t n, int32_t root_mode, float xy_lo,
+                             float xy_span, float x_off, float y_off, uint32_t flags, void* stream);
+/* Injected reset uniforms for parity tests: u [n, 5] f32 device, row t = (motor strength, Kp, Kd, x, y) of the
+ * t-th env id of the next lrl_sim_reset_idx_ex call with LRL_STEP_INJECT_UNIFORM (torch.rand draw order). */
+int32_t lrl_sim_inject_reset_uniforms(lrl_sim* sim, const float* u);
 /* Upstream reset path (legged_robot.py:177 `reset_idx` inside post_physics_step, re-enabled with
  * legacy_fork=False): after lrl_sim_step + lrl_sim_reset_idx_ex of the envs the step reset, re-run
  * compute_observations (:342-417) for them from the post-reset state with the step's own noise draws, set

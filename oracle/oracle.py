@@ -7,6 +7,7 @@ product path (rapid-locomotion-rl_amd/) never does.
 * ``env_step``         — lrl_oracle.c:lrlo_env_step (LeggedRobot.step, legged_robot.py:106-137).
 * ``physics_substep``  — lrl_oracle.c:lrlo_physics_substep (own dense dynamics; PhysX parity unpinned).
 * ``gae``              — RolloutStorage.compute_returns (rollout_storage.py:76-90) in numpy.
+* ``reset_idx_device`` — the device part of LeggedRobot.reset_idx (legged_robot.py:227-290) in numpy float32.
 """
 import ctypes as C
 import os
@@ -70,8 +71,14 @@ def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs, num_height_points=0
 
 
 def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_step_counter=1, noise_u=None,
-             dr_u=None):
-    """In-place LeggedRobot.step on a logical-layout state dict (see make_state)."""
+             dr_u=None, margins=None):
+    """In-place LeggedRobot.step on a logical-layout state dict (see make_state).  ``margins``: optional float64
+    [n, 2] array that receives each env's discontinuity margins of this step (lrl_oracle.c g_margin_*): the
+    smallest |separation - contact_offset| over its spheres and sub-steps, and the smallest |u_n +
+    bounce_threshold_velocity| of a contact with restitution."""
+    if margins is not None:
+        assert margins.dtype == np.float64 and margins.flags["C_CONTIGUOUS"] and margins.shape == (state["root"].shape[0], 2)
+    lib().lrlo_set_margin_out(margins.ctypes.data_as(C.c_void_p) if margins is not None else None)
     for k in ENV_FIELDS:
         a = state[k]
         assert a.flags["C_CONTIGUOUS"] and a.dtype == _dtype(k), k
@@ -156,3 +163,36 @@ def gae(rewards, dones, values, last_values, gamma, lam):
         returns[t] = adv + values[t]
     a = returns - values
     return returns, (a - a.mean(dtype=np.float64)) / (a.std(ddof=1, dtype=np.float64) + 1e-8)
+
+
+def reset_idx_device(params, state, ids, u, root_mode, xy_lo=0.0, xy_span=0.0, x_off=0.0, y_off=0.0):
+    """reset_idx's per-env state changes (legged_robot.py:244-259) on a logical-layout state dict, in place:
+    _randomize_dof_props (:544-560: rand * (max - min) + min, two float32 roundings), _reset_dofs (:690-712),
+    _reset_root_states (:714-755; root_mode as lrl.h: 0 fork custom origins (Q4), 1 base_init_state + origin,
+    2 upstream custom origins with the xy draw and init offsets), then last_actions / last_dof_vel / feet_air_time /
+    episode_length zeroed and reset_buf set.  u [len(ids), 5]: (motor strength, Kp, Kd, x, y) uniforms."""
+    f32 = np.float32
+    ids = np.asarray(ids)
+    u = np.asarray(u, f32)
+    span = [f32(s) for s in params.dr_span]
+    for flag, key, lo, j in ((params.randomize_motor_strength, "motor_strength", params.motor_strength_range[0], 0),
+                             (params.randomize_kp, "kp", params.kp_range[0], 1),
+                             (params.randomize_kd, "kd", params.kd_range[0], 2)):
+        if flag:
+            state[key][ids] = ((u[:, j] * span[j]).astype(f32) + f32(lo)).astype(f32)[:, None]
+    state["dof_pos"][ids] = np.array(params.default_dof_pos[:], f32)
+    state["dof_vel"][ids] = 0.0
+    if root_mode != 0:
+        r = np.tile(np.array(params.base_init_state[:], f32), (len(ids), 1))
+        r[:, :3] = r[:, :3] + state["env_origins"][ids]
+        if root_mode == 2:
+            xy = (f32(xy_span) * u[:, 3:5]).astype(f32) + f32(xy_lo)
+            r[:, :2] = r[:, :2] + xy
+            r[:, 0] = r[:, 0] + f32(x_off)
+            r[:, 1] = r[:, 1] + f32(y_off)
+        state["root"][ids] = r
+    for k in ("last_actions", "last_dof_vel", "feet_air_time"):
+        state[k][ids] = 0.0
+    state["episode_length"][ids] = 0
+    state["reset"][ids] = 1
+    return state

@@ -9,30 +9,49 @@
 
 namespace lrl {
 
+// The reset / curriculum kernels follow torch's float32 op order exactly (the build uses
+// -ffp-contract=fast-honor-pragmas, so this pragma really keeps multiply-adds unfused; __fmul_rn / __fadd_rn alone
+// are plain operators in HIP and do not).
+#pragma clang fp contract(off)
+
 // reset_idx (legged_robot.py:227-290) device part: _randomize_dof_props (:544-560), _reset_dofs
-// (:690-712), _reset_root_states (:714-755), buffer zeroing (:255-259).  root_mode: 0 = leave the root
-// (fork quirk Q4 for custom origins), 1 = base_init_state + env_origin (+ xy_offset).
+// (:690-712), _reset_root_states (:714-755), buffer zeroing (:255-259).  root_mode (lrl.h): 0 = leave the root
+// (fork quirk Q4 for custom origins), 1 = base_init_state + env_origin, 2 = custom origins with the upstream
+// xy draw xy_span * u + xy_lo and the (x_off, y_off) init offsets.  Uniform draws: (motor strength, Kp, Kd, x, y)
+// from Philox keyed by (global env, reset counter), or row t of S.inj_reset (the reference's torch.rand draws,
+// one row per env id in id order).  Float32 arithmetic in the reference's operation order, uncontracted.
 __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
-                             int32_t root_mode, float xy_off_x, float xy_off_y, int64_t counter) {
+                             int32_t root_mode, float xy_lo, float xy_span, float x_off, float y_off, int32_t inject,
+                             int64_t counter) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const lrl_env_params& P = K->p;
   const int N = S.stride;
   int e = ids[t];
   if (e < 0 || e >= S.n) return;
-  uint64_t genv = (uint64_t)(S.env_offset + e);
-  lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)counter, (LRL_RNG_RESET << 16) ^ (uint32_t)(counter >> 32), 0, S.seed);
-  int k = 0;
+  float u[5];
+  if (inject) {
+    for (int k = 0; k < 5; ++k) u[k] = S.inj_reset[(size_t)t * 5 + k];
+  } else {
+    uint64_t genv = (uint64_t)(S.env_offset + e);
+    const uint32_t key = (LRL_RNG_RESET << 16) ^ (uint32_t)(counter >> 32);
+    lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)counter, key, 0, S.seed);
+    lrl_u32x4 r2 = lrl_philox((uint32_t)genv, (uint32_t)counter, key, 1, S.seed);
+    for (int k = 0; k < 4; ++k) u[k] = lrl_u01(r.v[k]);
+    u[4] = lrl_u01(r2.v[0]);
+  }
+  // torch.rand(k) * (max - min) + min: two float32 roundings, the span rounded once from the python floats
+  auto draw = [](float uu, float span, float lo) { return __fadd_rn(__fmul_rn(uu, span), lo); };
   if (P.randomize_motor_strength) {
-    float v = lrl_u01(r.v[k++]) * (P.motor_strength_range[1] - P.motor_strength_range[0]) + P.motor_strength_range[0];
+    float v = draw(u[0], P.dr_span[0], P.motor_strength_range[0]);
     for (int j = 0; j < 12; ++j) S.motor_strength[j * N + e] = v;
   }
   if (P.randomize_kp) {
-    float v = lrl_u01(r.v[k++]) * (P.kp_range[1] - P.kp_range[0]) + P.kp_range[0];
+    float v = draw(u[1], P.dr_span[1], P.kp_range[0]);
     for (int j = 0; j < 12; ++j) S.kp[j * N + e] = v;
   }
   if (P.randomize_kd) {
-    float v = lrl_u01(r.v[k++]) * (P.kd_range[1] - P.kd_range[0]) + P.kd_range[0];
+    float v = draw(u[2], P.dr_span[2], P.kd_range[0]);
     for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
   }
   for (int j = 0; j < 12; ++j) {
@@ -41,12 +60,15 @@ __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int3
     S.last_actions[j * N + e] = 0.f;
     S.last_dof_vel[j * N + e] = 0.f;
   }
-  if (root_mode == 1) {
+  if (root_mode != 0) {
+    // torch_rand_float(lo, hi, (k, 2)) = (hi - lo) * rand + lo, xy_span = float32(hi - lo) from the host
     for (int c = 0; c < 13; ++c) {
       float v = P.base_init_state[c];
-      if (c < 3) v += S.env_origins[c * N + e];
-      if (c == 0) v += xy_off_x;
-      if (c == 1) v += xy_off_y;
+      if (c < 3) v = __fadd_rn(v, S.env_origins[c * N + e]);
+      if (root_mode == 2 && c < 2) {
+        v = __fadd_rn(v, __fadd_rn(__fmul_rn(xy_span, u[3 + c]), xy_lo));
+        v = __fadd_rn(v, c == 0 ? x_off : y_off);
+      }
       S.root[c * N + e] = v;
     }
   }
@@ -227,10 +249,11 @@ __global__ void randomize_kernel(KState S, float f0, float f1, float r0, float r
 
 extern "C" {
 hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* ids, int32_t n, int32_t root_mode,
-                            float xo, float yo, int64_t counter, hipStream_t st) {
+                            float xy_lo, float xy_span, float x_off, float y_off, int32_t inject, int64_t counter,
+                            hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, root_mode, xo, yo,
-                     counter);
+  hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, root_mode, xy_lo,
+                     xy_span, x_off, y_off, inject, counter);
   return hipGetLastError();
 }
 hipError_t lrl_launch_terrain_curriculum(const KState* S, const int32_t* ids, int32_t n, int64_t* levels,

@@ -29,8 +29,8 @@ extern "C" {
 hipError_t lrl_launch_env_step(const KParams*, const KState*, int, const float*, uint32_t, int64_t, int, hipStream_t);
 hipError_t lrl_launch_observe(const KParams*, const KState*, const int32_t*, int32_t, uint32_t, int64_t, hipStream_t);
 hipError_t lrl_env_kernel_setup(int lds_bytes);
-hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, int64_t,
-                            hipStream_t);
+hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, float, float,
+                            int32_t, int64_t, hipStream_t);
 hipError_t lrl_launch_set_root(const KState*, const float*, const int32_t*, int32_t, hipStream_t);
 hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t, int64_t*, const int64_t*,
                                          const int64_t*, const float*, int32_t, int32_t, float, float, int32_t,
@@ -409,14 +409,25 @@ int32_t lrl_sim_set_step_counter(lrl_sim* s, int64_t c) {
 }
 
 int32_t lrl_sim_reset_idx(lrl_sim* s, const int32_t* ids, int32_t n, void* stream) {
-  return lrl_sim_reset_idx_ex(s, ids, n, 1, 0.f, 0.f, stream);
+  return lrl_sim_reset_idx_ex(s, ids, n, 1, 0.f, 0.f, 0.f, 0.f, 0u, stream);
 }
 
-int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t root_mode, float xo, float yo,
-                             void* stream) {
+int32_t lrl_sim_inject_reset_uniforms(lrl_sim* s, const float* u) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  s->S.inj_reset = u;
+  return 0;
+}
+
+int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t root_mode, float xy_lo, float xy_span,
+                             float x_off, float y_off, uint32_t flags, void* stream) {
   if (!s || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  if (n < 0) return fail(LRL_E_INVALID, "negative env count");
+  if (root_mode < 0 || root_mode > 2) return fail(LRL_E_INVALID, "root_mode %d", root_mode);
+  const bool inject = (flags & LRL_STEP_INJECT_UNIFORM) != 0;
+  if (inject && n > 0 && !s->S.inj_reset) return fail(LRL_E_INVALID, "injected reset uniforms not set");
   s->reset_counter += 1;
-  HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, root_mode, xo, yo, s->reset_counter, (hipStream_t)stream));
+  HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, root_mode, xy_lo, xy_span, x_off, y_off, inject ? 1 : 0,
+                            s->reset_counter, (hipStream_t)stream));
   return 0;
 }
 

@@ -1396,7 +1396,8 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     if (P.randomize_motor_strength) {
       float u = inject ? (valid ? S.inj_dr[e] : 0.5f) : lrl_u01(r.v[k]);
       k++;
-      float v = u * (P.motor_strength_range[1] - P.motor_strength_range[0]) + P.motor_strength_range[0];
+      // torch.rand * (max - min) + min: two float32 roundings, the span rounded from the python-float difference
+      float v = __fadd_rn(__fmul_rn(u, P.dr_span[0]), P.motor_strength_range[0]);
 #pragma unroll
       for (int j = 0; j < 12; ++j) {
         ms_e[j] = v;
@@ -1405,13 +1406,13 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     }
     if (P.randomize_kp) {
       float u = lrl_u01(r.v[k++]);
-      float v = u * (P.kp_range[1] - P.kp_range[0]) + P.kp_range[0];
+      float v = __fadd_rn(__fmul_rn(u, P.dr_span[1]), P.kp_range[0]);
 #pragma unroll
       for (int j = 0; j < 12; ++j) S.kp[j * N + e] = v;
     }
     if (P.randomize_kd) {
       float u = lrl_u01(r.v[k++]);
-      float v = u * (P.kd_range[1] - P.kd_range[0]) + P.kd_range[0];
+      float v = __fadd_rn(__fmul_rn(u, P.dr_span[2]), P.kd_range[0]);
 #pragma unroll
       for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
     }

@@ -70,7 +70,7 @@ class LrlEnvParams(C.Structure):
         ("base_init_state", f32 * 13), ("num_history", i32), ("auto_reset", i32), ("max_episode_length", i32),
         ("terrain_mesh", i32), ("border_size", f32), ("horizontal_scale", f32), ("vertical_scale", f32),
         ("measure_heights", i32), ("num_height_points", i32), ("height_points", f32 * 2 * MAX_HEIGHT_POINTS),
-        ("obs_scale_height", f32), ("num_train_envs", i32), ("teleport_x_offset_eval", f32),
+        ("obs_scale_height", f32), ("num_train_envs", i32), ("teleport_x_offset_eval", f32), ("dr_span", f32 * 3),
     ]
 
 
@@ -147,7 +147,7 @@ def lib():
                      "lrl_sim_reset_idx_ex", "lrl_sim_observe_idx", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
                      "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student", "lrl_sim_set_terrain",
-                     "lrl_sim_terrain_curriculum"]:
+                     "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_ppo_workspace_bytes.restype = C.c_int64
         L.lrl_ppo_act_workspace_bytes.restype = C.c_int64

@@ -15,6 +15,7 @@ host — the command curriculum (numpy MT19937) and the per-reset episode loggin
 """
 import ctypes as C
 import math
+import os
 
 import numpy as np
 import torch
@@ -26,7 +27,9 @@ from .curriculum import RewardThresholdCurriculum
 from .robot import load_robot
 from .terrain import Terrain, convert_heightfield_to_trimesh
 
-MINI_GYM_ROOT_DIR = "/root/reference"  # only used to format Cfg.asset.file; tables ship in lrl/robots
+# Cfg.asset.file is formatted with the package root, as mini_gym does; only its file name selects the robot's
+# committed model table (lrl/robots/<name>.json) — no URDF is read at run time
+MINI_GYM_ROOT_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class _LazyExtras(dict):
@@ -436,12 +439,13 @@ class LeggedRobotEnv:
             interval = int(self.cfg.commands.resampling_time / self.dt)
             cached = self._due_next
             if cached is not None and cached[0] == self.episode_length_buf._version:
-                due = cached[1]  # known from the previous step's single device->host copy
-            else:  # first step, or episode_length_buf written by a caller since
+                due, due_np = cached[1], cached[2]  # known from the previous step's single device->host copy
+            else:  # first step, or episode_length_buf written by a caller since: host ids from the fresh set
                 due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
+                due_np = due.cpu().numpy()
             # (with several ranks every rank takes part whenever any rank has envs to resample)
             if (len(due) > 0) if self._dist is None else (self._dist_count(len(due)) > 0):
-                self.resample_commands(due, due.cpu().numpy() if cached is None else cached[2])
+                self.resample_commands(due, due_np)
         self._sums_host = None  # the kernel below changes the command sums
         timer = self.kernel_timer
         if timer is not None:  # HIP events on the launch stream around the fused kernel (bench.py)
@@ -532,12 +536,6 @@ class LeggedRobotEnv:
             self.update_command_curriculum(ev, self.eval_cfg)
         if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
             self.resample_commands(env_ids, _ids_host)
-        ids32 = env_ids.to(torch.int32).contiguous()
-        xo = yo = 0.0
-        if self.custom_origins:  # torch_rand_float(x_init_range, y_init_range) == constant (Q8)
-            t = self.cfg.terrain
-            xo = float(t.x_init_range) + float(t.x_init_offset)
-            yo = float(t.x_init_range) + float(t.y_init_offset)
         # episode logging before the per-env sums are zeroed (:261-276)
         if len(tr):
             ep = {}
@@ -552,8 +550,7 @@ class LeggedRobotEnv:
                 unset = ev[self.episode_sums_eval[k][ev] == -1]
                 self.episode_sums_eval[k][unset] = self.episode_sums[k][unset]
             self._episode_sums[:, ev] = 0.0
-        _abi.check(self._L.lrl_sim_reset_idx_ex(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
-                                                C.c_int32(1), C.c_float(xo), C.c_float(yo), self._stream()))
+        self._reset_device(env_ids)
         ep = self.extras.get("train/episode")
         if ep is None:
             ep = self.extras["train/episode"] = {}
@@ -563,8 +560,48 @@ class LeggedRobotEnv:
             self.env_command_bins_t = torch.tensor(self.env_command_bins, dtype=torch.float, device=self.device)
             self.extras["env_bins"] = self.env_command_bins_t[:self.num_train_envs]
             ep["command_area"] = np.sum(self.curriculum.weights) / self.curriculum.weights.shape[0]
+        if self.cfg.commands.yaw_command_curriculum:  # :283-286
+            ep["max_command_yaw"] = self.cfg.command_ranges["ang_vel_yaw"][1]
+            if self.eval_cfg is not None:
+                ev_ep = self.extras.get("eval/episode")
+                if ev_ep is None:
+                    ev_ep = self.extras["eval/episode"] = {}
+                ev_ep["max_command_yaw"] = self.eval_cfg.command_ranges["ang_vel_yaw"][1]
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self.time_out_buf[:self.num_train_envs]
+
+    def _root_mode(self):
+        """_reset_root_states (legged_robot.py:714-755) as a reset_kernel root mode (lrl.h): the plane path writes
+        all_root_states (mode 1); with custom origins the fork writes an advanced-index copy and pushes the unchanged
+        all_root_states, so the root is left as it is (mode 0); upstream semantics (legacy_fork=False)
+        place it at the origin plus the U[x_init_range, y_init_range] draw and the init offsets (mode 2)."""
+        if not self.custom_origins:
+            return 1
+        return 0 if self.legacy_fork else 2
+
+    def _reset_device(self, env_ids):
+        """The device part of reset_idx, one launch per train / eval group (each with its cfg's init ranges):
+        _randomize_dof_props, _reset_dofs, _reset_root_states and the buffer zeroing (:247-259).  A test may set
+        ``reset_uniforms`` ([len(env_ids), 5] device f32: motor strength, Kp, Kd, x, y per env id) to replace the
+        draws of the next reset."""
+        inj, self.reset_uniforms = getattr(self, "reset_uniforms", None), None
+        mode = self._root_mode()
+        for ids, c in (self._groups(env_ids) if len(env_ids) else []):
+            ids32 = ids.to(torch.int32).contiguous()
+            flags = 0
+            if inj is not None:
+                rows = inj if len(ids) == len(env_ids) else inj[torch.isin(env_ids, ids)]
+                rows = rows.to(self.device, torch.float32).contiguous()
+                _abi.check(self._L.lrl_sim_inject_reset_uniforms(self._sim, C.c_void_p(rows.data_ptr())))
+                flags = _abi.STEP_INJECT_UNIFORM
+            t = c.terrain
+            _abi.check(self._L.lrl_sim_reset_idx_ex(
+                self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)), C.c_int32(mode),
+                C.c_float(float(t.x_init_range)), C.c_float(float(t.y_init_range) - float(t.x_init_range)),
+                C.c_float(float(t.x_init_offset)),
+                C.c_float(float(t.y_init_offset)), C.c_uint32(flags), self._stream()))
+            if inj is not None:
+                torch.cuda.current_stream(self.device).synchronize()  # rows must outlive the launch
 
     def _rand_levels(self, like, high):
         """torch.randint_like(levels, high) of _update_terrain_curriculum (seeded device generator here;

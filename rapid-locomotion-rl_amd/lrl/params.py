@@ -203,5 +203,6 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         measure_heights=int(cfg.terrain.measure_heights), num_height_points=len(hp),
         height_points=hp.tolist(), obs_scale_height=s.height_measurements, num_train_envs=2 ** 30,
         teleport_x_offset_eval=float(getattr(cfg.terrain, "x_offset", 0)) * cfg.terrain.horizontal_scale,
+        dr_span=[float(r[1]) - float(r[0]) for r in (dr.motor_strength_range, dr.Kp_factor_range, dr.Kd_factor_range)],
     )
     return P

@@ -13,7 +13,12 @@ Fixtures written (all small .npz, inputs + expected outputs):
       then step() runs _compute_torques x4 (:653-688), post_physics_step (:139-188),
       teleport (:768-791), DR redraw (:544-560), check_termination (:190-202),
       compute_reward (:314-340, 12 terms), compute_observations (:342-417), clip (:133-136).
-  reset_mc.npz        reset_idx on all envs (:227-290) incl. curriculum/extras.
+  post_physics_all_terms.npz
+      the same for Mini Cheetah with all 21 _reward_* terms (:1506-1646) plus termination at non-zero
+      scales and only_positive_rewards off.
+  reset.npz           reset_idx (:227-290) on a subset of envs: Mini Cheetah fork (Q4), Go1 plane fork, Go1
+                      upstream (custom-origin spawn draw, _resample_commands, yaw curriculum), with the
+                      command curriculum, DR redraw, buffer zeroing and extras.
   curriculum.npz      RewardThresholdCurriculum set_to/sample/update/sample (curriculum.py).
   gae.npz             RolloutStorage.compute_returns (rollout_storage.py:76-90).
   ppo_update.npz      PPO.act/process_env_step/compute_returns/update (ppo.py:62-178) with
@@ -126,10 +131,10 @@ lr_mod.gymapi.DOMAIN_SIM = 0
 LEGS = ["FL", "FR", "RL", "RR"]
 DOF_NAMES = [f"{l}_{j}_joint" for l in LEGS for j in ["hip", "thigh", "calf"]]
 URDF_LIMITS = {
-    # (lower, upper, effort) per joint kind, from the URDFs (mini_cheetah.urdf:104,133,162; go1.urdf)
-    "mc": {"hip": (-1.6, 1.6, 18.0), "thigh": (-2.6, 2.6, 18.0), "calf": (-2.6, 2.6, 26.0)},
-    "go1": {"hip": (-0.802851455917, 0.802851455917, 33.5), "thigh": (-1.0471975512, 4.18879020479, 33.5),
-            "calf": (-2.69653369433, -0.916297857297, 33.5)},
+    # (lower, upper, effort, velocity) per joint kind, from the URDFs (mini_cheetah.urdf:104,133,162; go1.urdf)
+    "mc": {"hip": (-1.6, 1.6, 18.0, 40.0), "thigh": (-2.6, 2.6, 18.0, 40.0), "calf": (-2.6, 2.6, 26.0, 26.0)},
+    "go1": {"hip": (-0.802851455917, 0.802851455917, 33.5, 50.0), "thigh": (-1.0471975512, 4.18879020479, 33.5, 28.0),
+            "calf": (-2.69653369433, -0.916297857297, 33.5, 28.0)},
 }
 
 
@@ -176,8 +181,8 @@ def make_env(robot, n, seed, tweak=None):
     props = np.zeros(12, dtype=[("lower", np.float32), ("upper", np.float32), ("velocity", np.float32),
                                 ("effort", np.float32)])
     for i, name in enumerate(DOF_NAMES):
-        lo, hi, eff = lim[name.split("_")[1]]
-        props[i] = (lo, hi, 40.0, eff)
+        lo, hi, eff, vel = lim[name.split("_")[1]]
+        props[i] = (lo, hi, vel, eff)
     env._process_dof_props(props, 0)  # the reference's own soft-limit arithmetic (:501-516)
 
     # sim tensors (identity gather indices: one actor per env)
@@ -284,8 +289,24 @@ class InjectRand:
         torch.rand_like, torch.rand = self._rl, self._r
 
 
-def gen_post_physics(robot, n=16, steps=3, seed=7):
-    env, rng = make_env(robot, n, seed)
+ALL_TERMS = dict(energy=-1e-3, energy_expenditure=-2e-3, dof_vel=-1e-4, survival=0.3, dof_vel_limits=-0.5,
+                 torque_limits=-0.02, stumble=-0.4, stand_still=-0.2, feet_contact_forces=-0.01, orientation=-5.0,
+                 base_height=-30.0, termination=-2.0)
+
+
+def _all_terms_tweak(cfg):
+    """Every reward function of legged_robot.py:1506-1646 at a non-zero scale (the presets activate 12), with
+    limits low enough that the limit terms fire on the fixture's states."""
+    for k, v in ALL_TERMS.items():
+        setattr(cfg.rewards.scales, k, v)
+    cfg.rewards.soft_dof_vel_limit = 0.05
+    cfg.rewards.soft_torque_limit = 0.4
+    cfg.rewards.max_contact_force = 20.0
+    cfg.rewards.only_positive_rewards = False
+
+
+def gen_post_physics(robot, n=16, steps=3, seed=7, tweak=None, name=None):
+    env, rng = make_env(robot, n, seed, tweak)
     B = env.num_bodies
     rec = {k: [] for k in [
         "root_in", "dof_pos_in", "dof_vel_in", "contact_in", "actions", "commands", "noise_u", "ms_u",
@@ -388,7 +409,7 @@ def gen_post_physics(robot, n=16, steps=3, seed=7):
     out["dt"] = np.array(env.dt)
     out["max_episode_length"] = np.array(env.max_episode_length)
     out["rand_interval"] = np.array(env.cfg.domain_rand.rand_interval)
-    np.savez_compressed(os.path.join(HERE, f"post_physics_{robot}.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, name or f"post_physics_{robot}.npz"), **out)
     print("post_physics", robot, "reward terms:", list(env.reward_names))
 
 
@@ -685,6 +706,146 @@ def gen_terrain_curriculum(n=64, seed=13):
     print("terrain_curriculum:", {k: v.shape for k, v in out.items()})
 
 
+class InjectResetRand:
+    """Patch torch.rand during reset_idx: every draw (_randomize_dof_props' motor strength, torch_rand_float's xy
+    offsets) comes from ``rng`` and is recorded in call order."""
+
+    def __init__(self, rng):
+        self.rng, self.draws, self._r = rng, [], torch.rand
+
+    def __enter__(self):
+        def rand(*shape, **kw):
+            shape = shape[0] if len(shape) == 1 and isinstance(shape[0], (tuple, list)) else shape
+            u = torch.tensor(self.rng.random(tuple(shape)), dtype=torch.float)
+            self.draws.append(u.clone())
+            return u
+        torch.rand = rand
+        return self
+
+    def __exit__(self, *a):
+        torch.rand = self._r
+
+
+def _reset_case_tweak(case):
+    def tweak(cfg):
+        if case == "go1_up":  # custom origins + the upstream xy spawn draw with unequal ranges (Q8) and offsets
+            cfg.terrain.mesh_type = "trimesh"
+            cfg.terrain.x_init_range, cfg.terrain.y_init_range = -0.5, 0.75
+            cfg.terrain.x_init_offset, cfg.terrain.y_init_offset = 0.25, -0.125
+            cfg.commands.yaw_command_curriculum = True
+    return tweak
+
+
+def gen_reset(n=24, seed=17):
+    """reset_idx (legged_robot.py:227-290) for a subset of envs, three cases:
+      mc_fork  Mini Cheetah preset (trimesh, custom origins): the fork's Q4 — _reset_root_states (:724-741) writes
+               the advanced-index copy root_states and pushes the unchanged all_root_states, so roots stay put;
+      go1_fork Go1 preset (plane): roots to base_init_state + env origin (:736-737);
+      go1_up   upstream semantics: custom origins with root_states aliasing all_root_states (the upstream view),
+               _resample_commands (:595-626) inside reset_idx after the command curriculum (where the fork comments
+               it out, :246), x/y init ranges -0.5 / 0.75 and init offsets, yaw command curriculum on.
+    common_step_counter is a multiple of max_episode_length so _update_command_curriculum_uniform (:851-880) moves
+    the command ranges.  torch.rand draws are injected and recorded."""
+    out = {}
+    for case, robot in (("mc_fork", "mc"), ("go1_fork", "go1"), ("go1_up", "go1")):
+        env, rng = make_env(robot, n, seed, _reset_case_tweak(case))
+        cfg = env.cfg
+        env.custom_origins = cfg.terrain.mesh_type in ["heightfield", "trimesh"]
+        env.init_done = True
+        np.int = int  # Q12: the reference's _init_command_distribution uses the removed np.int alias
+        env._init_command_distribution(torch.arange(n))
+        env.terrain_levels = torch.zeros(n, dtype=torch.long)
+        env.envs = list(range(n))  # FakeGym.find_actor_index returns the env handle = env index
+        env.complete_video_frames, env.video_frames = None, []  # record_video bookkeeping (:743-748)
+        i = cfg.init_state  # _init_buffers (legged_robot.py:1003-1005)
+        env.base_init_state = torch.tensor(i.pos + i.rot + i.lin_vel + i.ang_vel, dtype=torch.float)
+        upstream = case.endswith("_up")
+        if upstream:
+            env.root_states = env.all_root_states  # upstream: a view, so the custom-origin reset lands
+            orig = env.update_command_curriculum
+
+            def ucc(ids, c, episode_sums=None, _o=orig, _e=env):
+                _o(ids, c)
+                _e._resample_commands(ids)  # upstream position of the call the fork comments out (:246)
+            env.update_command_curriculum = ucc
+        B = env.num_bodies
+        nz = np.flatnonzero(env.curriculum.weights > 0)
+        env.env_command_bins[:] = rng.choice(nz, n)
+        root = np.zeros((n, 13), np.float32)
+        root[:, :3] = rng.uniform(-3, 3, (n, 3))
+        root[:, 3:7] = rand_quat(rng, n)
+        root[:, 7:13] = rng.normal(size=(n, 6))
+        env.all_root_states[:] = torch.tensor(root)
+        dof_pos = (rng.normal(size=(n, 12)) * 0.5).astype(np.float32)
+        dof_vel = rng.normal(size=(n, 12)).astype(np.float32)
+        env.all_dof_state.view(n, 12, 2)[..., 0] = torch.tensor(dof_pos)
+        env.all_dof_state.view(n, 12, 2)[..., 1] = torch.tensor(dof_vel)
+        env.dof_state[:] = env.all_dof_state
+        env.env_origins = torch.tensor(rng.uniform(-20, 20, (n, 3)), dtype=torch.float)
+        env.last_actions[:] = torch.tensor(rng.normal(size=(n, 12)), dtype=torch.float)
+        env.last_dof_vel[:] = torch.tensor(rng.normal(size=(n, 12)), dtype=torch.float)
+        env.feet_air_time[:] = torch.tensor(rng.uniform(0, 1, (n, 4)), dtype=torch.float)
+        env.episode_length_buf[:] = torch.tensor(rng.integers(0, 1000, n))
+        env.reset_buf = torch.zeros(n, dtype=torch.bool)
+        env.time_out_buf[:] = torch.tensor(rng.random(n) < 0.4)
+        env.commands[:] = torch.tensor(rng.uniform(-1, 1, (n, 4)), dtype=torch.float)
+        for d in (env.episode_sums, env.command_sums):
+            for k in d:
+                d[k][:] = torch.tensor(rng.normal(size=n), dtype=torch.float)
+        # tracking sums high enough that the uniform command curriculum widens the ranges (mean / 1001 > 0.8 * scale)
+        env.episode_sums["tracking_lin_vel"][:] = torch.tensor(rng.uniform(15, 20, n), dtype=torch.float)
+        env.episode_sums["tracking_ang_vel"][:] = torch.tensor(rng.uniform(7, 12, n), dtype=torch.float)
+        # tracking command sums around the resampling thresholds, so some bins succeed and some do not
+        ep_len = min(cfg.env.max_episode_length, int(cfg.commands.resampling_time / env.dt))
+        env.command_sums["tracking_lin_vel"][:] = torch.tensor(rng.uniform(0.6, 1.0, n) * 0.02 * ep_len, dtype=torch.float)
+        env.command_sums["tracking_ang_vel"][:] = torch.tensor(rng.uniform(0.3, 0.7, n) * 0.01 * ep_len, dtype=torch.float)
+        env.motor_strengths[:] = torch.tensor(rng.uniform(0.9, 1.1, (n, 1)).repeat(12, 1), dtype=torch.float)
+        env.common_step_counter = 2 * int(cfg.env.max_episode_length)
+        env.extras = {}
+        ranges0 = {k: list(map(float, v)) for k, v in cfg.command_ranges.items() if k in ("lin_vel_x", "ang_vel_yaw")}
+        inp = dict(root=root, dof_pos=dof_pos, dof_vel=dof_vel, env_origins=env.env_origins.numpy().copy(),
+                   last_actions=env.last_actions.numpy().copy(), last_dof_vel=env.last_dof_vel.numpy().copy(),
+                   feet_air_time=env.feet_air_time.numpy().copy(), episode_length=env.episode_length_buf.numpy().copy(),
+                   time_out=env.time_out_buf.numpy().astype(np.uint8), commands=env.commands.numpy().copy(),
+                   episode_sums=np.stack([env.episode_sums[k].numpy().copy() for k in env.episode_sums]),
+                   command_sums=np.stack([env.command_sums[k].numpy().copy() for k in env.command_sums]),
+                   motor_strengths=env.motor_strengths.numpy().copy(), env_command_bins=env.env_command_bins.copy(),
+                   weights=env.curriculum.weights.copy())
+        ids = torch.tensor(np.sort(rng.choice(n, 14, replace=False)), dtype=torch.long)
+        with InjectResetRand(np.random.default_rng(seed + 100)) as inj:
+            env.reset_idx(ids)
+        k = len(ids)
+        u = np.full((k, 5), 0.5, np.float32)
+        u[:, 0] = inj.draws[0].numpy()
+        if env.custom_origins:  # torch_rand_float's (k, 2) draw (made in the fork too, into the discarded copy)
+            u[:, 3:5] = inj.draws[1].numpy()
+        assert len(inj.draws) == (2 if env.custom_origins else 1)
+        ep = env.extras["train/episode"]
+        res = dict(ids=ids.numpy(), u=u, root=env.all_root_states.numpy().copy(),
+                   dof_pos=env.dof_pos.numpy().copy(), dof_vel=env.dof_vel.numpy().copy(),
+                   all_dof=env.all_dof_state.view(n, 12, 2).numpy().copy(),
+                   motor_strengths=env.motor_strengths.numpy().copy(), last_actions=env.last_actions.numpy().copy(),
+                   last_dof_vel=env.last_dof_vel.numpy().copy(), feet_air_time=env.feet_air_time.numpy().copy(),
+                   episode_length=env.episode_length_buf.numpy().copy(), reset=env.reset_buf.numpy().astype(np.uint8),
+                   commands=env.commands.numpy().copy(),
+                   episode_sums=np.stack([env.episode_sums[k_].numpy().copy() for k_ in env.episode_sums]),
+                   command_sums=np.stack([env.command_sums[k_].numpy().copy() for k_ in env.command_sums]),
+                   env_command_bins=env.env_command_bins.copy(), weights=env.curriculum.weights.copy(),
+                   env_bins=env.extras["env_bins"].numpy().copy(), time_outs=env.extras["time_outs"].numpy().astype(np.uint8),
+                   ep_keys=np.array(sorted(ep)), ep_values=np.array([float(ep[k_]) for k_ in sorted(ep)]),
+                   lin_vel_x=np.array(cfg.command_ranges["lin_vel_x"], np.float64),
+                   ang_vel_yaw=np.array(cfg.command_ranges["ang_vel_yaw"], np.float64),
+                   lin_vel_x0=np.array(ranges0["lin_vel_x"]), ang_vel_yaw0=np.array(ranges0["ang_vel_yaw"]),
+                   common_step_counter=np.array(env.common_step_counter))
+        for key, v in inp.items():
+            out[f"{case}/in_{key}"] = v
+        for key, v in res.items():
+            out[f"{case}/{key}"] = v
+        print("reset", case, "ranges", ranges0, "->", cfg.command_ranges["lin_vel_x"], cfg.command_ranges["ang_vel_yaw"],
+              "extras", sorted(ep))
+    np.savez_compressed(os.path.join(HERE, "reset.npz"), **out)
+
+
 def gen_high_level(n=32, T=40, seed=5):
     """HighLevelControlWrapper (scripts/high_level_play.py:30-363) driven over the scripted low-level env of
     fake_ll_env.py (the reference constructor's _load_env is replaced by it; its hard-coded cuda:0 tensors are
@@ -733,6 +894,9 @@ def gen_high_level(n=32, T=40, seed=5):
 if __name__ == "__main__":
     gens = dict(post_physics_mc=lambda: gen_post_physics("mc"), post_physics_go1=lambda: gen_post_physics("go1"),
                 curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint, terrain=gen_terrain,
-                heights=gen_heights, terrain_curriculum=gen_terrain_curriculum, high_level=gen_high_level)
+                heights=gen_heights, terrain_curriculum=gen_terrain_curriculum, high_level=gen_high_level,
+                reset=gen_reset,
+                post_physics_all_terms=lambda: gen_post_physics("mc", tweak=_all_terms_tweak, seed=9,
+                                                                name="post_physics_all_terms.npz"))
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()

@@ -3,7 +3,7 @@
 import numpy as np
 import pytest
 
-from helpers import golden, make
+from helpers import POST_PHYSICS, golden, make
 from oracle import oracle
 from lrl import _abi
 from lrl import params as lparams
@@ -43,12 +43,16 @@ def _state_from_golden(g, cfg, M, P):
     return st
 
 
-@pytest.mark.parametrize("robot", ["mc", "go1"])
-def test_oracle_post_physics_matches_reference(robot):
+@pytest.mark.parametrize("case", list(POST_PHYSICS))
+def test_oracle_post_physics_matches_reference(case):
     """LeggedRobot.step with identity physics: torques, obs, priv-obs, rewards, sums, termination,
     teleport and DR redraw, 3 consecutive steps (stateful feet_air_time / last_*)."""
-    g = golden(f"post_physics_{robot}.npz")
-    cfg, rob, M, P = make(robot)
+    robot, fixture, over = POST_PHYSICS[case]
+    g = golden(fixture)
+    cfg, rob, M, P = make(robot, **over)
+    keys = lparams.reward_layout(cfg)[0]
+    assert [k for k in keys if k != "termination"] == [str(k) for k in g["reward_names"]]
+    assert keys + ["total"] == [str(k) for k in g["episode_sum_keys"]]
     st = _state_from_golden(g, cfg, M, P)
     flags = _abi.STEP_INJECT_UNIFORM
     for s in range(g["root_in"].shape[0]):
@@ -82,3 +86,31 @@ def test_oracle_gae_matches_reference():
     ret, adv = oracle.gae(g["rewards"], g["dones"], g["values"], g["last_values"], 0.99, 0.95)
     np.testing.assert_allclose(ret, g["returns"], rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(adv, g["advantages"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("case,robot,mode", [("mc_fork", "mc", 0), ("go1_fork", "go1", 1), ("go1_up", "go1", 2)])
+def test_reset_device_part_matches_reference(case, robot, mode):
+    """oracle.reset_idx_device against the reference's reset_idx (reset.npz): DR redraw, dof and root reset (the
+    fork's Q4 for custom origins, the plane path, the upstream spawn draw over unequal init ranges), zeroing."""
+    g = golden("reset.npz")
+    f = lambda k: g[f"{case}/{k}"]
+    over = {}
+    if case == "go1_up":
+        over = {"terrain.mesh_type": "trimesh", "terrain.x_init_range": -0.5, "terrain.y_init_range": 0.75,
+                "terrain.x_init_offset": 0.25, "terrain.y_init_offset": -0.125}
+    cfg, rob, M, P = make(robot, **over)
+    n = f("in_root").shape[0]
+    st = {"root": f("in_root").copy(), "dof_pos": f("in_dof_pos").copy(), "dof_vel": f("in_dof_vel").copy(),
+          "env_origins": f("in_env_origins"), "last_actions": f("in_last_actions").copy(),
+          "last_dof_vel": f("in_last_dof_vel").copy(), "feet_air_time": f("in_feet_air_time").copy(),
+          "episode_length": f("in_episode_length").astype(np.int32), "reset": np.zeros(n, np.uint8),
+          "motor_strength": f("in_motor_strengths").copy(), "kp": np.ones((n, 12), np.float32),
+          "kd": np.ones((n, 12), np.float32)}
+    t = cfg.terrain
+    oracle.reset_idx_device(P, st, f("ids"), f("u"), mode, float(t.x_init_range),
+                            float(t.y_init_range) - float(t.x_init_range), float(t.x_init_offset), float(t.y_init_offset))
+    for k, ref in (("root", "root"), ("dof_pos", "dof_pos"), ("dof_vel", "dof_vel"),
+                   ("motor_strength", "motor_strengths"), ("last_actions", "last_actions"),
+                   ("last_dof_vel", "last_dof_vel"), ("feet_air_time", "feet_air_time"),
+                   ("episode_length", "episode_length"), ("reset", "reset")):
+        np.testing.assert_array_equal(st[k], f(ref), err_msg=k)

@@ -13,7 +13,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import golden, make_rough
+from helpers import (SEP_EPS, VEL_EPS, golden, make_rough, oracle_sensitivity, perturb_state,
+                     physics_mismatch)
 from lrl import _abi
 from lrl import config as lcfg
 from oracle import oracle
@@ -137,23 +138,27 @@ def test_rough_terrain_physics_matches_oracle():
     dr = np.full(n, np.nan, np.float32)
     flags = _abi.STEP_PHYSICS | _abi.STEP_INJECT_UNIFORM
     _step_raw(env, _dev(act), flags, _dev(noise), _dev(dr))
-    oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr)
+    margins = np.zeros((n, 2))
+    st_p = perturb_state(st, np.random.default_rng(78))
+    oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr, margins=margins)
+    oracle.env_step(M, P, st_p, act, flags, noise_u=noise, dr_u=dr)
+    sens = oracle_sensitivity(st, st_p)
     got = {k: _np(getattr(env, a)) for k, a in dict(root="root_states", dof_pos="dof_pos", dof_vel="dof_vel",
                                                       contact="contact_forces", h="measured_heights").items()}
-    # fp32 kernel vs double oracle after 4 sub-steps against the mesh; tolerances as for the plane
-    # (test_env_gpu.py) — >= 95 % of envs here: besides contacts appearing at the contact_offset boundary,
-    # the nearest triangle can flip between fp32 and fp64 at mesh edges / step corners.
-    def frac_ok(a, b, atol, rtol=0.0):
-        err = np.abs(a - b) - rtol * np.abs(b)
-        return np.mean(np.all(err.reshape(n, -1) <= atol, axis=1))
+    # fp32 kernel vs double oracle after 4 sub-steps against the mesh, tolerances as for the plane
+    # (helpers.physics_mismatch): every env, except those on a contact-model discontinuity — a contact at the
+    # contact_offset boundary, and on the mesh a nearest-triangle flip with a different normal or a switch of the
+    # normal rule (step edges / corners) — which are counted and bounded
     contacts = (np.abs(st["contact"]).sum((1, 2)) > 0).mean()
     assert contacts > 0.5, contacts  # the poses do touch the terrain
-    assert frac_ok(got["root"][:, :3], st["root"][:, :3], 2e-4) >= 0.95
-    assert frac_ok(got["root"][:, 3:7], st["root"][:, 3:7], 2e-4) >= 0.95
-    assert frac_ok(got["dof_pos"], st["dof_pos"], 2e-3) >= 0.95
-    assert frac_ok(got["dof_vel"], st["dof_vel"], 5e-2, 1e-2) >= 0.95
-    assert frac_ok(got["root"][:, 7:], st["root"][:, 7:], 5e-2, 1e-2) >= 0.95
-    assert frac_ok(got["contact"], st["contact"], 2.0, 0.02) >= 0.95
+    bad, excl = physics_mismatch(got, st, margins, sens)
+    print(f"terrain n={n}: {excl.sum()} envs excluded (discontinuity margin "
+          f"{((margins[:, 0] < SEP_EPS) | (margins[:, 1] < VEL_EPS)).sum()}, oracle-sensitive {sens.sum()}), "
+          f"{bad.sum()} outside tolerance")
+    for e in np.flatnonzero(bad)[:4]:  # diagnostics of a failure
+        print(e, "margins", margins[e], "root", got["root"][e] - st["root"][e], "dq", got["dof_pos"][e] - st["dof_pos"][e])
+    assert bad.sum() == 0, np.flatnonzero(bad)[:16]
+    assert excl.mean() <= 0.25, excl.mean()
     assert np.isfinite(got["root"]).all() and np.isfinite(got["dof_vel"]).all()
     # the height scan runs on the post-step base pose: exact agreement wherever the poses agree exactly is not
     # expected (fp32 vs fp64 physics), so compare the scan of the GPU's own final pose through the oracle
@@ -171,7 +176,9 @@ def test_rough_terrain_standing_and_curriculum():
     cfg = _rough_cfg(n, 3.0, **{"terrain.num_rows": 6, "terrain.num_cols": 4, "noise.add_noise": False,
                                 "domain_rand.randomize_com_displacement": False,
                                 "domain_rand.randomize_base_mass": False})
-    env = LeggedRobotEnv("cuda:0", cfg=cfg, seed=1)
+    # upstream semantics: reset_idx places the robots at base_init_state over their tile origin (the fork leaves
+    # custom-origin roots where they are, SURVEY Q4, so its robots would start at the creation pose on the ground)
+    env = LeggedRobotEnv("cuda:0", cfg=cfg, seed=1, legacy_fork=False)
     env.reset()
     zero = torch.zeros(n, 12, device="cuda:0")
     for _ in range(100):
