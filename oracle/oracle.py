@@ -25,16 +25,33 @@ def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+def _load(path):
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    L.lrlo_env_step.restype = C.c_int
+    L.lrlo_physics_substep.restype = C.c_int
+    L.lrlo_energy.restype = C.c_double
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(SO):
-            build()
-        _lib = C.CDLL(SO)
-        _lib.lrlo_env_step.restype = C.c_int
-        _lib.lrlo_physics_substep.restype = C.c_int
-        _lib.lrlo_energy.restype = C.c_double
+        _lib = _load(SO)
     return _lib
+
+
+_cpu_lib = None
+
+
+def cpu_lib():
+    """The same source built in float with OpenMP over envs (oracle/Makefile liblrl_cpu.so): bench.py's CPU
+    baseline; thread count from OMP_NUM_THREADS."""
+    global _cpu_lib
+    if _cpu_lib is None:
+        _cpu_lib = _load(os.path.join(HERE, "build", "liblrl_cpu.so"))
+    return _cpu_lib
 
 
 ENV_FIELDS = ["root", "dof_pos", "dof_vel", "contact", "torques", "actions", "last_actions", "last_dof_vel",
@@ -71,14 +88,15 @@ def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs, num_height_points=0
 
 
 def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_step_counter=1, noise_u=None,
-             dr_u=None, margins=None):
+             dr_u=None, margins=None, library=None):
     """In-place LeggedRobot.step on a logical-layout state dict (see make_state).  ``margins``: optional float64
     [n, 2] array that receives each env's discontinuity margins of this step (lrl_oracle.c g_margin_*): the
     smallest |separation - contact_offset| over its spheres and sub-steps, and the smallest |u_n +
     bounce_threshold_velocity| of a contact with restitution."""
     if margins is not None:
         assert margins.dtype == np.float64 and margins.flags["C_CONTIGUOUS"] and margins.shape == (state["root"].shape[0], 2)
-    lib().lrlo_set_margin_out(margins.ctypes.data_as(C.c_void_p) if margins is not None else None)
+    L = library or lib()
+    L.lrlo_set_margin_out(margins.ctypes.data_as(C.c_void_p) if margins is not None else None)
     for k in ENV_FIELDS:
         a = state[k]
         assert a.flags["C_CONTIGUOUS"] and a.dtype == _dtype(k), k
@@ -87,7 +105,7 @@ def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_
     act = np.ascontiguousarray(actions, np.float32)
     nu = np.ascontiguousarray(noise_u, np.float32) if noise_u is not None else None
     du = np.ascontiguousarray(dr_u, np.float32) if dr_u is not None else None
-    rc = lib().lrlo_env_step(C.byref(model), C.byref(params), C.c_int32(n), C.c_int64(env_offset),
+    rc = L.lrlo_env_step(C.byref(model), C.byref(params), C.c_int32(n), C.c_int64(env_offset),
                              C.c_uint64(seed), C.c_int64(common_step_counter), C.byref(e),
                              act.ctypes.data_as(C.c_void_p), C.c_uint32(flags),
                              nu.ctypes.data_as(C.c_void_p) if nu is not None else None,

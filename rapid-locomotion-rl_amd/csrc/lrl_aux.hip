@@ -9,9 +9,10 @@
 
 namespace lrl {
 
-// The reset / curriculum kernels follow torch's float32 op order exactly (the build uses
-// -ffp-contract=fast-honor-pragmas, so this pragma really keeps multiply-adds unfused; __fmul_rn / __fadd_rn alone
-// are plain operators in HIP and do not).
+// The reset / curriculum kernels follow torch's float32 op order exactly: plain operators under this pragma (the
+// build uses -ffp-contract=fast-honor-pragmas, so it really keeps multiply-adds unfused).  Not __fmul_rn / __fadd_rn:
+// HIP defines them as plain operators in its own header, where contraction is on, so a product inlined from them
+// still fuses with the sum around it.
 #pragma clang fp contract(off)
 
 // reset_idx (legged_robot.py:227-290) device part: _randomize_dof_props (:544-560), _reset_dofs
@@ -41,7 +42,7 @@ __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int3
     u[4] = lrl_u01(r2.v[0]);
   }
   // torch.rand(k) * (max - min) + min: two float32 roundings, the span rounded once from the python floats
-  auto draw = [](float uu, float span, float lo) { return __fadd_rn(__fmul_rn(uu, span), lo); };
+  auto draw = [](float uu, float span, float lo) { return uu * span + lo; };
   if (P.randomize_motor_strength) {
     float v = draw(u[0], P.dr_span[0], P.motor_strength_range[0]);
     for (int j = 0; j < 12; ++j) S.motor_strength[j * N + e] = v;
@@ -64,10 +65,10 @@ __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int3
     // torch_rand_float(lo, hi, (k, 2)) = (hi - lo) * rand + lo, xy_span = float32(hi - lo) from the host
     for (int c = 0; c < 13; ++c) {
       float v = P.base_init_state[c];
-      if (c < 3) v = __fadd_rn(v, S.env_origins[c * N + e]);
+      if (c < 3) v = v + S.env_origins[c * N + e];
       if (root_mode == 2 && c < 2) {
-        v = __fadd_rn(v, __fadd_rn(__fmul_rn(xy_span, u[3 + c]), xy_lo));
-        v = __fadd_rn(v, c == 0 ? x_off : y_off);
+        v = v + (xy_span * u[3 + c] + xy_lo);
+        v = v + (c == 0 ? x_off : y_off);
       }
       S.root[c * N + e] = v;
     }
@@ -88,12 +89,12 @@ __global__ void terrain_curriculum_kernel(KState S, const int32_t* __restrict__ 
   const int e = ids[t];
   if (e < 0 || e >= S.n) return;
   const int N = S.stride;
-  const float dx = __fsub_rn(S.root[e], S.env_origins[e]), dy = __fsub_rn(S.root[N + e], S.env_origins[N + e]);
-  const float dist = __fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+  const float dx = S.root[e] - S.env_origins[e], dy = S.root[N + e] - S.env_origins[N + e];
+  const float dist = sqrtf(dx * dx + dy * dy);
   const float c0 = S.commands[e], c1 = S.commands[N + e];
-  const float cn = __fsqrt_rn(__fadd_rn(__fmul_rn(c0, c0), __fmul_rn(c1, c1)));
+  const float cn = sqrtf(c0 * c0 + c1 * c1);
   const bool up = dist > half;
-  const bool down = dist < __fmul_rn(__fmul_rn(cn, ep_len_s), 0.5f) && !up;
+  const bool down = dist < (cn * ep_len_s) * 0.5f && !up;
   int64_t lv = levels[e] + (up ? 1 : 0) - (down ? 1 : 0);
   lv = lv >= max_level ? rnd[t] : (lv < 0 ? 0 : lv);
   levels[e] = lv;

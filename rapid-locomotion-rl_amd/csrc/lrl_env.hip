@@ -52,6 +52,12 @@ __device__ unsigned long long g_env_prof[16];
 #define LRL_PROF_DECL
 #define LRL_PROF(i)
 #endif
+// Terrain-contact debug records (build with -DLRL_ENV_DEBUG; buffer set with lrl_debug_env_buffer): per env and
+// sphere 8 floats — candidate flag, separation found, world centre (x, y, z), window max, radius, 1 — of the last
+// sub-step of the launch (scripts/terrain_debug.py runs one sub-step per launch).
+#ifdef LRL_ENV_DEBUG
+__device__ float* g_env_dbg;
+#endif
 
 struct V3 {
   float x, y, z;
@@ -197,14 +203,6 @@ struct Lds {
   __device__ __forceinline__ float Kx(int l, int j, int r) const { return leg(l, 18 + 6 * j + r); }
   __device__ __forceinline__ float Di(int l, int k) const { return leg(l, 36 + k); }
 };
-
-// uniform-index read of a 12-entry register array without dynamic register indexing
-__device__ __forceinline__ float pick12(const float* a, int i) {
-  float v = a[0];
-#pragma unroll
-  for (int k = 1; k < 12; ++k) v = (i == k) ? a[k] : v;
-  return v;
-}
 
 __device__ __forceinline__ void chol6(float* L) {
 #pragma unroll
@@ -563,9 +561,9 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
   }
 }
 
-struct Body {  // per-lane env state during the step
+struct Body {  // per-lane env state during the step: the base in every lane of the quad, the joints of the lane's leg
   float pos[3], quat[4], V[3], W[3];
-  float q[12], qd[12];
+  float q[3], qd[3];  // joints 3 ql .. 3 ql + 2 (the whole 12 are gathered over the quad for the post-physics)
 };
 
 
@@ -701,10 +699,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   const M3 R = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
   const V3 wb = mulT(R, v3(st.W[0], st.W[1], st.W[2]));
   const V3 vb = mulT(R, v3(st.V[0], st.V[1], st.V[2])) - cross(wb, cb);
-  float nu[18];
+  float nu[9];  // base twist (6), then this lane's leg joint rates (3)
   nu[0] = wb.x; nu[1] = wb.y; nu[2] = wb.z; nu[3] = vb.x; nu[4] = vb.y; nu[5] = vb.z;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) nu[6 + j] = st.qd[j];
+  for (int j = 0; j < 3; ++j) nu[6 + j] = st.qd[j];
   const V3 gb = mulT(R, v3(P.gravity[0], P.gravity[1], P.gravity[2]));
   const SV v0 = SV{wb, vb};
   const SV a0 = SV{v3(0.f, 0.f, 0.f), v3(-gb.x, -gb.y, -gb.z)};
@@ -732,11 +730,11 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     M.sph(s, 1) = x.y;
     M.sph(s, 2) = x.z;
     V3 u = cross(wb, x) + vb;
-    if (lsel >= 0) {
+    if (lsel >= 0) {  // (a sphere recorded by this lane: its leg is the lane's own)
       V3 c[3];
       leg_dirs(M, lsel, link, x, c);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) u = u + pick12(st.qd, 3 * lsel + j) * c[j];
+      for (int j = 0; j < 3; ++j) u = u + st.qd[j] * c[j];
     }
     const float u0 = dot(nb, u);
     float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
@@ -760,6 +758,14 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       M.sph(s, 7) = pw.y;
       M.sph(s, 8) = pw.z;
       if (pw.z - rad - P.contact_offset <= hwin) cand |= 1ull << s;
+#ifdef LRL_ENV_DEBUG
+      {
+        const int e_ = blockIdx.x * ENVS + (int)(threadIdx.x >> 2);
+        float* d = g_env_dbg + ((size_t)e_ * 64 + s) * 8;
+        d[0] = (float)((cand >> s) & 1ull); d[1] = 1e30f; d[2] = pw.x; d[3] = pw.y; d[4] = pw.z; d[5] = hwin;
+        d[6] = rad; d[7] = 1.f;
+      }
+#endif
       return;
     }
     const float sep = pz + dot(Rz, x) - rad;
@@ -772,7 +778,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (lsel >= 0) {
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (j <= link) u = u + pick12(st.qd, 3 * lsel + j) * cross(aa[j], x - oo[j]);
+          if (j <= link) u = u + st.qd[j] * cross(aa[j], x - oo[j]);
       }
       const float u0 = dot(Rz, u);
       float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
@@ -805,7 +811,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #pragma unroll
       for (int k = 0; k < 9; ++k) Rf.m[k] = kl.rfix[j][k];
       const V3 ax = v3(kl.axis[j][0], kl.axis[j][1], kl.axis[j][2]);
-      const M3 Rj = mul(mul(Rp, Rf), axis_rot(ax, pick12(st.q, 3 * l + j)));
+      const M3 Rj = mul(mul(Rp, Rf), axis_rot(ax, st.q[j]));
       const V3 o = op + mul(Rp, v3(kl.xyz[j][0], kl.xyz[j][1], kl.xyz[j][2]));
       const V3 a = mul(Rj, ax);
       M.leg(l, 3 * j) = a.x; M.leg(l, 3 * j + 1) = a.y; M.leg(l, 3 * j + 2) = a.z;
@@ -855,7 +861,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     SV vj = v0, aj = a0, f[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const SV sq = scale(S[j], pick12(st.qd, 3 * l + j));
+      const SV sq = scale(S[j], st.qd[j]);
       vj = vj + sq;
       aj = aj + crm(vj, sq);
       f[j] = simul(Ij[j], aj) + crf(vj, simul(Ij[j], vj));
@@ -877,6 +883,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         const THit th = terrain_query(K, v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8)), M.sph4(s).w, P.contact_offset,
                                       reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS),
                                       (int)threadIdx.x);
+#ifdef LRL_ENV_DEBUG
+        g_env_dbg[((size_t)(blockIdx.x * ENVS + (int)(threadIdx.x >> 2)) * 64 + s) * 8 + 1] = th.sep;
+#endif
         if (th.sep < P.contact_offset) {
           M.sph(s, 3) = th.n.x;
           M.sph(s, 4) = th.n.y;
@@ -931,22 +940,18 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #pragma unroll
       for (int r = 0; r < 6; ++r) pb[r] = quad_sum(pb[r]) - cbv[r];
     }
-    __syncthreads();  // leg blocks of the other lanes are read below
     float xb[6];
     sym6mul(Sch, pb, xb);
 #pragma unroll
     for (int r = 0; r < 6; ++r) nu[r] += dt * xb[r];
+    // this lane's leg (its own K and y_l rows: no other lane's data, no barrier)
 #pragma unroll
-    for (int r = 0; r < 6; ++r) pb[r] = xb[r];
+    for (int j = 0; j < 3; ++j) {
+      float kx = 0.f;
 #pragma unroll
-    for (int l = 0; l < 4; ++l)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        float kx = 0.f;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) kx += M.Kx(l, j, r) * pb[r];
-        nu[6 + 3 * l + j] += dt * (M.leg(l, 42 + j) - kx);
-      }
+      for (int r = 0; r < 6; ++r) kx += M.Kx(ql, j, r) * xb[r];
+      nu[6 + j] += dt * (M.leg(ql, 42 + j) - kx);
+    }
   }
   LRL_PROF(1)  // Schur complement factor / inverse, free acceleration
   // contact solve.  Start state: v_b0 = free base velocity, qd0 = free joint rates (LDS), Y = 0.
@@ -960,7 +965,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       float k = 0.f;
 #pragma unroll
       for (int r = 0; r < 6; ++r) k += M.Kx(l, j, r) * vb0[r];
-      M.leg(l, 45 + j) = pick12(nu + 6, 3 * l + j) + k;
+      M.leg(l, 45 + j) = nu[6 + j] + k;
       M.leg(l, 48 + j) = 0.f;
     }
   }
@@ -1019,19 +1024,18 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   }
   __syncthreads();  // the leg accumulators each lane owned are read by the whole quad below
   LRL_PROF(3)  // PGS iterations
-  // materialise the lazily propagated joint rates
+  // materialise the lazily propagated joint rates of this lane's leg
 #pragma unroll
   for (int r = 0; r < 6; ++r) nu[r] = vbc[r];
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-    const V3 q = leg_qd(M, l, vbc);
-    nu[6 + 3 * l] = q.x;
-    nu[6 + 3 * l + 1] = q.y;
-    nu[6 + 3 * l + 2] = q.z;
+  {
+    const V3 q = leg_qd(M, ql, vbc);
+    nu[6] = q.x;
+    nu[7] = q.y;
+    nu[8] = q.z;
   }
   // semi-implicit integration
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
+  for (int j = 0; j < 3; ++j) {
     st.qd[j] = nu[6 + j];
     st.q[j] += dt * st.qd[j];
   }
@@ -1195,9 +1199,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 #pragma unroll
   for (int k = 0; k < 4; ++k) st.quat[k] = S.root[(3 + k) * N + e];
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    st.q[j] = S.dof_pos[j * N + e];
-    st.qd[j] = S.dof_vel[j * N + e];
+  for (int j = 0; j < 3; ++j) {
+    st.q[j] = S.dof_pos[(3 * ql + j) * N + e];
+    st.qd[j] = S.dof_vel[(3 * ql + j) * N + e];
   }
   float act[12], tau[12];
   {
@@ -1259,7 +1263,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   for (int sub = 0; sub < P.decimation; ++sub) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      float t = kp3[j] * (tg3[j] - pick12(st.q, 3 * ql + j)) - kd3[j] * pick12(st.qd, 3 * ql + j);
+      float t = kp3[j] * (tg3[j] - st.q[j]) - kd3[j] * st.qd[j];
       t = t * ms3[j];
       tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
     }
@@ -1269,11 +1273,16 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     prof_t = clock64();
 #endif
   }
-  // the last sub-step's torques of all 12 joints (rewards, torques buffer): from the quad's 4 lanes
+  // the last sub-step's torques and the joint state of all 12 joints (rewards, obs, buffers): from the quad's 4 lanes
+  float q12[12], qd12[12];
 #pragma unroll
   for (int l = 0; l < 4; ++l)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) tau[3 * l + j] = quad_bcast(tau3[j], l);
+    for (int j = 0; j < 3; ++j) {
+      tau[3 * l + j] = quad_bcast(tau3[j], l);
+      q12[3 * l + j] = quad_bcast(st.q[j], l);
+      qd12[3 * l + j] = quad_bcast(st.qd[j], l);
+    }
 #ifdef LRL_ENV_PROFILE
   prof_t = clock64();
 #endif
@@ -1393,11 +1402,15 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     int k = 0;
     lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter, (LRL_RNG_DR << 16) ^ (uint32_t)(step_counter >> 32), 0,
                              S.seed);
+    // the draw's words as scalars, selected by the runtime word index k (indexing r.v[k] directly would put the
+    // array in scratch)
+    const uint32_t w0 = r.v[0], w1 = r.v[1], w2 = r.v[2];
+    auto word = [&](int i) { return i == 0 ? w0 : (i == 1 ? w1 : w2); };
     if (P.randomize_motor_strength) {
-      float u = inject ? (valid ? S.inj_dr[e] : 0.5f) : lrl_u01(r.v[k]);
+      float u = inject ? (valid ? S.inj_dr[e] : 0.5f) : lrl_u01(word(k));
       k++;
       // torch.rand * (max - min) + min: two float32 roundings, the span rounded from the python-float difference
-      float v = __fadd_rn(__fmul_rn(u, P.dr_span[0]), P.motor_strength_range[0]);
+      float v = u * P.dr_span[0] + P.motor_strength_range[0];
 #pragma unroll
       for (int j = 0; j < 12; ++j) {
         ms_e[j] = v;
@@ -1405,14 +1418,14 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       }
     }
     if (P.randomize_kp) {
-      float u = lrl_u01(r.v[k++]);
-      float v = __fadd_rn(__fmul_rn(u, P.dr_span[1]), P.kp_range[0]);
+      float u = lrl_u01(word(k++));
+      float v = u * P.dr_span[1] + P.kp_range[0];
 #pragma unroll
       for (int j = 0; j < 12; ++j) S.kp[j * N + e] = v;
     }
     if (P.randomize_kd) {
-      float u = lrl_u01(r.v[k++]);
-      float v = __fadd_rn(__fmul_rn(u, P.dr_span[2]), P.kd_range[0]);
+      float u = lrl_u01(word(k++));
+      float v = u * P.dr_span[2] + P.kd_range[0];
 #pragma unroll
       for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
     }
@@ -1443,19 +1456,19 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
         break;
       case LRL_R_ENERGY:
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r += tau[j] * st.qd[j];
+        for (int j = 0; j < 12; ++j) r += tau[j] * qd12[j];
         break;
       case LRL_R_ENERGY_EXPENDITURE:
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r += fmaxf(tau[j] * st.qd[j], 0.f);
+        for (int j = 0; j < 12; ++j) r += fmaxf(tau[j] * qd12[j], 0.f);
         break;
       case LRL_R_DOF_VEL:
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r += sq(st.qd[j]);
+        for (int j = 0; j < 12; ++j) r += sq(qd12[j]);
         break;
       case LRL_R_DOF_ACC:
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r += sq((lqd[j] - st.qd[j]) / P.dt);
+        for (int j = 0; j < 12; ++j) r += sq((lqd[j] - qd12[j]) / P.dt);
         break;
       case LRL_R_ACTION_RATE:
 #pragma unroll
@@ -1466,15 +1479,15 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       case LRL_R_DOF_POS_LIMITS:
 #pragma unroll
         for (int j = 0; j < 12; ++j) {
-          float o = -fminf(st.q[j] - P.soft_dof_pos_lower[j], 0.f);
-          o += fmaxf(st.q[j] - P.soft_dof_pos_upper[j], 0.f);
+          float o = -fminf(q12[j] - P.soft_dof_pos_lower[j], 0.f);
+          o += fmaxf(q12[j] - P.soft_dof_pos_upper[j], 0.f);
           r += o;
         }
         break;
       case LRL_R_DOF_VEL_LIMITS:
 #pragma unroll
         for (int j = 0; j < 12; ++j)
-          r += fminf(fmaxf(fabsf(st.qd[j]) - P.dof_vel_limits[j] * P.soft_dof_vel_limit, 0.f), 1.f);
+          r += fminf(fmaxf(fabsf(qd12[j]) - P.dof_vel_limits[j] * P.soft_dof_vel_limit, 0.f), 1.f);
         break;
       case LRL_R_TORQUE_LIMITS:
 #pragma unroll
@@ -1507,7 +1520,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       case LRL_R_STAND_STILL: {
         float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
 #pragma unroll
-        for (int j = 0; j < 12; ++j) r += fabsf(st.q[j] - P.default_dof_pos[j]);
+        for (int j = 0; j < 12; ++j) r += fabsf(q12[j] - P.default_dof_pos[j]);
         r = r * (cn < 0.1f ? 1.f : 0.f);
       } break;
       case LRL_R_FEET_CONTACT_FORCES:
@@ -1573,7 +1586,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 
   // observations / privileged observations -> LDS tiles [env slot][.]
   LRL_PROF(12)  // rewards, termination, episode / command sums
-  obs_values(P, blv, bav, pg, cmd, st.q, st.qd, act, otile + es * NO);
+  obs_values(P, blv, bav, pg, cmd, q12, qd12, act, otile + es * NO);
   priv_row(P, S, e, payload, cb, ms_e, ptile + es * LRL_NUM_PRIV);
 
   LRL_PROF(13)  // obs / priv rows
@@ -1588,13 +1601,13 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   for (int k = 0; k < 4; ++k) S.root[(3 + k) * N + e] = st.quat[k];
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    S.dof_pos[j * N + e] = st.q[j];
-    S.dof_vel[j * N + e] = st.qd[j];
+    S.dof_pos[j * N + e] = q12[j];
+    S.dof_vel[j * N + e] = qd12[j];
     S.torques[j * N + e] = tau[j];
     S.joint_pos_target[j * N + e] = pos_target(P, act, j);
     S.actions[j * N + e] = act[j];
     S.last_actions[j * N + e] = act[j];
-    S.last_dof_vel[j * N + e] = st.qd[j];
+    S.last_dof_vel[j * N + e] = qd12[j];
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -1691,6 +1704,15 @@ extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
 #else
   (void)out;
   (void)reset;
+  return 0;
+#endif
+}
+
+extern "C" int lrl_debug_env_buffer(float* buf) {
+#ifdef LRL_ENV_DEBUG
+  return hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_dbg), &buf, sizeof(buf)) == hipSuccess ? 1 : -2;
+#else
+  (void)buf;
   return 0;
 #endif
 }
