@@ -298,12 +298,15 @@ __device__ __forceinline__ V3 leg_qd(const Lds& M, int L, const float* vb) {
 // Terrain mesh contact (own model; PhysX's trimesh / heightfield collision is closed): the sphere centre p
 // is tested against the 18 triangles of the 3x3 grid cells around it (vertex moves of the slope-corrected
 // trimesh are at most one cell, so every triangle within a cell of p is among them); the triangle whose
-// closest point is nearest wins (ties: first in cell order).  Inside its face region, or with p below its
-// plane, the contact normal is the face normal and the separation the signed plane distance minus r;
-// against an edge or vertex from outside, the normal points from the closest point to p and the separation
-// is the distance minus r.  Triangles whose xy bounding box, grown by r + contact_offset, does not hold p's xy
-// are skipped (part of the model: the oracle applies the same rule); a conservative max-height map skips the
-// test for spheres clear of the terrain.
+// closest point q is nearest wins (ties: first in cell order).  The separation is the signed distance to the
+// terrain surface minus r: |p - q| with the sign of the height-field test — p is inside the terrain when it is
+// below the plane of the triangle under it (the triangle whose xy projection holds p's xy; all triangles face
+// up) — so a centre above every vertex is never inside, whatever the slope of the nearest triangle.  The normal
+// is the winning face normal inside its face region and otherwise the direction from p towards the outside
+// ((p - q) / |p - q| above the surface, (q - p) / |p - q| below).  With no triangle under p (degenerate cells)
+// the sign falls back to the winning triangle's plane.  Triangles whose xy bounding box, grown by
+// r + contact_offset, does not hold p's xy are skipped (part of the model: the oracle applies the same rule);
+// a conservative max-height map skips the test, exactly, for spheres clear of the terrain.
 // ------------------------------------------------------------------------------------------------
 struct THit {
   float sep;
@@ -357,6 +360,17 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
 #pragma unroll
     for (int b = 0; b < 4; ++b) V[a][b] = vtx[vi * Cn + min(max(cj - 1 + b, 0), Cn - 1)];
   }
+  // local frame at vertex (ci, cj): differences of nearby fp32 coordinates are exact (Sterbenz), so the walk
+  // resolves distances to ~1e-8 m instead of the ~2e-6 m ulp of world coordinates 20-40 m from the origin
+  // (nearest-triangle ties between coplanar neighbours then go the way the exact geometry does)
+  {
+    const float4 O = V[1][1];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) V[a][b] = make_float4(V[a][b].x - O.x, V[a][b].y - O.y, V[a][b].z - O.z, 0.f);
+    p = p - v3(O.x, O.y, O.z);
+  }
   // triangles (bit 2 * (3 di + dj) + t) whose xy bounding box grown by g holds p's xy: a triangle under / over p
   // always qualifies, so penetrating spheres keep the triangle they are in
   uint32_t tris = 0;
@@ -382,6 +396,7 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   float best = 3.0e38f;
   V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
   bool bface = true;
+  int under = -1;  // height-field side of p from the triangle under it: 1 above / on, 0 below, -1 none found
   // each lane walks its own marked triangles in order (the wave runs max-over-lanes triangles, not 18)
   while (__any((int)(tris != 0u))) {
     if (tris) {
@@ -394,6 +409,13 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
       const V3 va = v3(fa.x, fa.y, fa.z), b = v3(fb.x, fb.y, fb.z), cv = v3(fc.x, fc.y, fc.z);
       const V3 nf = cross(b - va, cv - va);
       const float a2 = dot(nf, nf);
+      // under p: p's xy inside the triangle's xy projection (counter-clockwise when nf.z > 0)
+      if (nf.z > 0.f) {
+        const float wa = (b.x - p.x) * (cv.y - p.y) - (b.y - p.y) * (cv.x - p.x);
+        const float wb = (cv.x - p.x) * (va.y - p.y) - (cv.y - p.y) * (va.x - p.x);
+        const float wc = (va.x - p.x) * (b.y - p.y) - (va.y - p.y) * (b.x - p.x);
+        if (wa >= 0.f && wb >= 0.f && wc >= 0.f) under = dot(nf, p - va) >= 0.f ? 1 : 0;
+      }
       if (a2 >= 1e-12f) {  // (zero area: collapsed by the slope correction)
         bool face;
         const V3 q = closest_on_tri(p, va, b, cv, face);
@@ -410,12 +432,12 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
     }
   }
   const float dist = sqrtf(best), sd = dot(bn, p - ba);
-  if (!bface && dist > 1e-6f && sd > 0.f) {
-    h.n = (1.f / dist) * (p - bc);
-    h.sep = dist - r;
+  const bool above = under >= 0 ? under == 1 : sd >= 0.f;
+  h.sep = (above ? dist : -dist) - r;
+  if (bface || dist <= 1e-6f) {
+    h.n = (bface && (sd >= 0.f) != above) ? -1.f * bn : bn;
   } else {
-    h.n = bn;
-    h.sep = sd - r;
+    h.n = ((above ? 1.f : -1.f) / dist) * (p - bc);
   }
   return h;
 }
