@@ -43,35 +43,67 @@ def pmc_traffic(*kernels):
     return None, None
 
 
-def cpu_baseline(seconds=12.0):
-    """The CPU oracle (oracle/lrl_oracle.c: dense fp64 dynamics + fp32 bookkeeping), one core, on a
-    bounded sample of the same workload: 256 Mini Cheetah envs stepping with random actions."""
-    from oracle import oracle
-    from lrl import _abi
-    from lrl import config as lcfg
-    from lrl import params as lparams
-    from lrl.robot import load_robot
-    cfg = lcfg.make_cfg()
-    lcfg.config_mini_cheetah(cfg)
-    cfg.terrain.x_offset = 0
-    rob = load_robot("mini_cheetah.urdf")
-    P, M = lparams.build_params(cfg, rob), lparams.build_model(rob)
-    n = 256
-    st = oracle.make_state(n, M.num_bodies, P.num_obs, P.num_history, P.num_sum_keys + 1, P.num_sum_keys + 5)
-    st["root"][:, 2] = 0.32
-    st["root"][:, :2] = np.random.default_rng(0).uniform(10, 60, (n, 2))
-    st["dof_pos"][:] = np.array(P.default_dof_pos[:], np.float32)
-    st["friction"][:] = 1.0
-    rng = np.random.default_rng(1)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        oracle.env_step(M, P, st, rng.normal(size=(n, 12)).astype(np.float32) * 0.3,
-                        _abi.STEP_PHYSICS | _abi.STEP_HISTORY, common_step_counter=steps + 1)
-        steps += 1
+def _cpu_info():
+    """(threads this process may use, CPU model) — the GPU box's CPU share is its OMP_NUM_THREADS (16), nproc shows
+    the whole machine."""
+    avail = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return (min(avail, omp) if omp > 0 else avail), avail, model
+
+
+def cpu_baseline(env_seconds=4.0):
+    """CPU baseline on this box's host cores, on bounded samples of the same workload:
+    * a whole PPO iteration of configs[1] (4096 Mini Cheetah envs x 24 steps + GAE + the 5 x 4 minibatch update):
+      the env is the oracle's float + OpenMP build over all usable cores (oracle/cpu_env.py), the policy and update
+      the reference's torch PPO math on the CPU (lrl.ppo with fused=False, torch threads = the same cores) —
+      ``value`` is its env-steps/s, the unit of the headline;
+    * env-only stepping rates of the same CPU env with all usable cores and with one core (random actions).
+    The reference's own Isaac Gym CPU pipeline (PhysX CPU, num_threads=10) is proprietary and absent."""
+    from oracle.cpu_env import CpuVecEnv, cpu_compute_returns
+    from lrl.ppo import runner as R
+    threads, avail, model = _cpu_info()
+    prev_threads = torch.get_num_threads()
+
+    def env_rate(n, th):
+        env = CpuVecEnv(n, threads=th)
+        rng = np.random.default_rng(1)
+        a = torch.from_numpy((rng.normal(size=(n, 12)) * 0.3).astype(np.float32))
+        env.step(a)
+        steps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < env_seconds:
+            env.step(a)
+            steps += 1
+        return n * steps / (time.perf_counter() - t0), steps
+    env_all, n_all = env_rate(ENVS_PER_GPU, threads)
+    env_one, n_one = env_rate(256, 1)
+    torch.set_num_threads(threads)
+    env = CpuVecEnv(ENVS_PER_GPU, threads=threads)
+    runner = R.Runner(env, device="cpu", seed=1234)
+    runner.alg.storage.compute_returns = cpu_compute_returns(runner.alg.storage)
+    t0 = time.perf_counter()
+    runner.learn(1)
     dt = time.perf_counter() - t0
-    return dict(value=round(n * steps / dt, 1), unit="env-steps/s", cores=1, kind="port",
-                sample=f"{n} Mini Cheetah envs x {steps} steps ({dt:.1f} s), oracle/lrl_oracle.c, 1 thread; "
-                       "the reference's Isaac Gym CPU pipeline is proprietary and absent (BASELINE.md §3)")
+    torch.set_num_threads(prev_threads)
+    steps_iter = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env
+    return dict(value=round(steps_iter / dt, 1), unit="env-steps/s", cores=threads, kind="port",
+                ppo_iter_s=round(dt, 3),
+                env_only_all_cores_env_steps_per_s=round(env_all, 1),
+                env_only_1_core_env_steps_per_s=round(env_one, 1),
+                cpu_model=model, cpus_visible=os.cpu_count(), cpus_usable=avail,
+                sample=(f"one PPO iteration of {ENVS_PER_GPU} Mini Cheetah envs x {R.RunnerArgs.num_steps_per_env} steps "
+                        f"+ update ({dt:.1f} s; env: oracle/lrl_oracle.c float + OpenMP, {threads} threads; policy / "
+                        f"update: torch CPU, {threads} threads); env-only: {ENVS_PER_GPU} envs x {n_all} steps on "
+                        f"{threads} threads, 256 envs x {n_one} steps on 1 thread ({env_seconds:.0f} s each). The "
+                        "reference's Isaac Gym CPU pipeline is proprietary and absent (BASELINE.md §3)"))
 
 
 def bench_go1_rough(dev, iters=3, warmup=1):
@@ -269,8 +301,14 @@ def main():
         gemm_flop = 2.0 * 2 * 256 * 512 * mb_rows
         gemm_ms = g_ms.value / max(1, g_n.value)
         gemm_tf = gemm_flop / (gemm_ms * 1e-3) / 1e12 if g_n.value else None
-        # (the PMC summary keys dispatches by total grid size, which dW2 shares with dW3: no per-launch traffic)
-        gemm_traffic = None
+        # dW2 has its own symbol (trace tag 1, csrc/lrl_gemm.hip tn_shape_tag): its PMC row is this launch's traffic
+        gemm_kernel = "lrl::gemm_glds_tn_kernel<3, 128, 1>"
+        gemm_traffic, gemm_traffic_src = pmc_traffic(gemm_kernel)
+        # whole iteration against the fp32 MFMA peak: SURVEY.md §8(d)'s 3.92 MFLOP per minibatch row and epoch of
+        # the update (5 epochs over the 98,304 rollout rows) + 0.94 MFLOP per rollout row of the act
+        rows_iter = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env
+        iter_flop = rows_iter * (5 * 3.92e6 + 0.94e6)
+        iter_tf = iter_flop / (elapsed / args.steps) / 1e12
         out = {
             "metric": "env-steps/sec, 4096 Mini Cheetah envs, 1/2/4/8 MI355X; PPO iters/sec",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -292,12 +330,19 @@ def main():
                                  f"shift adds 4872 B/env-step = {4872 * ENVS_PER_GPU} B per launch); the kernel is "
                                  "latency-bound (4 lanes per env, one single-wave workgroup per 16 envs), see DESIGN.md"},
             "roofline_update_gemm": {
-                "bound": "mfma", "kernel": "lrl::gemm_glds_tn_kernel<3> (dW2: 2 x 256x512, "
-                f"{mb_rows} rows)", "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": MFMA_F32_PEAK_TF,
+                "bound": "mfma", "kernel": f"{gemm_kernel} (dW2: 2 x 256x512, {mb_rows} rows)",
+                "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": MFMA_F32_PEAK_TF,
                 "unit": "TFLOP/s", "frac": round(gemm_tf / MFMA_F32_PEAK_TF, 4) if gemm_tf else None,
-                "traffic": round(gemm_traffic) if gemm_traffic else None, "launch_ms": round(gemm_ms, 4),
-                "launches": g_n.value,
-                "note": "the GEMM family is ~70% of the iteration's GPU time; this is its largest launch"},
+                "traffic": round(gemm_traffic) if gemm_traffic else None, "traffic_source": gemm_traffic_src,
+                "algorithmic_bytes": 4 * (2 * mb_rows * (256 + 512)),
+                "launch_ms": round(gemm_ms, 4), "launches": g_n.value,
+                "note": "the GEMM family is ~70% of the iteration's GPU time; this is its largest launch "
+                        "(split-k partials written to the workspace count in traffic)"},
+            "roofline_iteration": {
+                "bound": "mfma", "achieved": round(iter_tf, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
+                "frac": round(iter_tf / MFMA_F32_PEAK_TF, 4), "flop_per_iteration": iter_flop,
+                "note": "SURVEY.md §8(d): 3.92 MFLOP per row and epoch (update) + 0.94 MFLOP per rollout row; "
+                        "the env step's work is not counted"},
             "reference_context": {"upstream_example_run_env_steps_per_s": 41176, "upstream_ppo_iters_per_s": 0.429,
                                   "hardware": "unspecified NVIDIA GPU, 4000 envs (BASELINE.md §1)"},
         }

@@ -699,7 +699,9 @@ static int launch_thin(const GemmP& p, int groups, hipStream_t st) {
 // each 64x64 (2x2 MFMA tiles); MFMA operands are ds_read_b32 of [k][m] / [k][n] (consecutive m / n per
 // lane).  The split's gathered row list is converted to int32 in LDS once.  Bias-gradient partial: column
 // sums of the dY slice (n-tile 0 workgroups).
-template <int NST, int BN>
+// SHAPE: trace tag only (the code is the same for every value): each weight-gradient shape of the update gets
+// its own symbol, so a kernel trace / PMC pass keys its launches apart (see tn_shape_tag)
+template <int NST, int BN, int SHAPE>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
   // BN = 128: 4 waves of 64x64 (2x2 MFMA tiles); BN = 64 (narrow inputs, e.g. the 60-wide actor/critic input):
   // 4 waves of 64x32
@@ -821,19 +823,45 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
     p.bias_part[((int64_t)sp * p.groups + g) * p.M + m0 + threadIdx.x] = bsum;
 }
 
-template <int BN>
-static int launch_glds_tn(const GemmP& p, int groups, hipStream_t st) {
+// trace tag of a weight-gradient shape (M x N per group, groups): 1 = the update's largest product, the actor /
+// critic layer-2 gradient (256 x 512, 2 groups); 2 = their layer 3 (128 x 256, 2 groups); 3 = their layer 1
+// (512 x 60); 4 = the adaptation module's first layer (256 x 630 history); 5 = the env-factor encoder's first
+// layer (256 x 18); 6 = its second (128 x 256, 1 group); 0 = any other shape
+static int tn_shape_tag(int M, int N, int groups) {
+  if (M == 256 && N == 512) return 1;
+  if (M == 128 && N == 256) return groups > 1 ? 2 : 6;
+  if (M == 512 && N <= 64) return 3;
+  if (M == 256 && N >= 600) return 4;
+  if (M == 256 && N <= 64) return 5;
+  return 0;
+}
+
+template <int BN, int SHAPE>
+static int launch_glds_tn_tag(const GemmP& p, int groups, hipStream_t st) {
   const size_t lds = (size_t)3 * 16 * (128 + BN) * sizeof(float) + (p.b_rows ? (size_t)p.kps * sizeof(int) : 0);
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_glds_tn_kernel<3, BN>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_glds_tn_kernel<3, BN, SHAPE>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
       return LRL_E_HIP;
     attr = true;
   }
   dim3 gt((p.M / 128) * ((p.N + BN - 1) / BN) * groups * p.splits);
-  hipLaunchKernelGGL((gemm_glds_tn_kernel<3, BN>), gt, dim3(GTHREADS), lds, st, p);
+  hipLaunchKernelGGL((gemm_glds_tn_kernel<3, BN, SHAPE>), gt, dim3(GTHREADS), lds, st, p);
   return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+}
+
+template <int BN>
+static int launch_glds_tn(const GemmP& p, int groups, hipStream_t st) {
+  switch (tn_shape_tag(p.M, p.N, groups)) {
+    case 1: return launch_glds_tn_tag<BN, 1>(p, groups, st);
+    case 2: return launch_glds_tn_tag<BN, 2>(p, groups, st);
+    case 3: return launch_glds_tn_tag<BN, 3>(p, groups, st);
+    case 4: return launch_glds_tn_tag<BN, 4>(p, groups, st);
+    case 5: return launch_glds_tn_tag<BN, 5>(p, groups, st);
+    case 6: return launch_glds_tn_tag<BN, 6>(p, groups, st);
+    default: return launch_glds_tn_tag<BN, 0>(p, groups, st);
+  }
 }
 
 template <int BM, int BN>

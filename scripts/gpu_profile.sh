@@ -25,4 +25,11 @@ for C in FETCH_SIZE WRITE_SIZE; do
   F=$(find /tmp/lrlprof/cal_$C -name "*counter_collection.csv" | head -n 1)
   python3 "$ROOT/scripts/pmc_reduce.py" "$F" "$C" > "$OUT/cal_$C.csv"
 done
+# SQ pass (one run, 8 SQ counters): wave cycles split into issue / wait / active, VALU instructions, for the
+# env kernel's latency-bound diagnosis (SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_* count quad-cycles)
+SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
+timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d /tmp/lrlprof/sq -o run -- \
+  python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-secondary > "$OUT/pmc_sq.log" 2>&1
+F=$(find /tmp/lrlprof/sq -name "*counter_collection.csv" | head -n 1)
+for C in $SQ; do python3 "$ROOT/scripts/pmc_reduce.py" "$F" "$C" > "$OUT/sq_$C.csv"; done
 ls -la "$OUT"

@@ -1,8 +1,8 @@
 """Data-parallel native PPO update on one GPU with two ranks (gloo moves the CUDA tensors; bench.py runs
 the same calls over RCCL, one GPU per rank): the flat-gradient / KL all-reduce between
 lrl_ppo_forward_backward and lrl_ppo_optimizer_step and the adaptation-gradient all-reduce keep both
-ranks' parameters bit-identical although their rollouts differ, and the update equals the single-process
-update on the averaged gradient (checked through the learning-rate schedule and finiteness)."""
+ranks' parameters bit-identical although their rollouts differ, and the all-reduced gradient is the mean of
+the single-process gradients of the two rollouts (checked on minibatch 0 against world-1 runs)."""
 import os
 import socket
 
@@ -42,11 +42,56 @@ def _worker(rank, world, port, out):
     alg.init_storage(N, T, [42], [18], [630], [12])
     _random_storage(alg, N, T, seed=11 + rank)  # different rollouts per rank
     alg.record_lr = True
+    # the first all-reduce of the update is minibatch 0's flat policy gradient + KL slot: keep it before and after
+    cap = []
+    orig = dist.all_reduce
+
+    def probe(t, *a, **k):
+        if len(cap) == 0:
+            cap.append(t.detach().cpu().numpy().copy())
+            r = orig(t, *a, **k)
+            cap.append(t.detach().cpu().numpy().copy())
+            return r
+        return orig(t, *a, **k)
+    dist.all_reduce = probe
     torch.manual_seed(5)  # same minibatch permutation on both ranks (as torch.randperm is seeded alike)
     mv, ms, ma = alg.update()
+    dist.all_reduce = orig
     flat = ac._flat.detach().cpu().numpy().copy()
-    out[rank] = (flat, list(alg.lr_trace), [mv, ms, ma])
+    out[rank] = (flat, list(alg.lr_trace), [mv, ms, ma], cap[0], cap[1])
     dist.destroy_process_group()
+
+
+def _single_process_first_grad(seed):
+    """One process, world 1: minibatch 0's flat policy gradient (+ KL slot) of the native update on the rollout
+    a rank with ``seed`` holds — captured at the first lrl_ppo_optimizer_step, before any parameter moves."""
+    from lrl import _abi
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.ppo import PPO
+    from test_ppo_gpu import _random_storage, init_params
+    ac = ActorCritic(42, 18, 630, 12)
+    init_params(ac)
+    alg = PPO(ac.cuda(), device="cuda:0", fused=True)
+    assert not alg.grad_allreduce
+    N, T = 256, 24
+    alg.init_storage(N, T, [42], [18], [630], [12])
+    _random_storage(alg, N, T, seed=seed)
+    L = _abi.lib()
+    orig = L.lrl_ppo_optimizer_step
+    cap = []
+
+    def probe(*args):
+        if not cap:
+            net = alg._native["net"]
+            cap.append(alg._native["grads"][net.main_begin:net.kl_slot + 1].detach().cpu().numpy().copy())
+        return orig(*args)
+    L.lrl_ppo_optimizer_step = probe
+    try:
+        torch.manual_seed(5)
+        alg.update()
+    finally:
+        L.lrl_ppo_optimizer_step = orig
+    return cap[0]
 
 
 @pytest.mark.timeout(300)
@@ -59,6 +104,14 @@ def test_two_rank_native_update_keeps_replicas_identical():
     assert np.isfinite(a[0]).all()
     np.testing.assert_array_equal(a[0], b[0])   # identical replicas after 20 optimiser steps
     assert a[1] == b[1] and len(a[1]) == 20     # identical device-side learning-rate schedule
+    # data parallelism = one process on the averaged gradient: each rank's local gradient is the single-process
+    # gradient of its own rollout, and the all-reduced one (scaled 1 / world in the optimiser step) is their mean
+    single = [_single_process_first_grad(11 + r) for r in range(world)]
+    for r in range(world):
+        np.testing.assert_allclose(out[r][3], single[r], rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(out[r][4] / world, (single[0] + single[1]) / world, rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(a[4], b[4])
+    assert np.abs(single[0] - single[1]).max() > 1e-3  # the two rollouts really give different gradients
 
 
 def _curriculum_cfg(n):
