@@ -170,6 +170,12 @@ typedef struct lrl_env_params {
   /* float32(hi - lo) of motor_strength_range / kp_range / kd_range with the difference taken in double, as
    * torch.rand(k) * (max - min) + min rounds the python-float difference once (legged_robot.py:544-560) */
   float dr_span[3];
+  /* joint position limits (the URDF <limit lower upper> of every revolute joint, lrl_model::dof_lower / dof_upper),
+   * enforced as unilateral joint-space rows of the contact solve, as PhysX articulations enforce URDF limits:
+   * a joint whose distance d to its nearer limit is below joint_limit_margin + 2 sim_dt |qd| gets a row
+   * (speculative target -d / sim_dt, Baumgarte for d < 0). 0 = off. */
+  int32_t joint_limits;
+  float joint_limit_margin; /* rad */
 } lrl_env_params;
 
 /* ------------------------------------------------------------------------------------------

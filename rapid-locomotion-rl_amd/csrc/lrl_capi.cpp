@@ -97,6 +97,12 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
     }
   k->base_mass = m->base_mass;
   for (int c = 0; c < 6; ++c) k->base_inertia[c] = m->base_inertia[c];
+  if (p->joint_limits && !(p->joint_limit_margin >= 0.f)) return fail(LRL_E_INVALID, "joint_limit_margin");
+  for (int j = 0; j < LRL_NUM_DOF; ++j) {
+    const bool lim = m->dof_lower[j] < m->dof_upper[j];  // (a URDF joint without <limit> has lower = upper = 0)
+    k->dof_lo[j] = lim ? m->dof_lower[j] : -1e30f;
+    k->dof_hi[j] = lim ? m->dof_upper[j] : 1e30f;
+  }
   k->num_bodies = m->num_bodies;
   k->num_spheres = m->num_spheres;
   // spheres must be grouped: base first, then legs in order, bodies contiguous
@@ -226,7 +232,9 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   // obs tiles
   const int wg_envs = LRL_ENV_LANES / 4;
   int lds_contacts = (4 * 51 + model->num_spheres * 67) * wg_envs * 4;  // LEGF, NSF of lrl_env.hip
-  if (params->terrain_mesh) lds_contacts += 16 * LRL_ENV_LANES * 16;  // terrain query vertex block, float4 [16][lanes]
+  // terrain query vertex block, float4 [16][lanes]; the joint-limit rows (12 x 19 fields per env) alias it after the
+  // queries, and have their own region on the plane
+  lds_contacts += params->terrain_mesh ? 16 * LRL_ENV_LANES * 16 : LRL_NUM_DOF * 19 * wg_envs * 4;
   lds_contacts += (4 * (int)(sizeof(KLeg) / 4) + 5 * model->num_spheres) * 4;  // staged model tables (Lds::ktab)
   int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * wg_envs * 4;  // obs / priv tiles + reward rows
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;

@@ -34,6 +34,7 @@
 #define QL 4
 #define ENVS (BLOCK / QL)
 #define NSF 67  // LDS fields per contact sphere (map above contact_setup)
+#define LIMF 19  // LDS fields per joint-limit row (map above limit_setup)
 
 namespace lrl {
 
@@ -182,6 +183,7 @@ struct Lds {
   float* ktab;     // the model tables a lane reads at a lane-dependent index, staged once per launch:
                    // K->leg[4], then per sphere (x, y, z, radius), then per sphere its link (int)
   int nsph;
+  int lim_off;     // field offset of the joint-limit rows (LIM_* map below contact_pgs_q)
   __device__ __forceinline__ const KLeg& kleg(int l) const { return reinterpret_cast<const KLeg*>(ktab)[l]; }
   __device__ __forceinline__ float4 sph4(int s) const {
     return reinterpret_cast<const float4*>(ktab + 4 * KLEGF)[s];
@@ -200,6 +202,7 @@ struct Lds {
   // immediate instead of one address computation per field)
   __device__ __forceinline__ float* sp(int s) const { return base + (sph_off + s * NSF) * ENVS + es; }
   __device__ __forceinline__ float* lp(int l) const { return base + l * LEGF * ENVS + es; }
+  __device__ __forceinline__ float* lm(int r) const { return base + (lim_off + r * LIMF) * ENVS + es; }
   __device__ __forceinline__ float Kx(int l, int j, int r) const { return leg(l, 18 + 6 * j + r); }
   __device__ __forceinline__ float Di(int l, int k) const { return leg(l, 36 + k); }
 };
@@ -586,6 +589,9 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
 struct Body {  // per-lane env state during the step: the base in every lane of the quad, the joints of the lane's leg
   float pos[3], quat[4], V[3], W[3];
   float q[3], qd[3];  // joints 3 ql .. 3 ql + 2 (the whole 12 are gathered over the quad for the post-physics)
+  float lo[3], hi[3];  // their position limits (KParams::dof_lo / dof_hi)
+  float llam[3];       // their limit-row impulses after the last sub-step (warm start; on the terrain mesh the
+                       // rows' LDS is the next sub-step's query scratch)
 };
 
 
@@ -681,6 +687,105 @@ __device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, flo
   const float d1 = dn * z1[0] + dt1 * z1[1] + dt2 * z1[2];
   vo1 = q < 2 ? vo1 + d1 : 0.f;
   if (hj) lg[48 * ENVS] = y48 + (dn * ev[0] + dt1 * ev[1] + dt2 * ev[2]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Joint position limits (the URDF limits PhysX articulations enforce; own formulation): joint j of
+// leg L near its nearer limit gets a unilateral joint-space row with the generalised force sigma e_j (sigma = +1
+// at the lower limit, -1 at the upper), so its separation rate is u = sigma qd_j = g . v_b + sigma (q0_L + Y_L)_j
+// with g = -sigma K_L[j] (no base part: the limit pushes joint against joint), z = S^-1 g, e = sigma D_L^-1[:, j],
+// W = g . z + (D_L^-1)_jj.  Rows live after the contact spheres in the solver's index space (bit nsph + 3 L + j),
+// are owned by leg L's lane and are visited after the spheres, in joint order.  Row field map (LIMF floats,
+// LDS [field][env slot], after the contact rows; on the terrain mesh they alias the query's vertex blocks, which
+// are dead by the time the rows are written):
+//   0..5 g   6..11 z   12..14 e   15 1/W   16 velocity target   17 impulse   18 sigma
+// ------------------------------------------------------------------------------------------------
+#define LIM_G 0
+#define LIM_Z 6
+#define LIM_E 12
+#define LIM_IW 15
+#define LIM_B 16
+#define LIM_LAM 17
+#define LIM_SG 18
+
+// rows of joint r = 3 L + j (lane L): every LDS read up front, every store at the end
+__device__ __forceinline__ void limit_setup(const Lds& M, const float* Si, int r, int L) {
+  float* const row = M.lm(r);
+  const int j = r - 3 * L;
+  const float sg = row[LIM_SG * ENVS];
+  float kx[3][6], di[6];
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) kx[jj][c] = M.Kx(L, jj, c);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) di[k] = M.Di(L, k);
+  float g[6], z[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) g[c] = -sg * (j == 0 ? kx[0][c] : j == 1 ? kx[1][c] : kx[2][c]);
+  sym6mul(Si, g, z);
+  // column j of D^-1 (packed 00 11 22 01 02 12)
+  const float c0 = j == 0 ? di[0] : j == 1 ? di[3] : di[4];
+  const float c1 = j == 0 ? di[3] : j == 1 ? di[1] : di[5];
+  const float c2 = j == 0 ? di[4] : j == 1 ? di[5] : di[2];
+  float w = 0.f;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) w += g[c] * z[c];
+  w += j == 0 ? di[0] : j == 1 ? di[1] : di[2];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    row[(LIM_G + c) * ENVS] = g[c];
+    row[(LIM_Z + c) * ENVS] = z[c];
+  }
+  row[LIM_E * ENVS] = sg * c0;
+  row[(LIM_E + 1) * ENVS] = sg * c1;
+  row[(LIM_E + 2) * ENVS] = sg * c2;
+  row[LIM_IW * ENVS] = 1.f / w;
+}
+
+// warm start of a limit row in its owner lane with the carried impulse lam: v_b += lam z (summed over the quad by
+// the caller), Y_L += lam e
+__device__ __forceinline__ void limit_apply(const Lds& M, int r, int L, float lam, float* dvb) {
+  float* const row = M.lm(r);
+  float z[6], ev[3], y[3];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) z[c] = row[(LIM_Z + c) * ENVS];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) ev[k] = row[(LIM_E + k) * ENVS];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) y[k] = M.leg(L, 48 + k);
+  row[LIM_LAM * ENVS] = lam;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) dvb[c] += lam * z[c];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) M.leg(L, 48 + k) = y[k] + lam * ev[k];
+}
+
+// Gauss-Seidel update of limit row r (leg L, joint j) with the base velocity spread over the quad as in
+// contact_pgs_q: lane q owns v_b[q], v_b[q + 4] (q < 2) and component q of Y_L; lane j adds sigma (q0 + Y)_j
+__device__ __forceinline__ void limit_pgs_q(const Lds& M, int r, int q, float& vo0, float& vo1) {
+  const int L = (r * 11) >> 5;  // r / 3 for r < 12
+  const int j = r - 3 * L;
+  const bool hj = q < 3;
+  const int qh = hj ? q : 2;
+  float* const row = M.lm(r);
+  const float* const rq = row + q * ENVS;
+  float* const lg = M.lp(L) + qh * ENVS;
+  // (lanes 2, 3 read g / z entries 6, 7 of the next field group for the v_b[q + 4] terms and zero them with vo1 = 0)
+  const float g0 = rq[LIM_G * ENVS], g1 = rq[(LIM_G + 4) * ENVS];
+  const float z0 = rq[LIM_Z * ENVS], z1 = rq[(LIM_Z + 4) * ENVS];
+  const float ev = row[(LIM_E + qh) * ENVS];
+  const float y45 = lg[45 * ENVS], y48 = lg[48 * ENVS];
+  const float iw = row[LIM_IW * ENVS], b = row[LIM_B * ENVS], l0 = row[LIM_LAM * ENVS], sg = row[LIM_SG * ENVS];
+  float a = g0 * vo0 + g1 * vo1;
+  a += q == j ? sg * (y45 + y48) : 0.f;
+  const float u = quad_sum(a);
+  const float ln = fmaxf(l0 - (u - b) * iw, 0.f);
+  const float dn = ln - l0;
+  row[LIM_LAM * ENVS] = ln;
+  vo0 += dn * z0;
+  vo1 = q < 2 ? vo1 + dn * z1 : 0.f;
+  if (hj) lg[48 * ENVS] = y48 + dn * ev;
 }
 
 // lane of the quad that owns sphere s: its leg, or round-robin for the base spheres
@@ -924,6 +1029,21 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     prof[14] += clock64() - tq0;  // terrain queries (part of kin+dyn+detect)
 #endif
   }
+  // joint limits of this lane's leg (after the terrain queries: on the mesh the rows alias their vertex blocks)
+  if (P.joint_limits) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float sh = st.hi[j] - st.q[j], sl = st.q[j] - st.lo[j];
+      const bool up = sh < sl;
+      const float sep = up ? sh : sl;
+      if (sep < P.joint_limit_margin + 2.f * dt * fabsf(st.qd[j])) {
+        active |= 1ull << (M.nsph + 3 * ql + j);
+        float* const row = M.lm(3 * ql + j);
+        row[LIM_SG * ENVS] = up ? -1.f : 1.f;
+        row[LIM_B * ENVS] = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+      }
+    }
+  }
   // ---- quad reductions: legs -> base ----
 #pragma unroll
   for (int k = 0; k < 21; ++k) Sch[k] = quad_sum(Sch[k]);
@@ -998,7 +1118,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     if (m) {
       const int s = __builtin_ctzll(m);
       m &= m - 1ull;
-      contact_setup<TERR>(M, Sch, R, s, sph_leg_of(SL, s), M.slink(s));
+      if (s >= M.nsph)
+        limit_setup(M, Sch, s - M.nsph, ql);
+      else
+        contact_setup<TERR>(M, Sch, R, s, sph_leg_of(SL, s), M.slink(s));
     }
   }
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
@@ -1007,15 +1130,24 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     float dvb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (uint64_t m = active & own & ~prev_active; m; m &= m - 1ull) {
       const int s = __builtin_ctzll(m);
-      M.sph(s, 10) = 0.f;
-      M.sph(s, 11) = 0.f;
-      M.sph(s, 12) = 0.f;
+      if (s >= M.nsph) {
+        M.lm(s - M.nsph)[LIM_LAM * ENVS] = 0.f;
+      } else {
+        M.sph(s, 10) = 0.f;
+        M.sph(s, 11) = 0.f;
+        M.sph(s, 12) = 0.f;
+      }
     }
     for (uint64_t m = active & own & prev_active; __any((int)(m != 0ull));) {
       if (m) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        apply_impulse(M, s, sph_leg_of(SL, s), M.sph(s, 10), M.sph(s, 11), M.sph(s, 12), dvb);
+        if (s >= M.nsph) {
+          const int j = s - M.nsph - 3 * ql;
+          limit_apply(M, s - M.nsph, ql, j == 0 ? st.llam[0] : j == 1 ? st.llam[1] : st.llam[2], dvb);
+        } else {
+          apply_impulse(M, s, sph_leg_of(SL, s), M.sph(s, 10), M.sph(s, 11), M.sph(s, 12), dvb);
+        }
       }
     }
 #pragma unroll
@@ -1036,7 +1168,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         if (m) {
           const int s = __builtin_ctzll(m);
           m &= m - 1ull;
-          contact_pgs_q(M, s, sph_leg_of(SL, s), mu, ql, vo0, vo1);
+          if (s >= M.nsph)
+            limit_pgs_q(M, s - M.nsph, ql, vo0, vo1);
+          else
+            contact_pgs_q(M, s, sph_leg_of(SL, s), mu, ql, vo0, vo1);
         }
       }
 #pragma unroll
@@ -1045,6 +1180,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     vbc[5] = quad_bcast(vo1, 1);
   }
   __syncthreads();  // the leg accumulators each lane owned are read by the whole quad below
+  if (P.joint_limits) {  // this leg's limit impulses, carried to the next sub-step in registers
+#pragma unroll
+    for (int j = 0; j < 3; ++j) st.llam[j] = M.lm(3 * ql + j)[LIM_LAM * ENVS];
+  }
   LRL_PROF(3)  // PGS iterations
   // materialise the lazily propagated joint rates of this lane's leg
 #pragma unroll
@@ -1224,6 +1363,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   for (int j = 0; j < 3; ++j) {
     st.q[j] = S.dof_pos[(3 * ql + j) * N + e];
     st.qd[j] = S.dof_vel[(3 * ql + j) * N + e];
+    st.lo[j] = K->dof_lo[3 * ql + j];
+    st.hi[j] = K->dof_hi[3 * ql + j];
+    st.llam[j] = 0.f;
   }
   float act[12], tau[12];
   {
@@ -1236,7 +1378,10 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   }
   // leg blocks first, then the contact rows, (terrain: the query's vertex block), then the model tables
   const int nsph = K->num_spheres;
-  const Lds M{lds, 4 * LEGF, es, lds + (4 * LEGF + nsph * NSF) * ENVS + (TERR ? 64 * BLOCK : 0), nsph};
+  static_assert(LRL_NUM_DOF * LIMF * ENVS <= 64 * BLOCK, "joint-limit rows must fit the terrain vertex blocks");
+  const Lds M{lds, 4 * LEGF, es,
+              lds + (4 * LEGF + nsph * NSF) * ENVS + (TERR ? 64 * BLOCK : LRL_NUM_DOF * LIMF * ENVS), nsph,
+              4 * LEGF + nsph * NSF};
   {
     const float* src = reinterpret_cast<const float*>(K->leg);
     for (int i = lane; i < 4 * KLEGF; i += BLOCK) M.ktab[i] = src[i];
@@ -1264,6 +1409,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
   for (int s = 0; s < K->num_spheres; ++s)
     if (sph_owner(K, s) == ql) own |= 1ull << s;
+  own |= 7ull << (nsph + 3 * ql);  // this leg's joint-limit rows
   unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   LRL_PROF_DECL
 #ifdef LRL_ENV_PROFILE

@@ -26,6 +26,8 @@ struct KParams {
   lrl_env_params p;
   KLeg leg[LRL_NUM_LEGS];
   float base_mass, base_inertia[6];
+  // joint position limits in dof order (3 l + j), +-1e30 for a joint without limits (lrl_model::dof_lower / upper)
+  float dof_lo[LRL_NUM_DOF], dof_hi[LRL_NUM_DOF];
   int32_t num_bodies, num_spheres;
   // spheres sorted by body (model order: base, then leg 0..3)
   float sph_pos[LRL_MAX_SPHERES][3];
