@@ -60,6 +60,8 @@ extern "C" {
 #define LRL_MAX_HEIGHT_POINTS 192
 #define LRL_MAX_REWARD_TERMS 24
 #define LRL_NUM_PRIV 18
+#define LRL_SELF_SLOTS 8        /* self-contact rows per env and sub-step (solver slots) */
+#define LRL_MAX_SELF_PAIRS 256  /* candidate self-collision sphere pairs of a model */
 
 /* ------------------------------------------------------------------------------------------
  * Robot model: a floating base with 4 legs x 3 revolute joints (hip, thigh, calf) and an optional
@@ -176,6 +178,12 @@ typedef struct lrl_env_params {
    * (speculative target -d / sim_dt, Baumgarte for d < 0). 0 = off. */
   int32_t joint_limits;
   float joint_limit_margin; /* rad */
+  /* self-collision (Cfg.asset.self_collisions == 0, the collision filter legged_robot.py:1246-1247 passes to create_actor: Isaac Gym
+   * enables PhysX self-collision for 0): collision spheres of different, non-adjacent links of the articulation
+   * (own model, DESIGN.md §4: sphere-sphere between legs and inside a leg, leg sphere against the base box the
+   * base-corner spheres span), up to LRL_SELF_SLOTS contacts per env and sub-step in the canonical pair order,
+   * friction / restitution of the robot's own material.  0 = off. */
+  int32_t self_collisions;
 } lrl_env_params;
 
 /* ------------------------------------------------------------------------------------------

@@ -159,6 +159,18 @@ def physics_substep(model, params, root, q, qd, tau, friction, restitution, payl
     return ro, qo, qdo, co, n
 
 
+def self_pairs(model, q=None):
+    """lrl_oracle.c:lrlo_self_pairs: the self-collision candidate pairs [n, 2] (b = -1: the base box) in the canonical
+    order and, for joint angles q [12] (default 0), their separations [n]."""
+    L = lib()
+    pairs = np.zeros((256, 2), np.int32)
+    sep = np.zeros(256, np.float64)
+    qa = None if q is None else np.ascontiguousarray(q, np.float32)
+    n = L.lrlo_self_pairs(C.byref(model), None if qa is None else qa.ctypes.data_as(C.c_void_p),
+                          pairs.ctypes.data_as(C.c_void_p), sep.ctypes.data_as(C.c_void_p))
+    return pairs[:n].copy(), sep[:n].copy()
+
+
 def energy(model, params, root, q, qd, payload=0.0, com=(0, 0, 0)):
     f = lambda a, n: np.ascontiguousarray(a, np.float32).reshape(n)
     p = lambda a: a.ctypes.data_as(C.c_void_p)

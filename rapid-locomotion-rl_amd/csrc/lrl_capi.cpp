@@ -1,7 +1,9 @@
 // lrl_capi.cpp — the extern "C" boundary of liblrl.so (include/lrl.h): sim object lifetime, the
 // SoA HBM arena, tensor descriptors (acquire_*_tensor) and the launch entry points.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -65,6 +67,60 @@ static void quat_to_rowmajor(const float* q, float* R) {
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
   R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
   R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+// Self-collision candidates (the oracle enumerates the same list, oracle/lrl_oracle.c::self_pairs).
+// PhysX collides every pair of shapes on different links of an articulation except a link and its parent; with the
+// fixed feet merged into the calves, a leg sphere's dynamic link is min(body_link, 2).  Candidates: leg spheres with a
+// radius (the base's radius-0 corner spheres span the base box instead), in the canonical order lane La major, then
+// g = 0: inside leg La, links two apart (hip - calf); g = 1..3: against leg La + g; g = 4: a leg sphere below the hip
+// (whose parent is the base) against the base box.  Inside a group: sphere a, then sphere b, in model order.
+static int self_pairs(const lrl_model* m, KParams* k) {
+  auto leg_of = [&](int s) { return m->body_leg[m->sphere_body[s]]; };
+  auto link_of = [&](int s) { int l = m->body_link[m->sphere_body[s]]; return l > 2 ? 2 : l; };
+  auto on_leg = [&](int s, int L) { return leg_of(s) == L && m->sphere_radius[s] > 0.f; };
+  float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+  int nbase = 0;
+  for (int s = 0; s < m->num_spheres; ++s)
+    if (leg_of(s) < 0) {
+      ++nbase;
+      for (int c = 0; c < 3; ++c) {
+        lo[c] = fminf(lo[c], m->sphere_pos[s][c] - m->sphere_radius[s]);
+        hi[c] = fmaxf(hi[c], m->sphere_pos[s][c] + m->sphere_radius[s]);
+      }
+    }
+  for (int c = 0; c < 3; ++c) {
+    k->box_c[c] = nbase ? 0.5f * (lo[c] + hi[c]) : 0.f;
+    k->box_h[c] = nbase ? 0.5f * (hi[c] - lo[c]) : -1.f;  // no base shapes: no box group
+  }
+  int n = 0;
+  auto add = [&](int a, int b) {
+    if (n >= LRL_MAX_SELF_PAIRS) return false;
+    const int bb = b < 0 ? 0 : m->sphere_body[b];
+    k->self_pair[n++] = (uint32_t)a | (uint32_t)(b < 0 ? 255 : b) << 8 | (uint32_t)m->sphere_body[a] << 16 | (uint32_t)bb << 24;
+    return true;
+  };
+  for (int La = 0; La < 4; ++La)
+    for (int g = 0; g < 5; ++g) {
+      k->self_grp[La][g][0] = n;
+      const int Lb = g == 0 ? La : La + g;
+      for (int a = 0; a < m->num_spheres; ++a) {
+        if (!on_leg(a, La)) continue;
+        if (g == 4) {
+          if (nbase && link_of(a) >= 1 && !add(a, -1)) return fail(LRL_E_INVALID, "too many self-collision pairs");
+          continue;
+        }
+        if (Lb > 3) continue;
+        for (int b = g == 0 ? a + 1 : 0; b < m->num_spheres; ++b) {
+          if (!on_leg(b, Lb)) continue;
+          if (g == 0 && abs(link_of(a) - link_of(b)) < 2) continue;
+          if (!add(a, b)) return fail(LRL_E_INVALID, "too many self-collision pairs");
+        }
+      }
+      k->self_grp[La][g][1] = n;
+    }
+  k->self_npairs = n;
+  return 0;
 }
 
 static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
@@ -141,6 +197,8 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
     if (b < 0 || b >= m->num_bodies) return fail(LRL_E_INVALID, "foot index");
     k->body_foot[b] = f;
   }
+  int rc = self_pairs(m, k);
+  if (rc) return rc;
   k->num_history = p->num_history;
   k->n_es = p->num_sum_keys + 1;
   k->n_cs = p->num_sum_keys + 5;
@@ -202,6 +260,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   addf(&S.joint_pos_target, 12ull * N);
   const int NP = params->measure_heights ? params->num_height_points : 0;
   addf(&S.heights, (size_t)(NP > 0 ? NP : 1) * N);
+  addf(&S.selfrow, (size_t)LRL_SELF_SLOTS * 104 * N);  // SSF of lrl_env.hip
   size_t total = 0;
   for (auto& f : fields) total += (f.bytes + 255) / 256 * 256;
   void* arena = nullptr;
@@ -236,6 +295,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   // queries, and have their own region on the plane
   lds_contacts += params->terrain_mesh ? 16 * LRL_ENV_LANES * 16 : LRL_NUM_DOF * 19 * wg_envs * 4;
   lds_contacts += (4 * (int)(sizeof(KLeg) / 4) + 5 * model->num_spheres) * 4;  // staged model tables (Lds::ktab)
+  lds_contacts += (40 + s->hk.self_npairs) * 4;  // + the self-collision groups and pairs
   int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * wg_envs * 4;  // obs / priv tiles + reward rows
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
   if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);

@@ -35,6 +35,7 @@
 #define ENVS (BLOCK / QL)
 #define NSF 67  // LDS fields per contact sphere (map above contact_setup)
 #define LIMF 19  // LDS fields per joint-limit row (map above limit_setup)
+#define SSF 104  // HBM fields per self-contact row (map above self_setup; lrl_capi.cpp sizes KState::selfrow with it)
 
 namespace lrl {
 
@@ -190,6 +191,11 @@ struct Lds {
   }
   __device__ __forceinline__ int slink(int s) const {
     return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 4 * nsph)[s];
+  }
+  // self-collision groups [lane][g][begin, end) (KParams::self_grp) and pairs (KParams::self_pair), after the links
+  __device__ __forceinline__ const int* sgrp() const { return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 5 * nsph); }
+  __device__ __forceinline__ uint32_t spair(int p) const {
+    return reinterpret_cast<const uint32_t*>(ktab + 4 * KLEGF + 5 * nsph + 40)[p];
   }
   // field f of a row = row pointer + f * ENVS (a constant f folds into the ds_read / ds_write immediate offset)
   __device__ __forceinline__ float& leg(int l, int f) const { return lp(l)[f * ENVS]; }
@@ -814,10 +820,350 @@ __device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
   return l;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Self-collision (PhysX collides the links of an articulation with each other when Cfg.asset.self_collisions is
+// 0, except a link and its parent; own formulation).  Candidate pairs (KParams::self_pair, canonical
+// order: lane / leg La major, then its groups) are sphere-sphere between the legs and inside a leg, and leg sphere
+// against the base box.  The contact normal n points from body B to body A (an impulse lambda n pushes A, -lambda n
+// pushes B) and both bodies share the contact point x, so the base motion cancels from the relative velocity:
+//   u_d = hA_d . qd_A + hB_d . qd_B,  hA_d = C_A^T n_d,  hB_d = -C_B^T n_d  (C = joint directions at x)
+//       = g_d . v_b + hA_d . (q0_A + Y_A) + hB_d . (q0_B + Y_B)  with  g_d = -K_A^T hA_d - K_B^T hB_d,
+// an impulse moves v_b by lambda S^-1 g_d and Y_A / Y_B by lambda D^-1 hA_d / D^-1 hB_d (a same-leg pair folds hB
+// into hA; the base box has no hB).  The first LRL_SELF_SLOTS active pairs of an env in the canonical order get
+// the solver rows after the joint limits (bits nsph + 12 + slot), built cold every sub-step (no warm start: a
+// pair's slot can change between sub-steps).  Rows live in HBM (KState::selfrow, [slot][SSF][N]; the LDS is
+// spent on the contact rows): only envs in self-contact touch them.  Field map:
+//   0..2 n (base frame)  3..5 x (base frame)  6 leg A  7 leg B (-1: base box)  8 link A  9 link B  10 velocity target
+//   11..13 impulse (n, t1, t2)  14 1/W_nn  15 W_t1n  16 W_t2n  17..19 (W_tt)^-1 (11, 12, 22)  20..37 g_d
+//   38..46 hA_d  47..55 hB_d  56..73 z_d = S^-1 g_d  74..82 D_A^-1 hA_d  83..91 D_B^-1 hB_d
+//   92..100 (n, t1, t2) in the world frame (contact forces)  101 body A  102 body B
+// ------------------------------------------------------------------------------------------------
+#define SR_N 0
+#define SR_X 3
+#define SR_LA 6
+#define SR_LB 7
+#define SR_KA 8
+#define SR_KB 9
+#define SR_B 10
+#define SR_LAM 11
+#define SR_IW 14
+#define SR_G 20
+#define SR_HA 38
+#define SR_HB 47
+#define SR_Z 56
+#define SR_EA 74
+#define SR_EB 83
+#define SR_F 92
+#define SR_BA 101
+#define SR_BB 102
+
+// separation of a sphere (centre ca, radius ra) against a sphere (cb, rb) or, box, the base box: n from B to A, x = the
+// contact point (contraction off: the register gate and the LDS pass evaluate it bitwise alike)
+__device__ __forceinline__ float self_geom_c(const KParams* __restrict__ K, V3 ca, float ra, V3 cb, float rb, bool box,
+                                             V3& n, V3& x) {
+#pragma clang fp contract(off)
+  if (!box) {
+    const V3 d = ca - cb;
+    const float dd = dot(d, d), dist = sqrtf(dd);
+    n = dd > 1e-18f ? (1.f / dist) * d : v3(0.f, 0.f, 1.f);
+    x = 0.5f * ((ca - ra * n) + (cb + rb * n));
+    return dist - ra - rb;
+  }
+  const V3 bc = v3(K->box_c[0], K->box_c[1], K->box_c[2]), bh = v3(K->box_h[0], K->box_h[1], K->box_h[2]);
+  const V3 c = ca - bc;
+  const V3 q = v3(fminf(fmaxf(c.x, -bh.x), bh.x), fminf(fmaxf(c.y, -bh.y), bh.y), fminf(fmaxf(c.z, -bh.z), bh.z));
+  const V3 d = c - q;
+  const float dd = dot(d, d);
+  if (dd > 0.f) {  // centre outside the box: nearest surface point
+    const float dist = sqrtf(dd);
+    n = (1.f / dist) * d;
+    x = q + bc;
+    return dist - ra;
+  }
+  // centre inside: the nearest face (first of x, y, z on ties)
+  const float dx = bh.x - fabsf(c.x), dy = bh.y - fabsf(c.y), dz = bh.z - fabsf(c.z);
+  const int k = (dx <= dy && dx <= dz) ? 0 : (dy <= dz ? 1 : 2);
+  const float sx = c.x < 0.f ? -1.f : 1.f, sy = c.y < 0.f ? -1.f : 1.f, sz = c.z < 0.f ? -1.f : 1.f;
+  n = k == 0 ? v3(sx, 0.f, 0.f) : k == 1 ? v3(0.f, sy, 0.f) : v3(0.f, 0.f, sz);
+  x = v3(k == 0 ? sx * bh.x : c.x, k == 1 ? sy * bh.y : c.y, k == 2 ? sz * bh.z : c.z) + bc;
+  return -(k == 0 ? dx : k == 1 ? dy : dz) - ra;
+}
+// the same for candidate pair pk, centres from the contact rows' fields 0..2 (the leg pass writes every centre there)
+__device__ __forceinline__ float self_geom(const KParams* __restrict__ K, const Lds& M, uint32_t pk, V3& n, V3& x) {
+  const int a = pk & 255u, b = (pk >> 8) & 255u;
+  const V3 ca = v3(M.sph(a, 0), M.sph(a, 1), M.sph(a, 2));
+  const bool box = b == 255;
+  const int bb = box ? a : b;
+  const V3 cb = v3(M.sph(bb, 0), M.sph(bb, 1), M.sph(bb, 2));
+  return self_geom_c(K, ca, M.sph4(a).w, cb, M.sph4(bb).w, box, n, x);
+}
+
+__device__ __forceinline__ bool aabb_overlap(V3 alo, V3 ahi, V3 blo, V3 bhi) {
+  return alo.x <= bhi.x && blo.x <= ahi.x && alo.y <= bhi.y && blo.y <= ahi.y && alo.z <= bhi.z && blo.z <= ahi.z;
+}
+
+__device__ __forceinline__ int quad_bcast_i(int v, int l) { return __float_as_int(quad_bcast(__int_as_float(v), l)); }
+
+// Per-lane gate (no barrier; it runs every sub-step, so it is kept to a few instructions per sphere — the kernel
+// issues about one VALU instruction per 6 cycles): this leg's same-leg and box candidates within the offset and its
+// bounding box for the leg-leg groups, from its own sphere centres in LDS (written by this lane in the leg pass), every
+// read up front over a clamped index (a leg has at most 8 spheres, lrl_capi.cpp).  Squared distances against the
+// offset widened by 1e-5 m: conservative, the LDS pass decides every pair the gate lets through exactly.
+struct SelfGate {
+  V3 lo, hi;     // this leg's sphere surfaces grown by contact_offset / 2
+  int hits, nh;  // same-leg + box candidates; link-0 spheres with a radius (> 2: the LDS pass decides)
+};
+__device__ __forceinline__ SelfGate self_gate(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, int ql,
+                                              float co) {
+  const int b = ql == 0 ? SL.b[0] : ql == 1 ? SL.b[1] : ql == 2 ? SL.b[2] : SL.b[3];
+  const int e = ql == 0 ? SL.e[0] : ql == 1 ? SL.e[1] : ql == 2 ? SL.e[2] : SL.e[3];
+  float cx[8], cy[8], cz[8], r[8];
+  int lk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int s = min(b + k, e - 1);
+    cx[k] = M.sph(s, 0);
+    cy[k] = M.sph(s, 1);
+    cz[k] = M.sph(s, 2);
+    r[k] = M.sph4(s).w;
+    lk[k] = M.slink(s);
+  }
+  const float cw = co + 1e-5f;
+  const float bcx = K->box_c[0], bcy = K->box_c[1], bcz = K->box_c[2];
+  const float bhx = K->box_h[0], bhy = K->box_h[1], bhz = K->box_h[2];
+  SelfGate G;
+  G.lo = v3(1e30f, 1e30f, 1e30f);
+  G.hi = v3(-1e30f, -1e30f, -1e30f);
+  G.hits = 0;
+  G.nh = 0;
+  float h0x = 0.f, h0y = 0.f, h0z = 0.f, h0r = -1e30f;  // the leg's first link-0 sphere
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool use = b + k < e && r[k] > 0.f;
+    const float rg = r[k] + 0.5f * co;
+    if (use) {
+      G.lo = v3(fminf(G.lo.x, cx[k] - rg), fminf(G.lo.y, cy[k] - rg), fminf(G.lo.z, cz[k] - rg));
+      G.hi = v3(fmaxf(G.hi.x, cx[k] + rg), fmaxf(G.hi.y, cy[k] + rg), fmaxf(G.hi.z, cz[k] + rg));
+    }
+    // base box: squared distance of the centre from the box (0 inside) against (r + offset)^2
+    const float px = fabsf(cx[k] - bcx) - bhx, py = fabsf(cy[k] - bcy) - bhy, pz = fabsf(cz[k] - bcz) - bhz;
+    const float qx = fmaxf(px, 0.f), qy = fmaxf(py, 0.f), qz = fmaxf(pz, 0.f);
+    const float rb = r[k] + cw;
+    const bool hb = qx * qx + qy * qy + qz * qz < rb * rb;
+    // the leg's hip sphere
+    const float ax = cx[k] - h0x, ay = cy[k] - h0y, az = cz[k] - h0z, rh = h0r + rb;
+    const bool hh = rh > 0.f && ax * ax + ay * ay + az * az < rh * rh;
+    G.hits += (use && ((lk[k] >= 1 && bhx >= 0.f && hb) || (lk[k] == 2 && hh))) ? 1 : 0;
+    if (use && lk[k] == 0) {
+      if (G.nh == 0) { h0x = cx[k]; h0y = cy[k]; h0z = cz[k]; h0r = r[k]; }
+      G.nh += 1;  // (a second link-0 sphere sends the leg to the LDS pass)
+    }
+  }
+  return G;
+}
+
+// Rows of the quad's self-contacts, entered only by waves the gate flags (a hit, a leg-leg bounding-box overlap, or a
+// leg with more than two link-0 spheres): the canonical count over this lane's live groups from the LDS centres, the
+// quad prefix of the counts, then the first LRL_SELF_SLOTS hits get rows — geometry, legs / links / bodies and the
+// velocity target (restitution from the sub-step-start joint rates, LDS leg fields 45..47).
+__device__ __attribute__((noinline)) void self_detect(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, float* __restrict__ srow,
+                            int N, int ql, unsigned live, float dt, float rest, uint64_t& active, uint64_t& sown) {
+  const lrl_env_params& P = K->p;
+  const float co = P.contact_offset;
+  const int* G = M.sgrp() + 10 * ql;
+  int cnt = 0;
+#pragma unroll
+  for (int g = 0; g < 5; ++g)
+    if ((live >> g) & 1u)
+      for (int p = G[2 * g]; p < G[2 * g + 1]; ++p) {
+        V3 n, x;
+        cnt += self_geom(K, M, M.spair(p), n, x) < co ? 1 : 0;
+      }
+  const int c0 = quad_bcast_i(cnt, 0), c1 = quad_bcast_i(cnt, 1), c2 = quad_bcast_i(cnt, 2);
+  int slot = ql == 0 ? 0 : ql == 1 ? c0 : ql == 2 ? c0 + c1 : c0 + c1 + c2;
+  const int end = min(slot + cnt, LRL_SELF_SLOTS);
+  if (slot >= end) return;
+#pragma unroll
+  for (int g = 0; g < 5; ++g)
+    if ((live >> g) & 1u)
+      for (int p = G[2 * g]; p < G[2 * g + 1] && slot < end; ++p) {
+        const uint32_t pk = M.spair(p);
+        V3 n, x;
+        const float sep = self_geom(K, M, pk, n, x);
+        if (!(sep < co)) continue;
+        const int a = pk & 255u, b = (pk >> 8) & 255u;
+        const int la = ql, lb = b == 255 ? -1 : sph_leg_of(SL, b);
+        const int ka = M.slink(a), kb = b == 255 ? 0 : M.slink(b);
+        // relative normal velocity at the sub-step start: sum_j (a_j x (x - o_j)) . n qd_j over A's carrying joints,
+        // minus the same over B's
+        float u0 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j <= ka) u0 += dot(cross(M.a(la, j), x - M.o(la, j)), n) * M.leg(la, 45 + j);
+          if (lb >= 0 && j <= kb) u0 -= dot(cross(M.a(lb, j), x - M.o(lb, j)), n) * M.leg(lb, 45 + j);
+        }
+        float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+        if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
+        float* const row = srow + (size_t)slot * SSF * N;
+        row[(SR_N + 0) * N] = n.x; row[(SR_N + 1) * N] = n.y; row[(SR_N + 2) * N] = n.z;
+        row[(SR_X + 0) * N] = x.x; row[(SR_X + 1) * N] = x.y; row[(SR_X + 2) * N] = x.z;
+        row[SR_LA * N] = (float)la;
+        row[SR_LB * N] = (float)lb;
+        row[SR_KA * N] = (float)ka;
+        row[SR_KB * N] = (float)kb;
+        row[SR_B * N] = tgt;
+        row[SR_BA * N] = (float)((pk >> 16) & 255u);
+        row[SR_BB * N] = (float)(pk >> 24);
+        const uint64_t bit = 1ull << (M.nsph + LRL_NUM_DOF + slot);
+        active |= bit;
+        sown |= bit;
+        ++slot;
+      }
+}
+
+// solver rows of self-contact slot k in its owner lane (every global / LDS read up front)
+__device__ __attribute__((noinline)) void self_setup(const Lds& M, const float* Si, const M3& R, float* __restrict__ srow, int N, int k) {
+  float* const row = srow + (size_t)k * SSF * N;
+  const V3 n = v3(row[SR_N * N], row[(SR_N + 1) * N], row[(SR_N + 2) * N]);
+  const V3 x = v3(row[SR_X * N], row[(SR_X + 1) * N], row[(SR_X + 2) * N]);
+  const int la = (int)row[SR_LA * N], lb = (int)row[SR_LB * N], ka = (int)row[SR_KA * N], kb = (int)row[SR_KB * N];
+  const int lbr = lb < 0 ? la : lb;
+  V3 ca[3], cbv[3];
+  float kxa[3][6], kxb[3][6], dia[6], dib[6];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    ca[j] = j <= ka ? cross(M.a(la, j), x - M.o(la, j)) : v3(0.f, 0.f, 0.f);
+    cbv[j] = (lb >= 0 && j <= kb) ? cross(M.a(lbr, j), x - M.o(lbr, j)) : v3(0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      kxa[j][r] = M.Kx(la, j, r);
+      kxb[j][r] = M.Kx(lbr, j, r);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    dia[c] = M.Di(la, c);
+    dib[c] = M.Di(lbr, c);
+  }
+  const bool same = lb == la;
+  V3 fr[3];
+  fr[0] = n;
+  contact_frame(n, fr[1], fr[2]);
+  V3 ha[3], hb[3], ea[3], eb[3];
+  float g[3][6], z[3][6];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    V3 h1 = v3(dot(ca[0], fr[d]), dot(ca[1], fr[d]), dot(ca[2], fr[d]));
+    V3 h2 = v3(-dot(cbv[0], fr[d]), -dot(cbv[1], fr[d]), -dot(cbv[2], fr[d]));
+    if (same) {
+      h1 = h1 + h2;
+      h2 = v3(0.f, 0.f, 0.f);
+    }
+    ha[d] = h1;
+    hb[d] = h2;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+      g[d][r] = -(kxa[0][r] * h1.x + kxa[1][r] * h1.y + kxa[2][r] * h1.z) -
+                (kxb[0][r] * h2.x + kxb[1][r] * h2.y + kxb[2][r] * h2.z);
+    ea[d] = sym3mul(dia[0], dia[1], dia[2], dia[3], dia[4], dia[5], h1);
+    eb[d] = sym3mul(dib[0], dib[1], dib[2], dib[3], dib[4], dib[5], h2);
+    sym6mul(Si, g[d], z[d]);
+  }
+  float W[3][3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e)
+#pragma unroll
+    for (int d = 0; d <= e; ++d) {
+      float w = 0.f;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) w += g[d][r] * z[e][r];
+      w += dot(ha[d], ea[e]) + dot(hb[d], eb[e]);
+      W[d][e] = w;
+      W[e][d] = w;
+    }
+  // a relative Jacobian of zero (contact point on the joint axes) leaves an inert row
+  const float det = W[1][1] * W[2][2] - W[1][2] * W[2][1];
+  const float id = det > 1e-12f ? 1.f / det : 0.f;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      row[(SR_G + 6 * d + r) * N] = g[d][r];
+      row[(SR_Z + 6 * d + r) * N] = z[d][r];
+    }
+    row[(SR_HA + 3 * d) * N] = ha[d].x; row[(SR_HA + 3 * d + 1) * N] = ha[d].y; row[(SR_HA + 3 * d + 2) * N] = ha[d].z;
+    row[(SR_HB + 3 * d) * N] = hb[d].x; row[(SR_HB + 3 * d + 1) * N] = hb[d].y; row[(SR_HB + 3 * d + 2) * N] = hb[d].z;
+    row[(SR_EA + 3 * d) * N] = ea[d].x; row[(SR_EA + 3 * d + 1) * N] = ea[d].y; row[(SR_EA + 3 * d + 2) * N] = ea[d].z;
+    row[(SR_EB + 3 * d) * N] = eb[d].x; row[(SR_EB + 3 * d + 1) * N] = eb[d].y; row[(SR_EB + 3 * d + 2) * N] = eb[d].z;
+    const V3 fw = mul(R, fr[d]);
+    row[(SR_F + 3 * d) * N] = fw.x; row[(SR_F + 3 * d + 1) * N] = fw.y; row[(SR_F + 3 * d + 2) * N] = fw.z;
+    row[(SR_LAM + d) * N] = 0.f;
+  }
+  row[SR_IW * N] = W[0][0] > 1e-12f ? 1.f / W[0][0] : 0.f;
+  row[(SR_IW + 1) * N] = W[1][0];
+  row[(SR_IW + 2) * N] = W[2][0];
+  row[(SR_IW + 3) * N] = W[2][2] * id;
+  row[(SR_IW + 4) * N] = -W[1][2] * id;
+  row[(SR_IW + 5) * N] = W[1][1] * id;
+}
+
+// Gauss-Seidel update of self-contact slot k with the base velocity spread over the quad as in contact_pgs_q: lane q
+// owns v_b[q], v_b[q + 4] (q < 2) and component q of Y_A and Y_B
+__device__ __attribute__((noinline)) void self_pgs_q(const Lds& M, float* __restrict__ srow, int N, int k, float mu, int q,
+                                           float& vo0, float& vo1) {
+  float* const row = srow + (size_t)k * SSF * N;
+  const bool hj = q < 3;
+  const int qh = hj ? q : 2;
+  const int la = (int)row[SR_LA * N], lb = (int)row[SR_LB * N];
+  const int lbr = lb < 0 ? la : lb;
+  float g0[3], g1[3], ha[3], hb[3], z0[3], z1[3], ea[3], eb[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {  // (lanes 2, 3 read g / z entries 6, 7 of the next field group for the v_b[q + 4]
+    g0[d] = row[(SR_G + 6 * d + q) * N];  //  terms; vo1 = 0 there)
+    g1[d] = row[(SR_G + 6 * d + q + 4) * N];
+    z0[d] = row[(SR_Z + 6 * d + q) * N];
+    z1[d] = row[(SR_Z + 6 * d + q + 4) * N];
+    ha[d] = row[(SR_HA + 3 * d + qh) * N];
+    hb[d] = row[(SR_HB + 3 * d + qh) * N];
+    ea[d] = row[(SR_EA + 3 * d + qh) * N];
+    eb[d] = row[(SR_EB + 3 * d + qh) * N];
+  }
+  const float iWnn = row[SR_IW * N], Wt1n = row[(SR_IW + 1) * N], Wt2n = row[(SR_IW + 2) * N];
+  const float i11 = row[(SR_IW + 3) * N], i12 = row[(SR_IW + 4) * N], i22 = row[(SR_IW + 5) * N], b = row[SR_B * N];
+  const float ln0 = row[SR_LAM * N], lt10 = row[(SR_LAM + 1) * N], lt20 = row[(SR_LAM + 2) * N];
+  float* const lga = M.lp(la) + qh * ENVS;
+  float* const lgb = M.lp(lbr) + qh * ENVS;
+  const float ya45 = lga[45 * ENVS], ya48 = lga[48 * ENVS], yb45 = lgb[45 * ENVS], yb48 = lgb[48 * ENVS];
+  float u[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    float a = g0[d] * vo0 + g1[d] * vo1;
+    a += hj ? ha[d] * (ya45 + ya48) + hb[d] * (yb45 + yb48) : 0.f;
+    u[d] = quad_sum(a);
+  }
+  const float ln = fmaxf(ln0 - (u[0] - b) * iWnn, 0.f);
+  const float dn = ln - ln0;
+  const float ut1 = u[1] + Wt1n * dn, ut2 = u[2] + Wt2n * dn;
+  float lt1 = lt10 - (i11 * ut1 + i12 * ut2), lt2 = lt20 - (i12 * ut1 + i22 * ut2);
+  const float lim = mu * ln, nt2 = lt1 * lt1 + lt2 * lt2;
+  const float sc = nt2 > lim * lim ? (nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f) : 1.f;
+  lt1 *= sc;
+  lt2 *= sc;
+  row[SR_LAM * N] = ln;  // (the four lanes store the same values)
+  row[(SR_LAM + 1) * N] = lt1;
+  row[(SR_LAM + 2) * N] = lt2;
+  const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
+  vo0 += dn * z0[0] + dt1 * z0[1] + dt2 * z0[2];
+  const float d1 = dn * z1[0] + dt1 * z1[1] + dt2 * z1[2];
+  vo1 = q < 2 ? vo1 + d1 : 0.f;
+  if (hj) lga[48 * ENVS] = ya48 + (dn * ea[0] + dt1 * ea[1] + dt2 * ea[2]);
+  if (hj && lb >= 0 && lb != la) lgb[48 * ENVS] = yb48 + (dn * eb[0] + dt1 * eb[1] + dt2 * eb[2]);
+}
+
 template <bool TERR>
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau3, float mb, const float* Ib, V3 cb,
                         float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
-                        unsigned long long* prof) {
+                        float* __restrict__ srow, int N, float mu_s, float rest_s, unsigned long long* prof) {
   LRL_PROF_DECL
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
   const SphLegs SL = sph_legs(K);
@@ -873,6 +1219,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   // own list, so a wave pays max-over-lanes queries instead of every sphere of the model
   uint64_t cand = 0;
   float hwin = 0.f;
+
   if constexpr (TERR) hwin = terrain_window_max(K, st.pos);
   // aa / oo: the carrying leg's joint axes / origins in registers (the leg pass has them; no LDS read-back)
   auto detect = [&](int s, V3 x, float rad, int lsel, int link, const V3* aa, const V3* oo) {
@@ -896,11 +1243,11 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       return;
     }
     const float sep = pz + dot(Rz, x) - rad;
+    M.sph(s, 0) = x.x;  // (every centre: the self-collision pairs read them)
+    M.sph(s, 1) = x.y;
+    M.sph(s, 2) = x.z;
     if (sep < P.contact_offset) {
       active |= (1ull << s);
-      M.sph(s, 0) = x.x;
-      M.sph(s, 1) = x.y;
-      M.sph(s, 2) = x.z;
       V3 u = cross(wb, x) + vb;
       if (lsel >= 0) {
 #pragma unroll
@@ -954,7 +1301,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       for (int s = sb; s < se; ++s)
         if (M.slink(s) == j) {
           const float4 sp = M.sph4(s);
-          detect(s, o + mul(Rj, v3(sp.x, sp.y, sp.z)), sp.w, l, j, aa, oo);
+          const V3 x = o + mul(Rj, v3(sp.x, sp.y, sp.z));
+          detect(s, x, sp.w, l, j, aa, oo);
         }
       Rp = Rj;
       op = o;
@@ -997,6 +1345,11 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     M.leg(l, 42) = sdot(S[0], Fc0);
     M.leg(l, 43) = sdot(S[1], Fc1);
     M.leg(l, 44) = sdot(S[2], Fc2);
+    // the sub-step-start joint rates, for the self-contact restitution test of the other lanes (overwritten by q0
+    // when the contact solve starts)
+    M.leg(l, 45) = st.qd[0];
+    M.leg(l, 46) = st.qd[1];
+    M.leg(l, 47) = st.qd[2];
     Cleg = Fc0;
   }
   if constexpr (TERR) {  // terrain queries of the recorded spheres (the leg frames are in LDS now)
@@ -1043,6 +1396,32 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         row[LIM_B * ENVS] = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
       }
     }
+  }
+  uint64_t sown = 0;  // self-contact slots this lane detected (their rows are built here)
+  if (P.self_collisions) {
+#ifdef LRL_ENV_PROFILE
+    const unsigned long long ts0 = clock64();
+#endif
+    // live groups of this lane: same leg and box always (the gate counted their hits), the legs above when the
+    // bounding boxes (grown by contact_offset / 2) overlap — a culled pair is separated by more than the offset
+    const SelfGate sg = self_gate(K, M, SL, ql, P.contact_offset);
+    unsigned live = 1u | (K->box_h[0] >= 0.f ? 16u : 0u);
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      const V3 lo = v3(quad_bcast(sg.lo.x, l), quad_bcast(sg.lo.y, l), quad_bcast(sg.lo.z, l));
+      const V3 hi = v3(quad_bcast(sg.hi.x, l), quad_bcast(sg.hi.y, l), quad_bcast(sg.hi.z, l));
+      if (l > ql && aabb_overlap(sg.lo, sg.hi, lo, hi)) live |= 1u << (l - ql);
+    }
+    if (__any((int)(sg.hits > 0 || sg.nh > 1 || (live & 14u)))) {  // rare: the LDS pass over the live groups
+      __syncthreads();  // sphere centres, joint frames and rates of the whole quad
+      self_detect(K, M, SL, srow, N, ql, live, dt, rest_s, active, sown);
+#ifdef LRL_ENV_PROFILE
+      if constexpr (!TERR) prof[15] += 1;  // waves entering the LDS pass (per lane: summed over the wave's lanes)
+#endif
+    }
+#ifdef LRL_ENV_PROFILE
+    if constexpr (!TERR) prof[14] += clock64() - ts0;  // self-collision detection (part of kin+dyn+detect)
+#endif
   }
   // ---- quad reductions: legs -> base ----
 #pragma unroll
@@ -1124,6 +1503,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         contact_setup<TERR>(M, Sch, R, s, sph_leg_of(SL, s), M.slink(s));
     }
   }
+  // self-contact rows (owner lanes; rare: only waves with a detected pair enter)
+  if (__any((int)(sown != 0ull)))
+    for (uint64_t m = sown >> (M.nsph + LRL_NUM_DOF); m; m &= m - 1ull) self_setup(M, Sch, R, srow, N, __builtin_ctzll(m));
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
   // lanes apply them in parallel and the base-velocity changes are summed over the quad
   {
@@ -1163,8 +1545,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #pragma unroll
     for (int r = 1; r < 4; ++r) vo0 = ql == r ? vbc[r] : vo0;
     vo1 = ql == 1 ? vbc[5] : (ql == 0 ? vo1 : 0.f);
-    for (int it = 0; it < P.solver_iterations; ++it)
-      for (uint64_t m = active; __any((int)(m != 0ull));) {
+    const uint64_t sact = active >> (M.nsph + LRL_NUM_DOF);  // self-contact slots of the env
+    const uint64_t cact = active & ~(sact << (M.nsph + LRL_NUM_DOF));
+    for (int it = 0; it < P.solver_iterations; ++it) {
+      for (uint64_t m = cact; __any((int)(m != 0ull));) {
         if (m) {
           const int s = __builtin_ctzll(m);
           m &= m - 1ull;
@@ -1174,6 +1558,15 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
             contact_pgs_q(M, s, sph_leg_of(SL, s), mu, ql, vo0, vo1);
         }
       }
+      if (__any((int)(sact != 0ull)))  // self-contact slots after the contacts and limits
+        for (uint64_t m = sact; __any((int)(m != 0ull));) {
+          if (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1ull;
+            self_pgs_q(M, srow, N, k, mu_s, ql, vo0, vo1);
+          }
+        }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) vbc[r] = quad_bcast(vo0, r);
     vbc[4] = quad_bcast(vo1, 0);
@@ -1391,6 +1784,13 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       s4[s] = make_float4(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2], K->sph_rad[s]);
       sl[s] = K->sph_link[s];
     }
+    if (P.self_collisions) {
+      int* sg = sl + nsph;
+      const int* kg = &K->self_grp[0][0][0];
+      for (int i = lane; i < 40; i += BLOCK) sg[i] = kg[i];
+      uint32_t* sp = reinterpret_cast<uint32_t*>(sg + 40);
+      for (int i = lane; i < K->self_npairs; i += BLOCK) sp[i] = K->self_pair[i];
+    }
     __syncthreads();
   }
   const float payload = S.payload[e];
@@ -1404,6 +1804,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   }
   const float mu = 0.5f * (S.friction[e] + P.ground_friction);
   const float rest = 0.5f * (S.restitution[e] + P.ground_restitution);
+  // self-contacts: both shapes carry the env's robot material, so PhysX's average combine is that material
+  const float mu_s = S.friction[e], rest_s = S.restitution[e];
+  float* const srow = S.selfrow + e;
   const bool physics = flags & LRL_STEP_PHYSICS;
   uint64_t active = 0;
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
@@ -1436,7 +1839,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
     }
     LRL_PROF(8)  // PD torques
-    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, prof);
+    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, srow, N, mu_s, rest_s, prof);
 #ifdef LRL_ENV_PROFILE
     prof_t = clock64();
 #endif
@@ -1499,6 +1902,19 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
             fz += M.sph(s, 10);
           }
         }
+      if (active >> (nsph + LRL_NUM_DOF)) {  // self-contacts: +impulse on body A, -impulse on body B (world frame)
+        for (int k = 0; k < LRL_SELF_SLOTS; ++k)
+          if ((active >> (nsph + LRL_NUM_DOF + k)) & 1ull) {
+            const float* row = srow + (size_t)k * SSF * N;
+            const int ba = (int)row[SR_BA * N], bb = (int)row[SR_BB * N];
+            if (ba != b && bb != b) continue;
+            const float sg = ba == b ? 1.f : -1.f;
+            const float l0 = row[SR_LAM * N], l1 = row[(SR_LAM + 1) * N], l2 = row[(SR_LAM + 2) * N];
+            fx += sg * (l0 * row[SR_F * N] + l1 * row[(SR_F + 3) * N] + l2 * row[(SR_F + 6) * N]);
+            fy += sg * (l0 * row[(SR_F + 1) * N] + l1 * row[(SR_F + 4) * N] + l2 * row[(SR_F + 7) * N]);
+            fz += sg * (l0 * row[(SR_F + 2) * N] + l1 * row[(SR_F + 5) * N] + l2 * row[(SR_F + 8) * N]);
+          }
+      }
       fx *= inv_dt;
       fy *= inv_dt;
       fz *= inv_dt;

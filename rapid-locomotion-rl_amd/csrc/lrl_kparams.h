@@ -38,6 +38,13 @@ struct KParams {
   int32_t leg_sph_begin[LRL_NUM_LEGS], leg_sph_end[LRL_NUM_LEGS];
   int32_t body_sph_begin[LRL_MAX_BODIES], body_sph_end[LRL_MAX_BODIES];
   int32_t body_foot[LRL_MAX_BODIES];  // foot slot 0..3 or -1
+  // self-collision candidates (p.self_collisions; lrl_capi.cpp::self_pairs): the canonical pair order is lane (leg
+  // La) major, then per lane the groups g = 0 pairs inside leg La, g = 1..3 against leg La + g, g = 4 against the base
+  // box; a pair packs sphere a | sphere b << 8 (255 = the base box) | body of a << 16 | body of b << 24
+  int32_t self_npairs;
+  int32_t self_grp[LRL_NUM_LEGS][5][2];  // [lane][group] -> [begin, end) in self_pair
+  uint32_t self_pair[LRL_MAX_SELF_PAIRS];
+  float box_c[3], box_h[3];  // base box (the span of the base's spheres): centre and half extents, base frame
   int32_t num_history;
   int32_t n_es, n_cs;                 // rows of episode_sums / command_sums
   // terrain mesh (p.terrain_mesh == 1, lrl_sim_set_terrain): vertex grid [rows][cols] as (x, y, z, 0) in the
@@ -64,6 +71,7 @@ struct KState {
   float *episode_sums, *command_sums, *feet_air_time, *friction, *restitution, *payload, *com, *motor_strength,
       *kp, *kd, *env_origins, *base_lin_vel, *base_ang_vel, *projected_gravity, *joint_pos_target;
   float* heights;  // measured_heights [num_height_points][N]
+  float* selfrow;  // self-contact solver rows [LRL_SELF_SLOTS][SSF][N] (lrl_env.hip; touched only by envs in self-contact)
   const float *inj_noise, *inj_dr;
   const float* inj_reset;  // [n_ids][5] (motor strength, Kp, Kd, x, y) uniforms of an injected reset_idx
 };

@@ -71,7 +71,7 @@ class LrlEnvParams(C.Structure):
         ("terrain_mesh", i32), ("border_size", f32), ("horizontal_scale", f32), ("vertical_scale", f32),
         ("measure_heights", i32), ("num_height_points", i32), ("height_points", f32 * 2 * MAX_HEIGHT_POINTS),
         ("obs_scale_height", f32), ("num_train_envs", i32), ("teleport_x_offset_eval", f32), ("dr_span", f32 * 3),
-        ("joint_limits", i32), ("joint_limit_margin", f32),
+        ("joint_limits", i32), ("joint_limit_margin", f32), ("self_collisions", i32),
     ]
 
 

@@ -96,11 +96,13 @@ def body_sets(cfg, robot):
 
 
 def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte=0.2, terrain_mesh=0,
-                 joint_limits=True, joint_limit_margin=0.02):
+                 joint_limits=True, joint_limit_margin=0.02, self_collisions=None):
     """terrain_mesh: 1 when the sim collides with a generated height field / trimesh (lrl_sim_set_terrain),
     0 for the plane z = 0 (mesh_type 'plane', or a trimesh whose heights are all zero).
     joint_limits: enforce the URDF joint position limits in the contact solve (Isaac Gym / PhysX always enforces
-    them for limited revolute joints: the reference has no switch); joint_limit_margin: activation window, rad."""
+    them for limited revolute joints: the reference has no switch); joint_limit_margin: activation window, rad.
+    self_collisions: None follows Cfg.asset.self_collisions (0 = enabled, Isaac Gym's filter semantics: both presets
+    enable it, mini_cheetah_config.py:44, go1_config.py:44); True / False override."""
     dt = derived(cfg)
     P = _abi.LrlEnvParams()
     dof_names = robot["dof_names"]
@@ -208,5 +210,6 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         teleport_x_offset_eval=float(getattr(cfg.terrain, "x_offset", 0)) * cfg.terrain.horizontal_scale,
         dr_span=[float(r[1]) - float(r[0]) for r in (dr.motor_strength_range, dr.Kp_factor_range, dr.Kd_factor_range)],
         joint_limits=int(joint_limits), joint_limit_margin=joint_limit_margin,
+        self_collisions=int(cfg.asset.self_collisions == 0 if self_collisions is None else self_collisions),
     )
     return P

@@ -16,6 +16,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 which = sys.argv[2] if len(sys.argv) > 2 else "mc"
 cfg = lcfg.make_cfg()
 (lcfg.config_mini_cheetah if which == "mc" else lcfg.config_go1)(cfg)
+if os.environ.get("LRL_SELF") == "0":
+    cfg.asset.self_collisions = 1  # off
 if which == "go1_rough":
     cfg.terrain.mesh_type = "trimesh"
     cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]
@@ -42,7 +44,10 @@ for i, nm in enumerate(names[:9]):
     print(f"{nm:16s} {buf[i] / waves / K:10.0f} cycles/wave/step  {100 * buf[i] / tot:5.1f}%")
 for i, nm in zip(range(10, 14), ["  contact forces", "  loads/teleport/DR", "  rewards+sums", "  obs/priv rows"]):
     print(f"{nm:16s} {buf[i] / waves / K:10.0f} cycles/wave/step  (part of post-physics)")
-if buf[15]:
+if which != "go1_rough" and buf[14]:
+    print(f"  self detect     {buf[14] / waves / K:10.0f} cycles/wave/step  (part of kin+dyn+detect); LDS pass entered "
+          f"{buf[15] / waves / K:.3f} times per wave and step")
+if which == "go1_rough" and buf[15]:
     print(f"  terrain queries {buf[14] / waves / K:10.0f} cycles/wave/step  ({buf[15] / waves / K:.1f} per lane, "
           f"{buf[14] / buf[15]:.0f} cycles each; part of kin+dyn+detect)")
 print(f"total {tot / waves / K:.0f} cycles/wave/step (wave lifetime {buf[9] / waves / K:.0f}); "

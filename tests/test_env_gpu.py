@@ -145,14 +145,37 @@ def _limit_states(rng, n, P, M, root, dof, dofv):
     return dof, dofv, act, pick
 
 
-def _physics_vs_oracle(robot, n, steps, limits=False):
-    cfg, rob, M, P = make(robot, **{"env.num_envs": n})
-    env = _env(robot, n)
-    rng = np.random.default_rng(5 + steps + (100 if limits else 0))
+def _self_states(rng, n, M, root, dof):
+    """Joint angles uniform inside the URDF limits, kept when no candidate pair overlaps by more than 5 mm (a deeper
+    start is a violent Baumgarte push-out, chaotic over ten steps) and filled so that half of the envs start within
+    the contact offset of a self-contact (legs folded into each other or into the base box); half of the robots
+    airborne."""
+    lo, hi = np.array(M.dof_lower[:], np.float32), np.array(M.dof_upper[:], np.float32)
+    near, far = [], []
+    while len(near) < n // 2 or len(far) < n - n // 2:
+        q = rng.uniform(lo + 0.05, hi - 0.05, 12).astype(np.float32)
+        m = oracle.self_pairs(M, q)[1].min()
+        if m < -0.005:
+            continue
+        (near if m < 0.01 else far).append(q)
+    dof = np.stack(near[: n // 2] + far[: n - n // 2])[rng.permutation(n)]
+    root = root.copy()
+    root[: n // 2, 2] = 0.8
+    return root, dof
+
+
+def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True):
+    over = {} if self_on else {"asset.self_collisions": 1}
+    cfg, rob, M, P = make(robot, **{"env.num_envs": n}, **over)
+    env = _env(robot, n, **over)
+    assert P.self_collisions == int(self_on) and env._P.self_collisions == int(self_on)  # presets: asset.self_collisions 0
+    rng = np.random.default_rng(5 + steps + (100 if limits else 0) + (200 if selfc else 0))
     root, dof, dofv = _random_states(rng, n, P, robot)
     act_lim = None
     if limits:
         dof, dofv, act_lim, picked = _limit_states(rng, n, P, M, root, dof, dofv)
+    if selfc:
+        root, dof = _self_states(rng, n, M, root, dof)
     st = oracle.make_state(n, M.num_bodies, P.num_obs, P.num_history, P.num_sum_keys + 1, P.num_sum_keys + 5)
     fr = rng.uniform(0.05, 4.5, n).astype(np.float32)
     rs = rng.uniform(0, 1, n).astype(np.float32)
@@ -194,9 +217,13 @@ def _physics_vs_oracle(robot, n, steps, limits=False):
     pose_tol = 2e-4 if steps == 1 else 4e-4
     sens = np.any([oracle_sensitivity(st, sp, pose_tol) for sp in st_p], axis=0)
     bad, excl = physics_mismatch(got, st, margins, sens, pose_tol)
-    print(f"{robot} n={n} steps={steps} limits={limits}: {excl.sum()} of {n} envs excluded (discontinuity margin "
+    print(f"{robot} n={n} steps={steps} limits={limits} self={selfc}: {excl.sum()} of {n} envs excluded (discontinuity margin "
           f"{((margins[:, 0] < SEP_EPS) | (margins[:, 1] < VEL_EPS)).sum()}, oracle-sensitive {sens.sum()}), "
           f"{bad.sum()} outside tolerance")
+    if bad.any():  # per-field errors of the first bad envs (diagnostics)
+        for e in np.flatnonzero(bad)[:4]:
+            errs = {k: float(np.abs(got[k][e] - st[k][e]).max()) for k in ("root", "dof_pos", "dof_vel", "contact")}
+            print("bad env", e, errs, "margins", margins[e], "sens", sens[e])
     assert bad.sum() == 0, np.flatnonzero(bad)[:16]
     assert excl.mean() <= (0.15 if steps == 1 else 0.4), excl.mean()
     # termination (check_termination, legged_robot.py:190-202): the kernel's flag is exactly its own force test, and
@@ -226,11 +253,20 @@ def test_physics_matches_oracle(robot, n, steps):
 def test_joint_limits_match_oracle(robot, steps):
     """Joint position limits (the URDF limits PhysX enforces): joints started at or past a limit,
     moving into it, with position targets 0.4 rad beyond it.  Kernel and oracle agree within the physics
-    tolerances, and the limit holds: no joint ends more than the Baumgarte-recovering overshoot past its limit."""
-    got, st, M = _physics_vs_oracle(robot, 256, steps, limits=True)
+    tolerances, and the limit holds: no joint ends more than the Baumgarte-recovering overshoot past its limit.
+    (Self-collision off: the limit poses fold legs into the base box, where the two constraints cannot both hold.)"""
+    got, st, M = _physics_vs_oracle(robot, 256, steps, limits=True, self_on=False)
     lo, hi = np.array(M.dof_lower[:], np.float32), np.array(M.dof_upper[:], np.float32)
     over = np.maximum(got["dof_pos"] - hi, lo - got["dof_pos"]).max()
     assert over < (0.09 if steps == 1 else 0.02), over  # started up to 0.03 rad past; recovers at 0.2 / sub-step
+
+
+@pytest.mark.parametrize("robot,steps", [("mc", 1), ("go1", 1), ("mc", 10), ("go1", 10)])
+def test_self_collision_matches_oracle(robot, steps):
+    """Self-collision (Cfg.asset.self_collisions = 0 in both presets): legs folded into each other
+    and into the base box.  Kernel and oracle agree within the physics tolerances, contact forces included (the
+    base's self-contact force feeds the termination test)."""
+    _physics_vs_oracle(robot, 256, steps, selfc=True)
 
 
 @pytest.mark.parametrize("robot", ["mc", "go1"])

@@ -1,0 +1,76 @@
+"""CPU checks of the oracle's self-collision (Cfg.asset.self_collisions = 0 in both presets,
+mini_cheetah_config.py:44, go1_config.py:44, passed to create_actor at legged_robot.py:1246-1247).
+
+* the candidate list follows PhysX's articulation filter: every pair of collision spheres on different links except
+  a link and its parent (the fixed Go1 feet merged into the calves), leg spheres below the hip against the base box;
+* with self-collision on, legs driven into each other and into the base stop there (the Baumgarte-recovered overlap
+  stays small); with it off, the same drive interpenetrates.
+The GPU parity of the kernel against these rows is tests/test_env_gpu.py::test_self_collision_matches_oracle."""
+import numpy as np
+import pytest
+
+from helpers import make
+from lrl import _abi
+from oracle import oracle
+
+
+def _dyn(M, s):
+    b = M.sphere_body[s]
+    return M.body_leg[b], min(M.body_link[b], 2)
+
+
+@pytest.mark.parametrize("robot", ["mc", "go1"])
+def test_candidate_pairs_follow_the_articulation_filter(robot):
+    cfg, rob, M, P = make(robot)
+    pairs, _ = oracle.self_pairs(M)
+    got = {(int(a), int(b)) for a, b in pairs}
+    assert len(got) == len(pairs)  # no duplicates
+    want = set()
+    legs = [s for s in range(M.num_spheres) if M.body_leg[M.sphere_body[s]] >= 0 and M.sphere_radius[s] > 0]
+    for a in legs:
+        la, ka = _dyn(M, a)
+        if ka >= 1:
+            want.add((a, -1))  # not the hip, whose parent is the base
+        for b in legs:
+            lb, kb = _dyn(M, b)
+            if lb < la or (lb == la and (b <= a or abs(ka - kb) < 2)):
+                continue
+            want.add((a, b))
+    assert got == want
+    # canonical order: leg of a, then group (same leg, legs above, the box), then a, then b
+    grp = [(_dyn(M, a)[0], 4 if b < 0 else _dyn(M, b)[0] - _dyn(M, a)[0], a, b) for a, b in pairs]
+    assert grp == sorted(grp)
+
+
+@pytest.mark.parametrize("robot", ["mc", "go1"])
+def test_oracle_self_collision_separates_and_holds(robot):
+    """Passive legs (PD gains 0) started interpenetrating each other or the base by 0.5-2 cm, at rest, in free fall:
+    the self-contact rows push the links apart (Baumgarte) and keep them apart; without them nothing moves them."""
+    n = 4096
+    rng = np.random.default_rng(11)
+    cfg, rob, M, P = make(robot, **{"env.num_envs": 1})
+    lo, hi = np.array(M.dof_lower[:], np.float32), np.array(M.dof_upper[:], np.float32)
+    q0 = rng.uniform(lo + 0.05, hi - 0.05, (n, 12)).astype(np.float32)
+    worst0 = np.array([oracle.self_pairs(M, q)[1].min() for q in q0])
+    q0 = q0[(worst0 < -0.005) & (worst0 > -0.02)][:24]
+    n = len(q0)
+    assert n >= 8
+    act = np.zeros((n, 12), np.float32)
+    pen = np.array([oracle.self_pairs(M, q)[1] for q in q0]) < 0  # the pairs interpenetrating at the start
+    worst = {}
+    for on in (1, 0):
+        cfg, rob, M, P = make(robot, **{"env.num_envs": n})
+        P.self_collisions = on
+        for j in range(12):
+            P.p_gains[j] = P.d_gains[j] = 0.0
+        st = oracle.make_state(n, M.num_bodies, P.num_obs, P.num_history, P.num_sum_keys + 1, P.num_sum_keys + 5)
+        st["root"][:] = 0
+        st["root"][:, 2] = 0.8  # airborne: only the self-contacts act on the legs
+        st["root"][:, 6] = 1
+        st["dof_pos"][:] = q0
+        for s in range(5):
+            oracle.env_step(M, P, st, act, _abi.STEP_PHYSICS, common_step_counter=s + 1)
+        sep = np.array([oracle.self_pairs(M, q)[1] for q in st["dof_pos"]])
+        worst[on] = sep[pen].min()
+    assert worst[0] < -0.005, worst  # still interpenetrated without the rows
+    assert worst[1] > -1e-3, worst  # pushed apart (Baumgarte) with them, within 0.1 s
