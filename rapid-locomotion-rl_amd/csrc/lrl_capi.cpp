@@ -120,6 +120,19 @@ static int self_pairs(const lrl_model* m, KParams* k) {
       k->self_grp[La][g][1] = n;
     }
   k->self_npairs = n;
+  k->self_kmax = 0;
+  for (int L = 0; L < 4; ++L) {
+    int cnt = 0, nh = 0, lead = 1;
+    for (int s = 0; s < m->num_spheres; ++s) {
+      if (leg_of(s) != L) continue;
+      ++cnt;
+      if (lead && link_of(s) == 0 && m->sphere_radius[s] > 0.f) ++nh;
+      else lead = 0;
+    }
+    k->self_nhip[L] = nh;
+    if (cnt > k->self_kmax) k->self_kmax = cnt;
+  }
+  if (k->self_kmax > 8) return fail(LRL_E_INVALID, "more than 8 collision spheres on a leg");
   return 0;
 }
 
@@ -260,7 +273,6 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   addf(&S.joint_pos_target, 12ull * N);
   const int NP = params->measure_heights ? params->num_height_points : 0;
   addf(&S.heights, (size_t)(NP > 0 ? NP : 1) * N);
-  addf(&S.selfrow, (size_t)LRL_SELF_SLOTS * 104 * N);  // SSF of lrl_env.hip
   size_t total = 0;
   for (auto& f : fields) total += (f.bytes + 255) / 256 * 256;
   void* arena = nullptr;

@@ -35,7 +35,6 @@
 #define ENVS (BLOCK / QL)
 #define NSF 67  // LDS fields per contact sphere (map above contact_setup)
 #define LIMF 19  // LDS fields per joint-limit row (map above limit_setup)
-#define SSF 104  // HBM fields per self-contact row (map above self_setup; lrl_capi.cpp sizes KState::selfrow with it)
 
 namespace lrl {
 
@@ -831,8 +830,10 @@ __device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
 // an impulse moves v_b by lambda S^-1 g_d and Y_A / Y_B by lambda D^-1 hA_d / D^-1 hB_d (a same-leg pair folds hB
 // into hA; the base box has no hB).  The first LRL_SELF_SLOTS active pairs of an env in the canonical order get
 // the solver rows after the joint limits (bits nsph + 12 + slot), built cold every sub-step (no warm start: a
-// pair's slot can change between sub-steps).  Rows live in HBM (KState::selfrow, [slot][SSF][N]; the LDS is
-// spent on the contact rows): only envs in self-contact touch them.  Field map:
+// pair's slot can change between sub-steps).  A row lives in the LDS rows of two contact spheres the env has NOT in
+// ground contact in the sub-step (fields 3..66 of each, 128 floats; fields 0..2 keep the sphere centres the detection
+// reads): slot k takes the env's free spheres 2k and 2k + 1 in index order, so an env gets min(LRL_SELF_SLOTS, free / 2)
+// slots (the oracle applies the same cap).  Field map:
 //   0..2 n (base frame)  3..5 x (base frame)  6 leg A  7 leg B (-1: base box)  8 link A  9 link B  10 velocity target
 //   11..13 impulse (n, t1, t2)  14 1/W_nn  15 W_t1n  16 W_t2n  17..19 (W_tt)^-1 (11, 12, 22)  20..37 g_d
 //   38..46 hA_d  47..55 hB_d  56..73 z_d = S^-1 g_d  74..82 D_A^-1 hA_d  83..91 D_B^-1 hB_d
@@ -856,6 +857,28 @@ __device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
 #define SR_F 92
 #define SR_BA 101
 #define SR_BB 102
+
+// the n-th set bit of m (n < popcount(m))
+__device__ __forceinline__ int nth_bit(uint64_t m, int n) {
+  for (int i = 0; i < n; ++i) m &= m - 1ull;
+  return __builtin_ctzll(m);
+}
+// self-contact row k of this env in the rows of its free spheres 2k, 2k + 1 (constant field indices fold the choice)
+struct SRow {
+  float* a;
+  float* b;
+  __device__ __forceinline__ float& operator[](int f) const { return f < 64 ? a[f * ENVS] : b[(f - 64) * ENVS]; }
+};
+__device__ __forceinline__ SRow self_row(const Lds& M, uint64_t freem, int k) {
+  const int h1 = nth_bit(freem, 2 * k);
+  const int h2 = __builtin_ctzll(freem & ~((2ull << h1) - 1ull));  // the next free sphere
+  return SRow{M.sp(h1) + 3 * ENVS, M.sp(h2) + 3 * ENVS};
+}
+// spheres of the env free of ground contact (the quad-ORed active mask's sphere bits)
+__device__ __forceinline__ uint64_t free_spheres(const Lds& M, uint64_t act) {
+  const uint64_t all = M.nsph >= 64 ? ~0ull : (1ull << M.nsph) - 1ull;
+  return ~act & all;
+}
 
 // separation of a sphere (centre ca, radius ra) against a sphere (cb, rb) or, box, the base box: n from B to A, x = the
 // contact point (contraction off: the register gate and the LDS pass evaluate it bitwise alike)
@@ -911,54 +934,59 @@ __device__ __forceinline__ int quad_bcast_i(int v, int l) { return __float_as_in
 // offset widened by 1e-5 m: conservative, the LDS pass decides every pair the gate lets through exactly.
 struct SelfGate {
   V3 lo, hi;     // this leg's sphere surfaces grown by contact_offset / 2
-  int hits, nh;  // same-leg + box candidates; link-0 spheres with a radius (> 2: the LDS pass decides)
+  int hits;      // same-leg + box candidates (and 1 for a leg with more than two link-0 spheres: the LDS pass decides)
 };
 __device__ __forceinline__ SelfGate self_gate(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, int ql,
                                               float co) {
   const int b = ql == 0 ? SL.b[0] : ql == 1 ? SL.b[1] : ql == 2 ? SL.b[2] : SL.b[3];
   const int e = ql == 0 ? SL.e[0] : ql == 1 ? SL.e[1] : ql == 2 ? SL.e[2] : SL.e[3];
+  const int kmax = __builtin_amdgcn_readfirstlane(K->self_kmax);  // (wave-uniform loop bound)
+  const int nhip = K->self_nhip[ql];
   float cx[8], cy[8], cz[8], r[8];
   int lk[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int s = min(b + k, e - 1);
-    cx[k] = M.sph(s, 0);
-    cy[k] = M.sph(s, 1);
-    cz[k] = M.sph(s, 2);
-    r[k] = M.sph4(s).w;
-    lk[k] = M.slink(s);
-  }
-  const float cw = co + 1e-5f;
+  for (int k = 0; k < 8; ++k)
+    if (k < kmax) {
+      const int s = min(b + k, e - 1);
+      cx[k] = M.sph(s, 0);
+      cy[k] = M.sph(s, 1);
+      cz[k] = M.sph(s, 2);
+      r[k] = M.sph4(s).w;
+      lk[k] = M.slink(s);
+    }
+  const float cw = co + 1e-5f, hc = 0.5f * co;
   const float bcx = K->box_c[0], bcy = K->box_c[1], bcz = K->box_c[2];
   const float bhx = K->box_h[0], bhy = K->box_h[1], bhz = K->box_h[2];
+  const bool box = bhx >= 0.f;
+  // the leg's hip spheres (its first one or two spheres when it has them)
+  const float h0x = cx[0], h0y = cy[0], h0z = cz[0], h0r = nhip >= 1 ? r[0] + cw : -1e30f;
+  const float h1x = cx[1], h1y = cy[1], h1z = cz[1], h1r = nhip >= 2 ? r[1] + cw : -1e30f;
   SelfGate G;
   G.lo = v3(1e30f, 1e30f, 1e30f);
   G.hi = v3(-1e30f, -1e30f, -1e30f);
-  G.hits = 0;
-  G.nh = 0;
-  float h0x = 0.f, h0y = 0.f, h0z = 0.f, h0r = -1e30f;  // the leg's first link-0 sphere
+  int hits = nhip > 2 ? 1 : 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const bool use = b + k < e && r[k] > 0.f;
-    const float rg = r[k] + 0.5f * co;
-    if (use) {
-      G.lo = v3(fminf(G.lo.x, cx[k] - rg), fminf(G.lo.y, cy[k] - rg), fminf(G.lo.z, cz[k] - rg));
-      G.hi = v3(fmaxf(G.hi.x, cx[k] + rg), fmaxf(G.hi.y, cy[k] + rg), fmaxf(G.hi.z, cz[k] + rg));
+  for (int k = 0; k < 8; ++k)
+    if (k < kmax) {
+      const bool use = b + k < e;
+      const float rg = r[k] + hc;
+      const float xl = use ? cx[k] - rg : 1e30f, yl = use ? cy[k] - rg : 1e30f, zl = use ? cz[k] - rg : 1e30f;
+      const float xh = use ? cx[k] + rg : -1e30f, yh = use ? cy[k] + rg : -1e30f, zh = use ? cz[k] + rg : -1e30f;
+      G.lo = v3(fminf(G.lo.x, xl), fminf(G.lo.y, yl), fminf(G.lo.z, zl));
+      G.hi = v3(fmaxf(G.hi.x, xh), fmaxf(G.hi.y, yh), fmaxf(G.hi.z, zh));
+      // base box: squared distance of the centre from the box (0 inside) against (r + offset)^2
+      const float qx = fmaxf(fabsf(cx[k] - bcx) - bhx, 0.f), qy = fmaxf(fabsf(cy[k] - bcy) - bhy, 0.f),
+                  qz = fmaxf(fabsf(cz[k] - bcz) - bhz, 0.f);
+      const float rb = r[k] + cw;
+      const bool hb = box && lk[k] >= 1 && qx * qx + qy * qy + qz * qz < rb * rb;
+      // the hip spheres against the calf's
+      const float ax = cx[k] - h0x, ay = cy[k] - h0y, az = cz[k] - h0z, rh = h0r + r[k];
+      const float bx = cx[k] - h1x, by = cy[k] - h1y, bz = cz[k] - h1z, ri = h1r + r[k];
+      const bool hh = lk[k] == 2 && ((rh > 0.f && ax * ax + ay * ay + az * az < rh * rh) ||
+                                     (ri > 0.f && bx * bx + by * by + bz * bz < ri * ri));
+      hits += (use && (hb || hh)) ? 1 : 0;
     }
-    // base box: squared distance of the centre from the box (0 inside) against (r + offset)^2
-    const float px = fabsf(cx[k] - bcx) - bhx, py = fabsf(cy[k] - bcy) - bhy, pz = fabsf(cz[k] - bcz) - bhz;
-    const float qx = fmaxf(px, 0.f), qy = fmaxf(py, 0.f), qz = fmaxf(pz, 0.f);
-    const float rb = r[k] + cw;
-    const bool hb = qx * qx + qy * qy + qz * qz < rb * rb;
-    // the leg's hip sphere
-    const float ax = cx[k] - h0x, ay = cy[k] - h0y, az = cz[k] - h0z, rh = h0r + rb;
-    const bool hh = rh > 0.f && ax * ax + ay * ay + az * az < rh * rh;
-    G.hits += (use && ((lk[k] >= 1 && bhx >= 0.f && hb) || (lk[k] == 2 && hh))) ? 1 : 0;
-    if (use && lk[k] == 0) {
-      if (G.nh == 0) { h0x = cx[k]; h0y = cy[k]; h0z = cz[k]; h0r = r[k]; }
-      G.nh += 1;  // (a second link-0 sphere sends the leg to the LDS pass)
-    }
-  }
+  G.hits = hits;
   return G;
 }
 
@@ -966,8 +994,8 @@ __device__ __forceinline__ SelfGate self_gate(const KParams* __restrict__ K, con
 // leg with more than two link-0 spheres): the canonical count over this lane's live groups from the LDS centres, the
 // quad prefix of the counts, then the first LRL_SELF_SLOTS hits get rows — geometry, legs / links / bodies and the
 // velocity target (restitution from the sub-step-start joint rates, LDS leg fields 45..47).
-__device__ __attribute__((noinline)) void self_detect(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, float* __restrict__ srow,
-                            int N, int ql, unsigned live, float dt, float rest, uint64_t& active, uint64_t& sown) {
+__device__ void self_detect(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, int ql, unsigned live,
+                            float dt, float rest, uint64_t& active, uint64_t& sown) {
   const lrl_env_params& P = K->p;
   const float co = P.contact_offset;
   const int* G = M.sgrp() + 10 * ql;
@@ -981,7 +1009,8 @@ __device__ __attribute__((noinline)) void self_detect(const KParams* __restrict_
       }
   const int c0 = quad_bcast_i(cnt, 0), c1 = quad_bcast_i(cnt, 1), c2 = quad_bcast_i(cnt, 2);
   int slot = ql == 0 ? 0 : ql == 1 ? c0 : ql == 2 ? c0 + c1 : c0 + c1 + c2;
-  const int end = min(slot + cnt, LRL_SELF_SLOTS);
+  const uint64_t freem = free_spheres(M, quad_or(active));
+  const int end = min(slot + cnt, min(LRL_SELF_SLOTS, __builtin_popcountll(freem) >> 1));
   if (slot >= end) return;
 #pragma unroll
   for (int g = 0; g < 5; ++g)
@@ -1004,16 +1033,16 @@ __device__ __attribute__((noinline)) void self_detect(const KParams* __restrict_
         }
         float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
         if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
-        float* const row = srow + (size_t)slot * SSF * N;
-        row[(SR_N + 0) * N] = n.x; row[(SR_N + 1) * N] = n.y; row[(SR_N + 2) * N] = n.z;
-        row[(SR_X + 0) * N] = x.x; row[(SR_X + 1) * N] = x.y; row[(SR_X + 2) * N] = x.z;
-        row[SR_LA * N] = (float)la;
-        row[SR_LB * N] = (float)lb;
-        row[SR_KA * N] = (float)ka;
-        row[SR_KB * N] = (float)kb;
-        row[SR_B * N] = tgt;
-        row[SR_BA * N] = (float)((pk >> 16) & 255u);
-        row[SR_BB * N] = (float)(pk >> 24);
+        const SRow row = self_row(M, freem, slot);
+        row[SR_N + 0] = n.x; row[SR_N + 1] = n.y; row[SR_N + 2] = n.z;
+        row[SR_X + 0] = x.x; row[SR_X + 1] = x.y; row[SR_X + 2] = x.z;
+        row[SR_LA] = (float)la;
+        row[SR_LB] = (float)lb;
+        row[SR_KA] = (float)ka;
+        row[SR_KB] = (float)kb;
+        row[SR_B] = tgt;
+        row[SR_BA] = (float)((pk >> 16) & 255u);
+        row[SR_BB] = (float)(pk >> 24);
         const uint64_t bit = 1ull << (M.nsph + LRL_NUM_DOF + slot);
         active |= bit;
         sown |= bit;
@@ -1022,11 +1051,11 @@ __device__ __attribute__((noinline)) void self_detect(const KParams* __restrict_
 }
 
 // solver rows of self-contact slot k in its owner lane (every global / LDS read up front)
-__device__ __attribute__((noinline)) void self_setup(const Lds& M, const float* Si, const M3& R, float* __restrict__ srow, int N, int k) {
-  float* const row = srow + (size_t)k * SSF * N;
-  const V3 n = v3(row[SR_N * N], row[(SR_N + 1) * N], row[(SR_N + 2) * N]);
-  const V3 x = v3(row[SR_X * N], row[(SR_X + 1) * N], row[(SR_X + 2) * N]);
-  const int la = (int)row[SR_LA * N], lb = (int)row[SR_LB * N], ka = (int)row[SR_KA * N], kb = (int)row[SR_KB * N];
+__device__ void self_setup(const Lds& M, const float* Si, const M3& R, uint64_t freem, int k) {
+  const SRow row = self_row(M, freem, k);
+  const V3 n = v3(row[SR_N], row[SR_N + 1], row[SR_N + 2]);
+  const V3 x = v3(row[SR_X], row[SR_X + 1], row[SR_X + 2]);
+  const int la = (int)row[SR_LA], lb = (int)row[SR_LB], ka = (int)row[SR_KA], kb = (int)row[SR_KB];
   const int lbr = lb < 0 ? la : lb;
   V3 ca[3], cbv[3];
   float kxa[3][6], kxb[3][6], dia[6], dib[6];
@@ -1088,49 +1117,49 @@ __device__ __attribute__((noinline)) void self_setup(const Lds& M, const float* 
   for (int d = 0; d < 3; ++d) {
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      row[(SR_G + 6 * d + r) * N] = g[d][r];
-      row[(SR_Z + 6 * d + r) * N] = z[d][r];
+      row[SR_G + 6 * d + r] = g[d][r];
+      row[SR_Z + 6 * d + r] = z[d][r];
     }
-    row[(SR_HA + 3 * d) * N] = ha[d].x; row[(SR_HA + 3 * d + 1) * N] = ha[d].y; row[(SR_HA + 3 * d + 2) * N] = ha[d].z;
-    row[(SR_HB + 3 * d) * N] = hb[d].x; row[(SR_HB + 3 * d + 1) * N] = hb[d].y; row[(SR_HB + 3 * d + 2) * N] = hb[d].z;
-    row[(SR_EA + 3 * d) * N] = ea[d].x; row[(SR_EA + 3 * d + 1) * N] = ea[d].y; row[(SR_EA + 3 * d + 2) * N] = ea[d].z;
-    row[(SR_EB + 3 * d) * N] = eb[d].x; row[(SR_EB + 3 * d + 1) * N] = eb[d].y; row[(SR_EB + 3 * d + 2) * N] = eb[d].z;
+    row[SR_HA + 3 * d] = ha[d].x; row[SR_HA + 3 * d + 1] = ha[d].y; row[SR_HA + 3 * d + 2] = ha[d].z;
+    row[SR_HB + 3 * d] = hb[d].x; row[SR_HB + 3 * d + 1] = hb[d].y; row[SR_HB + 3 * d + 2] = hb[d].z;
+    row[SR_EA + 3 * d] = ea[d].x; row[SR_EA + 3 * d + 1] = ea[d].y; row[SR_EA + 3 * d + 2] = ea[d].z;
+    row[SR_EB + 3 * d] = eb[d].x; row[SR_EB + 3 * d + 1] = eb[d].y; row[SR_EB + 3 * d + 2] = eb[d].z;
     const V3 fw = mul(R, fr[d]);
-    row[(SR_F + 3 * d) * N] = fw.x; row[(SR_F + 3 * d + 1) * N] = fw.y; row[(SR_F + 3 * d + 2) * N] = fw.z;
-    row[(SR_LAM + d) * N] = 0.f;
+    row[SR_F + 3 * d] = fw.x; row[SR_F + 3 * d + 1] = fw.y; row[SR_F + 3 * d + 2] = fw.z;
+    row[SR_LAM + d] = 0.f;
   }
-  row[SR_IW * N] = W[0][0] > 1e-12f ? 1.f / W[0][0] : 0.f;
-  row[(SR_IW + 1) * N] = W[1][0];
-  row[(SR_IW + 2) * N] = W[2][0];
-  row[(SR_IW + 3) * N] = W[2][2] * id;
-  row[(SR_IW + 4) * N] = -W[1][2] * id;
-  row[(SR_IW + 5) * N] = W[1][1] * id;
+  row[SR_IW] = W[0][0] > 1e-12f ? 1.f / W[0][0] : 0.f;
+  row[SR_IW + 1] = W[1][0];
+  row[SR_IW + 2] = W[2][0];
+  row[SR_IW + 3] = W[2][2] * id;
+  row[SR_IW + 4] = -W[1][2] * id;
+  row[SR_IW + 5] = W[1][1] * id;
 }
 
 // Gauss-Seidel update of self-contact slot k with the base velocity spread over the quad as in contact_pgs_q: lane q
 // owns v_b[q], v_b[q + 4] (q < 2) and component q of Y_A and Y_B
-__device__ __attribute__((noinline)) void self_pgs_q(const Lds& M, float* __restrict__ srow, int N, int k, float mu, int q,
+__device__ __forceinline__ void self_pgs_q(const Lds& M, uint64_t freem, int k, float mu, int q,
                                            float& vo0, float& vo1) {
-  float* const row = srow + (size_t)k * SSF * N;
+  const SRow row = self_row(M, freem, k);
   const bool hj = q < 3;
   const int qh = hj ? q : 2;
-  const int la = (int)row[SR_LA * N], lb = (int)row[SR_LB * N];
+  const int la = (int)row[SR_LA], lb = (int)row[SR_LB];
   const int lbr = lb < 0 ? la : lb;
   float g0[3], g1[3], ha[3], hb[3], z0[3], z1[3], ea[3], eb[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {  // (lanes 2, 3 read g / z entries 6, 7 of the next field group for the v_b[q + 4]
-    g0[d] = row[(SR_G + 6 * d + q) * N];  //  terms; vo1 = 0 there)
-    g1[d] = row[(SR_G + 6 * d + q + 4) * N];
-    z0[d] = row[(SR_Z + 6 * d + q) * N];
-    z1[d] = row[(SR_Z + 6 * d + q + 4) * N];
-    ha[d] = row[(SR_HA + 3 * d + qh) * N];
-    hb[d] = row[(SR_HB + 3 * d + qh) * N];
-    ea[d] = row[(SR_EA + 3 * d + qh) * N];
-    eb[d] = row[(SR_EB + 3 * d + qh) * N];
+    g0[d] = row[SR_G + 6 * d + q];  //  terms; vo1 = 0 there)
+    g1[d] = row[SR_G + 6 * d + q + 4];
+    z0[d] = row[SR_Z + 6 * d + q];
+    z1[d] = row[SR_Z + 6 * d + q + 4];
+    ha[d] = row[SR_HA + 3 * d + qh];
+    hb[d] = row[SR_HB + 3 * d + qh];
+    ea[d] = row[SR_EA + 3 * d + qh];
+    eb[d] = row[SR_EB + 3 * d + qh];
   }
-  const float iWnn = row[SR_IW * N], Wt1n = row[(SR_IW + 1) * N], Wt2n = row[(SR_IW + 2) * N];
-  const float i11 = row[(SR_IW + 3) * N], i12 = row[(SR_IW + 4) * N], i22 = row[(SR_IW + 5) * N], b = row[SR_B * N];
-  const float ln0 = row[SR_LAM * N], lt10 = row[(SR_LAM + 1) * N], lt20 = row[(SR_LAM + 2) * N];
+  const float iWnn = row[SR_IW], Wt1n = row[SR_IW + 1], Wt2n = row[SR_IW + 2];
+  const float i11 = row[SR_IW + 3], i12 = row[SR_IW + 4], i22 = row[SR_IW + 5], b = row[SR_B];
+  const float ln0 = row[SR_LAM], lt10 = row[SR_LAM + 1], lt20 = row[SR_LAM + 2];
   float* const lga = M.lp(la) + qh * ENVS;
   float* const lgb = M.lp(lbr) + qh * ENVS;
   const float ya45 = lga[45 * ENVS], ya48 = lga[48 * ENVS], yb45 = lgb[45 * ENVS], yb48 = lgb[48 * ENVS];
@@ -1149,9 +1178,9 @@ __device__ __attribute__((noinline)) void self_pgs_q(const Lds& M, float* __rest
   const float sc = nt2 > lim * lim ? (nt2 > 0.f ? lim * rsqrtf(nt2) : 0.f) : 1.f;
   lt1 *= sc;
   lt2 *= sc;
-  row[SR_LAM * N] = ln;  // (the four lanes store the same values)
-  row[(SR_LAM + 1) * N] = lt1;
-  row[(SR_LAM + 2) * N] = lt2;
+  row[SR_LAM] = ln;  // (the four lanes store the same values)
+  row[SR_LAM + 1] = lt1;
+  row[SR_LAM + 2] = lt2;
   const float dt1 = lt1 - lt10, dt2 = lt2 - lt20;
   vo0 += dn * z0[0] + dt1 * z0[1] + dt2 * z0[2];
   const float d1 = dn * z1[0] + dt1 * z1[1] + dt2 * z1[2];
@@ -1163,7 +1192,7 @@ __device__ __attribute__((noinline)) void self_pgs_q(const Lds& M, float* __rest
 template <bool TERR>
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau3, float mb, const float* Ib, V3 cb,
                         float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
-                        float* __restrict__ srow, int N, float mu_s, float rest_s, unsigned long long* prof) {
+                        float mu_s, float rest_s, unsigned long long* prof) {
   LRL_PROF_DECL
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
   const SphLegs SL = sph_legs(K);
@@ -1397,32 +1426,6 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       }
     }
   }
-  uint64_t sown = 0;  // self-contact slots this lane detected (their rows are built here)
-  if (P.self_collisions) {
-#ifdef LRL_ENV_PROFILE
-    const unsigned long long ts0 = clock64();
-#endif
-    // live groups of this lane: same leg and box always (the gate counted their hits), the legs above when the
-    // bounding boxes (grown by contact_offset / 2) overlap — a culled pair is separated by more than the offset
-    const SelfGate sg = self_gate(K, M, SL, ql, P.contact_offset);
-    unsigned live = 1u | (K->box_h[0] >= 0.f ? 16u : 0u);
-#pragma unroll
-    for (int l = 1; l < 4; ++l) {
-      const V3 lo = v3(quad_bcast(sg.lo.x, l), quad_bcast(sg.lo.y, l), quad_bcast(sg.lo.z, l));
-      const V3 hi = v3(quad_bcast(sg.hi.x, l), quad_bcast(sg.hi.y, l), quad_bcast(sg.hi.z, l));
-      if (l > ql && aabb_overlap(sg.lo, sg.hi, lo, hi)) live |= 1u << (l - ql);
-    }
-    if (__any((int)(sg.hits > 0 || sg.nh > 1 || (live & 14u)))) {  // rare: the LDS pass over the live groups
-      __syncthreads();  // sphere centres, joint frames and rates of the whole quad
-      self_detect(K, M, SL, srow, N, ql, live, dt, rest_s, active, sown);
-#ifdef LRL_ENV_PROFILE
-      if constexpr (!TERR) prof[15] += 1;  // waves entering the LDS pass (per lane: summed over the wave's lanes)
-#endif
-    }
-#ifdef LRL_ENV_PROFILE
-    if constexpr (!TERR) prof[14] += clock64() - ts0;  // self-collision detection (part of kin+dyn+detect)
-#endif
-  }
   // ---- quad reductions: legs -> base ----
 #pragma unroll
   for (int k = 0; k < 21; ++k) Sch[k] = quad_sum(Sch[k]);
@@ -1474,6 +1477,36 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       nu[6 + j] += dt * (M.leg(ql, 42 + j) - kx);
     }
   }
+  // self-collision detection here, after the Schur / free-acceleration arithmetic (the leg pass's LDS stores have
+  // drained by now, so the gate's reads do not wait on them) and before the contact solve overwrites the sub-step-start
+  // joint rates in leg fields 45..47
+  uint64_t sown = 0;  // self-contact slots this lane detected (their rows are built here)
+  if (P.self_collisions) {
+#ifdef LRL_ENV_PROFILE
+    const unsigned long long ts0 = clock64();
+#endif
+    // live groups of this lane: same leg and box always (the gate counted their hits), the legs above when the
+    // bounding boxes (grown by contact_offset / 2) overlap — a culled pair is separated by more than the offset
+    const SelfGate sg = self_gate(K, M, SL, ql, P.contact_offset);
+    unsigned live = 1u | (K->box_h[0] >= 0.f ? 16u : 0u);
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      const V3 lo = v3(quad_bcast(sg.lo.x, l), quad_bcast(sg.lo.y, l), quad_bcast(sg.lo.z, l));
+      const V3 hi = v3(quad_bcast(sg.hi.x, l), quad_bcast(sg.hi.y, l), quad_bcast(sg.hi.z, l));
+      if (l > ql && aabb_overlap(sg.lo, sg.hi, lo, hi)) live |= 1u << (l - ql);
+    }
+    if (__any((int)(sg.hits > 0 || (live & 14u)))) {  // rare: the LDS pass over the live groups
+      __syncthreads();  // sphere centres, joint frames and rates of the whole quad
+      self_detect(K, M, SL, ql, live, dt, rest_s, active, sown);
+      active = quad_or(active);
+#ifdef LRL_ENV_PROFILE
+      if constexpr (!TERR) prof[15] += 1;  // waves entering the LDS pass (per lane: summed over the wave's lanes)
+#endif
+    }
+#ifdef LRL_ENV_PROFILE
+    if constexpr (!TERR) prof[14] += clock64() - ts0;  // self-collision detection (part of schur+free acc)
+#endif
+  }
   LRL_PROF(1)  // Schur complement factor / inverse, free acceleration
   // contact solve.  Start state: v_b0 = free base velocity, qd0 = free joint rates (LDS), Y = 0.
   float vb0[6], vbc[6];
@@ -1505,7 +1538,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   }
   // self-contact rows (owner lanes; rare: only waves with a detected pair enter)
   if (__any((int)(sown != 0ull)))
-    for (uint64_t m = sown >> (M.nsph + LRL_NUM_DOF); m; m &= m - 1ull) self_setup(M, Sch, R, srow, N, __builtin_ctzll(m));
+    for (uint64_t m = sown >> (M.nsph + LRL_NUM_DOF); m; m &= m - 1ull)
+      self_setup(M, Sch, R, free_spheres(M, active), __builtin_ctzll(m));
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
   // lanes apply them in parallel and the base-velocity changes are summed over the quad
   {
@@ -1563,7 +1597,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
           if (m) {
             const int k = __builtin_ctzll(m);
             m &= m - 1ull;
-            self_pgs_q(M, srow, N, k, mu_s, ql, vo0, vo1);
+            self_pgs_q(M, free_spheres(M, active), k, mu_s, ql, vo0, vo1);
           }
         }
     }
@@ -1806,7 +1840,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   const float rest = 0.5f * (S.restitution[e] + P.ground_restitution);
   // self-contacts: both shapes carry the env's robot material, so PhysX's average combine is that material
   const float mu_s = S.friction[e], rest_s = S.restitution[e];
-  float* const srow = S.selfrow + e;
   const bool physics = flags & LRL_STEP_PHYSICS;
   uint64_t active = 0;
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
@@ -1839,7 +1872,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
     }
     LRL_PROF(8)  // PD torques
-    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, srow, N, mu_s, rest_s, prof);
+    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, mu_s, rest_s, prof);
 #ifdef LRL_ENV_PROFILE
     prof_t = clock64();
 #endif
@@ -1905,14 +1938,14 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       if (active >> (nsph + LRL_NUM_DOF)) {  // self-contacts: +impulse on body A, -impulse on body B (world frame)
         for (int k = 0; k < LRL_SELF_SLOTS; ++k)
           if ((active >> (nsph + LRL_NUM_DOF + k)) & 1ull) {
-            const float* row = srow + (size_t)k * SSF * N;
-            const int ba = (int)row[SR_BA * N], bb = (int)row[SR_BB * N];
+            const SRow row = self_row(M, free_spheres(M, active), k);
+            const int ba = (int)row[SR_BA], bb = (int)row[SR_BB];
             if (ba != b && bb != b) continue;
             const float sg = ba == b ? 1.f : -1.f;
-            const float l0 = row[SR_LAM * N], l1 = row[(SR_LAM + 1) * N], l2 = row[(SR_LAM + 2) * N];
-            fx += sg * (l0 * row[SR_F * N] + l1 * row[(SR_F + 3) * N] + l2 * row[(SR_F + 6) * N]);
-            fy += sg * (l0 * row[(SR_F + 1) * N] + l1 * row[(SR_F + 4) * N] + l2 * row[(SR_F + 7) * N]);
-            fz += sg * (l0 * row[(SR_F + 2) * N] + l1 * row[(SR_F + 5) * N] + l2 * row[(SR_F + 8) * N]);
+            const float l0 = row[SR_LAM], l1 = row[SR_LAM + 1], l2 = row[SR_LAM + 2];
+            fx += sg * (l0 * row[SR_F] + l1 * row[SR_F + 3] + l2 * row[SR_F + 6]);
+            fy += sg * (l0 * row[SR_F + 1] + l1 * row[SR_F + 4] + l2 * row[SR_F + 7]);
+            fz += sg * (l0 * row[SR_F + 2] + l1 * row[SR_F + 5] + l2 * row[SR_F + 8]);
           }
       }
       fx *= inv_dt;

@@ -42,6 +42,8 @@ struct KParams {
   // La) major, then per lane the groups g = 0 pairs inside leg La, g = 1..3 against leg La + g, g = 4 against the base
   // box; a pair packs sphere a | sphere b << 8 (255 = the base box) | body of a << 16 | body of b << 24
   int32_t self_npairs;
+  int32_t self_nhip[LRL_NUM_LEGS];  // the leg's leading link-0 spheres with a radius (the same-leg group's sphere a)
+  int32_t self_kmax;                // most spheres on one leg (<= 8)
   int32_t self_grp[LRL_NUM_LEGS][5][2];  // [lane][group] -> [begin, end) in self_pair
   uint32_t self_pair[LRL_MAX_SELF_PAIRS];
   float box_c[3], box_h[3];  // base box (the span of the base's spheres): centre and half extents, base frame
@@ -71,7 +73,6 @@ struct KState {
   float *episode_sums, *command_sums, *feet_air_time, *friction, *restitution, *payload, *com, *motor_strength,
       *kp, *kd, *env_origins, *base_lin_vel, *base_ang_vel, *projected_gravity, *joint_pos_target;
   float* heights;  // measured_heights [num_height_points][N]
-  float* selfrow;  // self-contact solver rows [LRL_SELF_SLOTS][SSF][N] (lrl_env.hip; touched only by envs in self-contact)
   const float *inj_noise, *inj_dr;
   const float* inj_reset;  // [n_ids][5] (motor strength, Kp, Kd, x, y) uniforms of an injected reset_idx
 };
