@@ -113,7 +113,8 @@ typedef struct lrl_env_params {
   int32_t solver_iterations;
   float baumgarte;
   /* control (legged_robot.py:653-688) */
-  int32_t control_type; /* 0 = 'P' (only one supported) */
+  int32_t control_type; /* 0 = 'P', 1 = 'V', 2 = 'T' (legged_robot.py:668-675; 'P_compliantfeet' indexes DOF 15 of 12
+                         * and raises in the reference, so the host refuses it) */
   float action_scale, hip_scale_reduction, clip_actions;
   float p_gains[LRL_NUM_DOF], d_gains[LRL_NUM_DOF], default_dof_pos[LRL_NUM_DOF];
   float torque_limits[LRL_NUM_DOF];
@@ -184,6 +185,14 @@ typedef struct lrl_env_params {
    * base-corner spheres span), up to LRL_SELF_SLOTS contacts per env and sub-step in the canonical pair order,
    * friction / restitution of the robot's own material.  0 = off. */
   int32_t self_collisions;
+  /* _push_robots (legged_robot.py:757-766, called from _post_physics_step_callback :588): envs whose episode length
+   * (after this step's increment) is a multiple of push_interval get root linear velocity x / y =
+   * push_span * u + push_lo (torch_rand_float(-max_push_vel_xy, max_push_vel_xy, (k, 2)), float32 order), after the
+   * base-frame velocities of the step were taken (so it shows in root_states / last_root_vel, not in this step's obs).
+   * 0 = off. */
+  int32_t push_robots;
+  int32_t push_interval;
+  float push_lo, push_span;
 } lrl_env_params;
 
 /* ------------------------------------------------------------------------------------------
@@ -259,6 +268,9 @@ int32_t lrl_sim_step(lrl_sim* sim, const float* actions, uint32_t flags, void* s
 
 /* Injected uniforms for parity tests: noise_u [N,num_obs], dr_u [N] (NaN = no redraw). */
 int32_t lrl_sim_inject_uniforms(lrl_sim* sim, const float* noise_u, const float* dr_u);
+/* Injected push uniforms for parity tests: u [N,2] f32 device, row e = env e's (x, y) draw of _push_robots when it is
+ * pushed in the step (legged_robot.py:763-764); required with LRL_STEP_INJECT_UNIFORM when push_robots is on. */
+int32_t lrl_sim_inject_push_uniforms(lrl_sim* sim, const float* u);
 
 int32_t lrl_sim_reset_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, void* stream);
 /* reset_idx (legged_robot.py:227-290) with the root-state policy made explicit.

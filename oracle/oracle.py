@@ -88,7 +88,7 @@ def make_state(n, num_bodies, num_obs, num_hist, n_es, n_cs, num_height_points=0
 
 
 def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_step_counter=1, noise_u=None,
-             dr_u=None, margins=None, library=None):
+             dr_u=None, margins=None, library=None, push_u=None):
     """In-place LeggedRobot.step on a logical-layout state dict (see make_state).  ``margins``: optional float64
     [n, 2] array that receives each env's discontinuity margins of this step (lrl_oracle.c g_margin_*): the
     smallest |separation - contact_offset| over its spheres and sub-steps, and the smallest |u_n +
@@ -105,6 +105,8 @@ def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_
     act = np.ascontiguousarray(actions, np.float32)
     nu = np.ascontiguousarray(noise_u, np.float32) if noise_u is not None else None
     du = np.ascontiguousarray(dr_u, np.float32) if dr_u is not None else None
+    pu = np.ascontiguousarray(push_u, np.float32) if push_u is not None else None
+    L.lrlo_set_push_uniforms(pu.ctypes.data_as(C.c_void_p) if pu is not None else None)
     rc = L.lrlo_env_step(C.byref(model), C.byref(params), C.c_int32(n), C.c_int64(env_offset),
                              C.c_uint64(seed), C.c_int64(common_step_counter), C.byref(e),
                              act.ctypes.data_as(C.c_void_p), C.c_uint32(flags),
@@ -112,6 +114,7 @@ def env_step(model, params, state, actions, flags, seed=0, env_offset=0, common_
                              du.ctypes.data_as(C.c_void_p) if du is not None else None)
     if rc != 0:
         raise RuntimeError("oracle env_step failed (non-SPD mass matrix)")
+    L.lrlo_set_push_uniforms(None)
     return state
 
 

@@ -143,6 +143,8 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
   if (m->num_spheres < 0 || m->num_spheres > LRL_MAX_SPHERES) return fail(LRL_E_INVALID, "num_spheres %d", m->num_spheres);
   if (p->num_obs <= 0 || p->num_obs > LRL_MAX_OBS) return fail(LRL_E_INVALID, "num_obs %d", p->num_obs);
   if (p->decimation < 1 || p->sim_dt <= 0.f) return fail(LRL_E_INVALID, "bad timing");
+  if (p->control_type < 0 || p->control_type > 2) return fail(LRL_E_INVALID, "bad control_type %d", p->control_type);
+  if (p->push_robots && p->push_interval < 1) return fail(LRL_E_INVALID, "push_robots with push_interval < 1");
   if (p->num_reward_terms < 0 || p->num_reward_terms > LRL_MAX_REWARD_TERMS) return fail(LRL_E_INVALID, "reward terms");
   for (int t = 0; t < p->num_reward_terms; ++t)
     if (p->reward_term[t] < 0 || p->reward_term[t] >= LRL_R_NUM_TERMS) return fail(LRL_E_INVALID, "reward term id");
@@ -471,10 +473,18 @@ int32_t lrl_sim_inject_uniforms(lrl_sim* s, const float* noise_u, const float* d
   return 0;
 }
 
+int32_t lrl_sim_inject_push_uniforms(lrl_sim* s, const float* u) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  s->S.inj_push = u;
+  return 0;
+}
+
 int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* stream) {
   if (!s || !actions) return fail(LRL_E_INVALID, "null argument");
   if ((flags & LRL_STEP_INJECT_UNIFORM) && (!s->S.inj_noise || !s->S.inj_dr))
     return fail(LRL_E_INVALID, "injected uniforms not set");
+  if ((flags & LRL_STEP_INJECT_UNIFORM) && s->hk.p.push_robots && !s->S.inj_push)
+    return fail(LRL_E_INVALID, "push_robots on but injected push uniforms not set");
   if (s->hk.p.terrain_mesh && !s->hk.terr_vtx) return fail(LRL_E_INVALID, "terrain_mesh set but no lrl_sim_set_terrain");
   s->step_counter += 1;  // common_step_counter (legged_robot.py:153)
   HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, s->hk.p.terrain_mesh,

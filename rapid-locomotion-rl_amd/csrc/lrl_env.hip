@@ -1659,10 +1659,13 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 // post-physics helpers: torch op order, no contraction
 // ------------------------------------------------------------------------------------------------
 #pragma clang fp contract(off)
-__device__ __forceinline__ float pos_target(const lrl_env_params& P, const float* act, int j) {
+__device__ __forceinline__ float act_scaled(const lrl_env_params& P, const float* act, int j) {
   float as = act[j] * P.action_scale;
   if (j % 3 == 0) as = as * P.hip_scale_reduction;  // hip columns 0,3,6,9 (legged_robot.py:666)
-  return as + P.default_dof_pos[j];
+  return as;
+}
+__device__ __forceinline__ float pos_target(const lrl_env_params& P, const float* act, int j) {
+  return act_scaled(P, act, j) + P.default_dof_pos[j];
 }
 __device__ __forceinline__ V3 quat_rotate_inverse(const float* q, V3 v) {
   float w = q[3];
@@ -1854,20 +1857,35 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   LRL_PROF(5)  // kernel start: state loads, setup
   // _compute_torques (legged_robot.py:653-688) for this lane's leg: the gain / strength factors and the
   // position targets do not change over the sub-steps, so they are read once
-  float kp3[3], kd3[3], ms3[3], tg3[3], lim3[3], tau3[3];
+  // 'P': kp3 / kd3 = gains x Kp / Kd factors, tg3 = position target; 'V': kp3 / kd3 = the bare gains, tg3 = the
+  // scaled action (a velocity target), lqd3 = last_dof_vel (constant over the sub-steps: post_physics_step sets it);
+  // 'T': tg3 = the scaled action (a torque)
+  const int ctl = P.control_type;
+  float kp3[3], kd3[3], ms3[3], tg3[3], lim3[3], tau3[3], lqd3[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int jj = 3 * ql + j;
-    kp3[j] = P.p_gains[jj] * S.kp[jj * N + e];
-    kd3[j] = P.d_gains[jj] * S.kd[jj * N + e];
+    const bool pos = ctl == 0;
+    kp3[j] = pos ? P.p_gains[jj] * S.kp[jj * N + e] : P.p_gains[jj];
+    kd3[j] = pos ? P.d_gains[jj] * S.kd[jj * N + e] : P.d_gains[jj];
     ms3[j] = S.motor_strength[jj * N + e];
-    tg3[j] = pos_target(P, act, jj);
+    tg3[j] = pos ? pos_target(P, act, jj) : act_scaled(P, act, jj);
     lim3[j] = P.torque_limits[jj];
+    lqd3[j] = ctl == 1 ? S.last_dof_vel[jj * N + e] : 0.f;
   }
   for (int sub = 0; sub < P.decimation; ++sub) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      float t = kp3[j] * (tg3[j] - st.q[j]) - kd3[j] * st.qd[j];
+      float t;
+      if (ctl == 0) {
+        t = kp3[j] * (tg3[j] - st.q[j]) - kd3[j] * st.qd[j];  // :669-671
+      } else if (ctl == 1) {
+        const float a = kp3[j] * (tg3[j] - st.qd[j]);  // :673-674, torch order: (d * (qd - lqd)) / sim_dt
+        const float b = kd3[j] * (st.qd[j] - lqd3[j]);
+        t = a - b / P.sim_dt;
+      } else {
+        t = tg3[j];  // :676
+      }
       t = t * ms3[j];
       tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
     }
@@ -2047,6 +2065,22 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
     }
   }
+  // _push_robots (legged_robot.py:757-766): after the base-frame velocities above, before the rewards; the pushed
+  // root velocity is what root_states, the next step's physics and last_root_vel see
+  if (P.push_robots && eplen % P.push_interval == 0) {
+    float u0, u1;
+    if (inject) {
+      u0 = valid ? S.inj_push[(size_t)e * 2] : 0.5f;
+      u1 = valid ? S.inj_push[(size_t)e * 2 + 1] : 0.5f;
+    } else {
+      lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter, (LRL_RNG_PUSH << 16) ^ (uint32_t)(step_counter >> 32),
+                               0, S.seed);
+      u0 = lrl_u01(r.v[0]);
+      u1 = lrl_u01(r.v[1]);
+    }
+    st.V[0] = P.push_span * u0 + P.push_lo;  // (upper - lower) * torch.rand + lower
+    st.V[1] = P.push_span * u1 + P.push_lo;
+  }
   if (P.use_terminal_body_height && st.pos[2] < P.terminal_body_height) rst = 1;
   // time-outs (legged_robot.py:196-198, commented out in the fork — Q2): upstream semantics only
   const int tout = (P.auto_reset && eplen > P.max_episode_length) ? 1 : 0;
@@ -2221,7 +2255,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     S.dof_pos[j * N + e] = q12[j];
     S.dof_vel[j * N + e] = qd12[j];
     S.torques[j * N + e] = tau[j];
-    S.joint_pos_target[j * N + e] = pos_target(P, act, j);
+    if (P.control_type == 0) S.joint_pos_target[j * N + e] = pos_target(P, act, j);  // set by 'P' only (:669)
     S.actions[j * N + e] = act[j];
     S.last_actions[j * N + e] = act[j];
     S.last_dof_vel[j * N + e] = qd12[j];

@@ -74,5 +74,6 @@ struct KState {
       *kp, *kd, *env_origins, *base_lin_vel, *base_ang_vel, *projected_gravity, *joint_pos_target;
   float* heights;  // measured_heights [num_height_points][N]
   const float *inj_noise, *inj_dr;
+  const float* inj_push;   // [n][2] injected _push_robots uniforms
   const float* inj_reset;  // [n_ids][5] (motor strength, Kp, Kd, x, y) uniforms of an injected reset_idx
 };

@@ -72,6 +72,7 @@ class LrlEnvParams(C.Structure):
         ("measure_heights", i32), ("num_height_points", i32), ("height_points", f32 * 2 * MAX_HEIGHT_POINTS),
         ("obs_scale_height", f32), ("num_train_envs", i32), ("teleport_x_offset_eval", f32), ("dr_span", f32 * 3),
         ("joint_limits", i32), ("joint_limit_margin", f32), ("self_collisions", i32),
+        ("push_robots", i32), ("push_interval", i32), ("push_lo", f32), ("push_span", f32),
     ]
 
 
@@ -148,7 +149,7 @@ def lib():
                      "lrl_sim_reset_idx_ex", "lrl_sim_observe_idx", "lrl_sim_set_step_counter", "lrl_ppo_forward_backward",
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
                      "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student", "lrl_sim_set_terrain",
-                     "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms"]:
+                     "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms", "lrl_sim_inject_push_uniforms"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_ppo_workspace_bytes.restype = C.c_int64
         L.lrl_ppo_act_workspace_bytes.restype = C.c_int64

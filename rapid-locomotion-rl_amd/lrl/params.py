@@ -23,6 +23,9 @@ def sim_dt(cfg):
     return F32(cfg.sim.dt)  # gymapi.SimParams.dt is a C float
 
 
+CONTROL_TYPES = ("P", "V", "T")  # lrl_env_params.control_type 0 / 1 / 2 (legged_robot.py:667-676)
+
+
 def policy_dt(cfg):
     return cfg.control.decimation * sim_dt(cfg)  # legged_robot.py:1418 (python double of a float32)
 
@@ -153,10 +156,13 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
     if len(hp) > _abi.MAX_HEIGHT_POINTS:
         raise ValueError(f"{len(hp)} height points exceed liblrl's {_abi.MAX_HEIGHT_POINTS}")
     cfg.env.num_height_points = len(hp)
-    if cfg.control.control_type != "P":
-        raise ValueError("only control_type 'P' is implemented")
-    if cfg.domain_rand.push_robots:  # off in config_mini_cheetah / config_go1 (mini_cheetah_config.py:90)
-        raise ValueError("domain_rand.push_robots is not implemented by the fused kernel")
+    ctl = cfg.control.control_type
+    if ctl == "P_compliantfeet":  # legged_robot.py:677-681 indexes DOF 15 of the 12 (spring_idxs = [3, 7, 11, 15])
+        raise IndexError("index 15 is out of bounds for dimension 0 with size 12")
+    if ctl not in CONTROL_TYPES:
+        raise NameError(f"Unknown controller type: {ctl}")  # :682-683
+    dr0 = cfg.domain_rand
+    push_max = float(dr0.max_push_vel_xy)
     nrm = cfg.normalization
     priv = [get_scale_shift(nrm.friction_range), get_scale_shift(nrm.restitution_range),
             get_scale_shift(nrm.added_mass_range), get_scale_shift(nrm.com_displacement_range),
@@ -176,7 +182,7 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         bounce_threshold_velocity=physx.bounce_threshold_velocity, ground_friction=cfg.terrain.static_friction,
         ground_restitution=cfg.terrain.restitution,
         solver_iterations=solver_iterations or physx.num_position_iterations, baumgarte=baumgarte,
-        control_type=0, action_scale=cfg.control.action_scale, hip_scale_reduction=cfg.control.hip_scale_reduction,
+        control_type=CONTROL_TYPES.index(ctl), action_scale=cfg.control.action_scale, hip_scale_reduction=cfg.control.hip_scale_reduction,
         clip_actions=cfg.normalization.clip_actions, p_gains=p_gains, d_gains=d_gains, default_dof_pos=default,
         torque_limits=robot["dof_effort"], soft_dof_pos_lower=soft_lo.tolist(), soft_dof_pos_upper=soft_hi.tolist(),
         dof_vel_limits=robot["dof_velocity"], num_feet=4, feet=feet,
@@ -211,5 +217,8 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         dr_span=[float(r[1]) - float(r[0]) for r in (dr.motor_strength_range, dr.Kp_factor_range, dr.Kd_factor_range)],
         joint_limits=int(joint_limits), joint_limit_margin=joint_limit_margin,
         self_collisions=int(cfg.asset.self_collisions == 0 if self_collisions is None else self_collisions),
+        # torch_rand_float(-max, max, (k, 2)) = (max - -max) * torch.rand + -max (legged_robot.py:763-764)
+        push_robots=int(bool(dr0.push_robots)), push_interval=int(cfg.domain_rand.push_interval),
+        push_lo=-push_max, push_span=push_max - (-push_max),
     )
     return P

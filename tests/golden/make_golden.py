@@ -305,11 +305,26 @@ def _all_terms_tweak(cfg):
     cfg.rewards.only_positive_rewards = False
 
 
+def _control_tweak(ctl, push):
+    """control_type 'V' / 'T' (legged_robot.py:672-676) and _push_robots every 5 policy steps (push_interval_s 0.1 at
+    dt 0.02, max_push_vel_xy 0.5 as the presets' value; :757-766)"""
+    def tweak(cfg):
+        cfg.control.control_type = ctl
+        if ctl == "V":  # gains of a velocity loop, so that few torques saturate at the 33.5 N m limit
+            cfg.control.stiffness = {"joint": 2.0}
+            cfg.control.damping = {"joint": 0.002}
+        if push:
+            cfg.domain_rand.push_robots = True
+            cfg.domain_rand.push_interval_s = 0.1
+            cfg.domain_rand.max_push_vel_xy = 0.5
+    return tweak
+
+
 def gen_post_physics(robot, n=16, steps=3, seed=7, tweak=None, name=None):
     env, rng = make_env(robot, n, seed, tweak)
     B = env.num_bodies
     rec = {k: [] for k in [
-        "root_in", "dof_pos_in", "dof_vel_in", "contact_in", "actions", "commands", "noise_u", "ms_u",
+        "root_in", "dof_pos_in", "dof_vel_in", "contact_in", "actions", "commands", "noise_u", "ms_u", "push_u",
         "obs", "priv", "rew", "reset", "torques", "root_out", "motor_strengths", "episode_sums",
         "command_sums", "feet_air_time", "last_contacts", "episode_length", "base_lin_vel",
         "base_ang_vel", "projected_gravity", "joint_pos_target"]}
@@ -381,11 +396,19 @@ def gen_post_physics(robot, n=16, steps=3, seed=7, tweak=None, name=None):
         with InjectRand(noise_u, ms_rng) as inj:
             obs, priv, rew, reset, extras = env.step(torch.tensor(actions))
         ms_u = np.full(n, np.nan, np.float32)
+        push_u = np.full((n, 2), np.nan, np.float32)
         redraw = np.nonzero((env.episode_length_buf.numpy() % int(env.cfg.domain_rand.rand_interval)) == 0)[0]
-        if len(inj.ms_draws):
-            ms_u[redraw] = inj.ms_draws[0].numpy()
+        # torch.rand draws of this step in call order: _push_robots' (k, 2) (legged_robot.py:763-764), then the
+        # motor-strength redraw's (k,) (:547)
+        dr_draws = [d for d in inj.ms_draws if d.dim() == 1]
+        for d in inj.ms_draws:
+            if d.dim() == 2:
+                pushed = np.nonzero((env.episode_length_buf.numpy() % int(env.cfg.domain_rand.push_interval)) == 0)[0]
+                push_u[pushed] = d.numpy()
+        if len(dr_draws):
+            ms_u[redraw] = dr_draws[0].numpy()
         for k, v in dict(root_in=root, dof_pos_in=dof_pos, dof_vel_in=dof_vel, contact_in=contact,
-                         actions=actions, commands=commands, noise_u=noise_u.numpy(), ms_u=ms_u,
+                         actions=actions, commands=commands, noise_u=noise_u.numpy(), ms_u=ms_u, push_u=push_u,
                          obs=obs.numpy(), priv=priv.numpy(), rew=rew.numpy(),
                          reset=reset.numpy().astype(np.uint8), torques=env.torques.numpy(),
                          root_out=env.root_states.numpy(), motor_strengths=env.motor_strengths.numpy(),
@@ -395,7 +418,8 @@ def gen_post_physics(robot, n=16, steps=3, seed=7, tweak=None, name=None):
                          episode_length=env.episode_length_buf.numpy(),
                          base_lin_vel=env.base_lin_vel.numpy(), base_ang_vel=env.base_ang_vel.numpy(),
                          projected_gravity=env.projected_gravity.numpy(),
-                         joint_pos_target=env.joint_pos_target.numpy()).items():
+                         # set by 'P' control only (:669); 'V' / 'T' never create it: our buffer stays zero
+                         joint_pos_target=getattr(env, "joint_pos_target", torch.zeros(n, 12)).numpy()).items():
             rec[k].append(np.array(v, copy=True))
     out = {k: np.stack(v) for k, v in rec.items()}
     out.update({"init_" + k: v for k, v in init.items()})
@@ -896,6 +920,10 @@ if __name__ == "__main__":
                 curriculum=gen_curriculum, gae=gen_gae, ppo=gen_ppo, checkpoint=gen_checkpoint, terrain=gen_terrain,
                 heights=gen_heights, terrain_curriculum=gen_terrain_curriculum, high_level=gen_high_level,
                 reset=gen_reset,
+                post_physics_ctl_v_push=lambda: gen_post_physics("go1", tweak=_control_tweak("V", True), seed=21,
+                                                                 name="post_physics_ctl_v_push.npz"),
+                post_physics_ctl_t=lambda: gen_post_physics("mc", tweak=_control_tweak("T", False), seed=23,
+                                                            name="post_physics_ctl_t.npz"),
                 post_physics_all_terms=lambda: gen_post_physics("mc", tweak=_all_terms_tweak, seed=9,
                                                                 name="post_physics_all_terms.npz"))
     for name in (sys.argv[1:] or list(gens)):

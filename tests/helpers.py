@@ -60,7 +60,14 @@ ALL_TERMS = {"rewards.scales.energy": -1e-3, "rewards.scales.energy_expenditure"
 # (robot, fixture, cfg overrides): the presets' 12 terms for both robots, and Mini Cheetah with every _reward_* term
 # of legged_robot.py:1506-1646 plus termination at a non-zero scale (make_golden.py ALL_TERMS, in that key order)
 POST_PHYSICS = {"mc": ("mc", "post_physics_mc.npz", {}), "go1": ("go1", "post_physics_go1.npz", {}),
-                "all_terms": ("mc", "post_physics_all_terms.npz", ALL_TERMS)}
+                "all_terms": ("mc", "post_physics_all_terms.npz", ALL_TERMS),
+                # control_type 'V' + _push_robots every 5 steps (Go1), control_type 'T' (Mini Cheetah):
+                # make_golden.py _control_tweak
+                "ctl_v_push": ("go1", "post_physics_ctl_v_push.npz",
+                               {"control.control_type": "V", "control.stiffness": {"joint": 2.0},
+                                "control.damping": {"joint": 0.002}, "domain_rand.push_robots": True,
+                                "domain_rand.push_interval_s": 0.1, "domain_rand.max_push_vel_xy": 0.5}),
+                "ctl_t": ("mc", "post_physics_ctl_t.npz", {"control.control_type": "T"})}
 
 
 def golden(name):

@@ -61,7 +61,8 @@ def test_oracle_post_physics_matches_reference(case):
         st["dof_vel"][:] = g["dof_vel_in"][s]
         st["contact"][:] = g["contact_in"][s]
         st["commands"][:] = g["commands"][s]
-        oracle.env_step(M, P, st, g["actions"][s], flags, noise_u=g["noise_u"][s], dr_u=g["ms_u"][s])
+        push_u = np.nan_to_num(g["push_u"][s]) if "push_u" in g.files else None
+        oracle.env_step(M, P, st, g["actions"][s], flags, noise_u=g["noise_u"][s], dr_u=g["ms_u"][s], push_u=push_u)
         tight = dict(rtol=2e-6, atol=2e-6)
         np.testing.assert_array_equal(st["torques"], g["torques"][s])
         np.testing.assert_array_equal(st["joint_pos_target"], g["joint_pos_target"][s])
