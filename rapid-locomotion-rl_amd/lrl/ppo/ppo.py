@@ -67,6 +67,7 @@ class PPO:
         self.grad_allreduce = _world() > 1
         self._native = None  # flat grads / Adam moments / ctrl / workspace of the native update
         self.record_lr = False  # native path: keep the per-minibatch learning rates (self.lr_trace)
+        self.overlap_adaptation = True  # native path: adaptation phases on a second stream (see _update_native)
         self.lr_trace = []
         if self.fused:
             self.actor_critic.flatten_parameters()
@@ -168,6 +169,8 @@ class PPO:
             if nbytes < 0:
                 raise RuntimeError("lrl_ppo_workspace_bytes rejected the network")
             st["ws"] = torch.empty(nbytes, dtype=torch.uint8, device=ac._flat.device)
+            # the adaptation phases run on their own stream with their own workspace (see _update_native)
+            st["ws_b"] = torch.empty(nbytes, dtype=torch.uint8, device=ac._flat.device)
             st["ws_batch"] = batch
         return st
 
@@ -203,6 +206,24 @@ class PPO:
         main = grads[net.main_begin:net.kl_slot + 1]
         adapt = grads[net.adapt_begin:net.adapt_end]
         scale = 1.0 / world
+        # The adaptation-module regression of minibatch i (phases 3 / 4) reads the encoder weights phase 2 of i wrote
+        # and touches only the adaptation module's parameters, gradients and Adam moments, which phases 1 / 2 never
+        # read or write.  So it runs on a second stream, overlapping phases 1 / 2 of minibatch i + 1 (the GEMM tails
+        # and small launches of one chain leave the CUs the other fills); phase 2 of i + 1 waits for it, since it
+        # overwrites the encoder weights phase 3 of i reads.  Each chain keeps its own launch order, so the result is
+        # bit-identical to the sequential order of ppo.py:94-178.
+        cur = torch.cuda.current_stream(params.device)
+        if self.overlap_adaptation:
+            sb = st.get("stream_b")
+            if sb is None:
+                sb = st["stream_b"] = torch.cuda.Stream(params.device)
+            stream_b, ws_b = C.c_void_p(sb.cuda_stream), st["ws_b"]
+        else:
+            sb, stream_b, ws_b = cur, stream, ws
+        # the adaptation chain's batch descriptor: the rows pointer of minibatch i must outlive the next C call
+        batch_b = _abi.LrlPpoBatch()
+        C.memmove(C.byref(batch_b), C.byref(batch), C.sizeof(batch))
+        adapt_done = None
         for epoch in range(PPO_Args.num_learning_epochs):
             for i in range(nmb):
                 rows = indices[i * mb:(i + 1) * mb]
@@ -211,22 +232,34 @@ class PPO:
                                                       C.byref(hp), ptr(ws), ptr(ctrl), stream))
                 if world > 1:
                     dist.all_reduce(main)
+                if adapt_done is not None:
+                    cur.wait_event(adapt_done)
                 st["steps"][0] += 1
                 _abi.check(L.lrl_ppo_optimizer_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
                                                     C.c_int64(st["steps"][0]), C.c_float(scale), C.byref(hp),
                                                     ptr(ws), ptr(ctrl), stream))
                 if self.record_lr:
                     trace.append(ctrl[0].clone())
+                if sb is not cur:
+                    sb.wait_stream(cur)
+                batch_b.rows = rows.data_ptr()
                 for _ in range(PPO_Args.num_adaptation_module_substeps):
                     _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), ptr(params), ptr(grads),
-                                                                     C.byref(batch), ptr(ws), ptr(ctrl), stream))
+                                                                     C.byref(batch_b), ptr(ws_b), ptr(ctrl), stream_b))
                     if world > 1:
-                        dist.all_reduce(adapt)
+                        with torch.cuda.stream(sb):
+                            dist.all_reduce(adapt)
                     st["steps"][1] += 1
                     _abi.check(L.lrl_ppo_adaptation_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
                                                          C.c_int64(st["steps"][1]),
                                                          C.c_double(PPO_Args.adaptation_module_learning_rate),
-                                                         C.c_float(scale), C.byref(hp), ptr(ctrl), stream))
+                                                         C.c_float(scale), C.byref(hp), ptr(ctrl), stream_b))
+                if sb is not cur:
+                    adapt_done = torch.cuda.Event()
+                    adapt_done.record(sb)
+        if sb is not cur:
+            cur.wait_stream(sb)
+            indices.record_stream(sb)
         num_updates = PPO_Args.num_learning_epochs * nmb
         lr, vsum, ssum, asum = ctrl[:4].tolist()
         if self.record_lr:

@@ -28,12 +28,12 @@ L = _abi.lib()
 buf = (C.c_ulonglong * 16)()
 g = torch.Generator(device="cuda:0").manual_seed(0)
 for _ in range(50):
-    env.step(0.5 * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
+    env.step(float(os.environ.get("LRL_ASTD", "0.5")) * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
 torch.cuda.synchronize()
 L.lrl_debug_env_profile(buf, 1)
 K = 100
 for _ in range(K):
-    env.step(0.5 * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
+    env.step(float(os.environ.get("LRL_ASTD", "0.5")) * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
 torch.cuda.synchronize()
 assert L.lrl_debug_env_profile(buf, 0) == 16, "library built without LRL_ENV_PROFILE"
 waves = (n + 15) // 16  # quad layout: 16 envs per wave

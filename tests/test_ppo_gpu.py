@@ -176,6 +176,43 @@ def test_native_update_matches_torch_autograd(N, T):
         assert d <= 2e-3 * (v.detach().abs().max().item() + 1e-2), (k, d)
 
 
+def test_overlapped_adaptation_phases_are_bit_identical():
+    """The native update runs the adaptation-module regression (phases 3 / 4) of minibatch i on a second stream,
+    overlapping phases 1 / 2 of minibatch i + 1 (ppo.py _update_native); each chain keeps its launch order, so every
+    parameter, Adam moment, learning rate and loss equals the sequential single-stream update bit for bit — at the
+    benchmark's minibatch (4096 envs x 24 steps / 4)."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.ppo import PPO
+    N, T = 4096, 24
+    algs = []
+    for overlap in (True, False):
+        torch.manual_seed(0)
+        ac = ActorCritic(42, 18, 630, 12)
+        init_params(ac)
+        alg = PPO(ac.cuda(), device="cuda:0", fused=True)
+        alg.overlap_adaptation = overlap
+        alg.init_storage(N, T, [42], [18], [630], [12])
+        algs.append(alg)
+    perm = torch.randperm(N * T, device="cuda:0")
+    orig = torch.randperm
+    torch.randperm = lambda n, **kw: perm
+    try:
+        outs = []
+        for alg in algs:
+            o = []
+            for it in range(2):  # two iterations: the second starts from Adam state the first left
+                _random_storage(alg, N, T, seed=1 + it)
+                o.append(alg.update())
+            outs.append(o)
+    finally:
+        torch.randperm = orig
+    assert outs[0] == outs[1]
+    assert algs[0].learning_rate == algs[1].learning_rate
+    assert torch.equal(algs[0].actor_critic._flat, algs[1].actor_critic._flat)
+    for k in ("exp_avg", "exp_avg_sq"):
+        assert torch.equal(algs[0]._native[k], algs[1]._native[k]), k
+
+
 def _random_storage(alg, N, T, seed=1):
     st = alg.storage
     g = torch.Generator(device="cuda:0").manual_seed(seed)
