@@ -219,15 +219,19 @@ __global__ void rigid_body_kernel(const KParams* __restrict__ K, KState S, const
 // HistoryWrapper.get_observations shift: hist = cat(hist[:, NO:], obs)  (history_wrapper.py:26-30)
 // HistoryWrapper history shift outside the step (get_observations, Q6): one workgroup per env row, the row
 // staged through LDS so every load and store is coalesced
-__global__ void shift_history_kernel(KState S, int NO, int H) {
+// append 0: the first H - NO floats only (hist[:, :H-NO] = hist[:, NO:]) — the shift half of the HistoryWrapper.step
+// update, launched by lrl_sim_step before the env kernel, which then writes the newest slot from its obs tile (a
+// bandwidth-shaped launch of 4096 workgroups instead of a latency-bound pass in the env kernel's single waves)
+__global__ void shift_history_kernel(KState S, int NO, int H, int append) {
   extern __shared__ float row[];
   const int e = blockIdx.x;
   if (e >= S.n) return;
   float* h = S.hist + (size_t)e * H;
   const float* o = S.obs + (size_t)e * NO;
-  for (int k = threadIdx.x; k < H; k += blockDim.x) row[k] = k < H - NO ? h[k + NO] : o[k - (H - NO)];
+  const int W = append ? H : H - NO;
+  for (int k = threadIdx.x; k < W; k += blockDim.x) row[k] = k < H - NO ? h[k + NO] : o[k - (H - NO)];
   __syncthreads();
-  for (int k = threadIdx.x; k < H; k += blockDim.x) h[k] = row[k];
+  for (int k = threadIdx.x; k < W; k += blockDim.x) h[k] = row[k];
 }
 
 // _randomize_rigid_body_props (legged_robot.py:519-542) for all envs
@@ -282,8 +286,8 @@ hipError_t lrl_launch_rigid_body(const KParams* K, const KState* S, const int32_
                      foot_xyz);
   return hipGetLastError();
 }
-hipError_t lrl_launch_shift_history(const KState* S, int NO, int H, hipStream_t st) {
-  hipLaunchKernelGGL(lrl::shift_history_kernel, dim3(S->n), dim3(128), H * sizeof(float), st, *S, NO, H);
+hipError_t lrl_launch_shift_history(const KState* S, int NO, int H, int append, hipStream_t st) {
+  hipLaunchKernelGGL(lrl::shift_history_kernel, dim3(S->n), dim3(128), H * sizeof(float), st, *S, NO, H, append);
   return hipGetLastError();
 }
 hipError_t lrl_launch_randomize(const KState* S, const float* fr, const float* rr, const float* pr, const float* cr,

@@ -40,7 +40,7 @@ hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t,
 hipError_t lrl_launch_set_dof(const KState*, const float*, const float*, const int32_t*, int32_t, hipStream_t);
 hipError_t lrl_launch_rigid_body(const KParams*, const KState*, const int32_t*, const int32_t*, const float*,
                                  hipStream_t);
-hipError_t lrl_launch_shift_history(const KState*, int, int, hipStream_t);
+hipError_t lrl_launch_shift_history(const KState*, int, int, int, hipStream_t);
 hipError_t lrl_launch_randomize(const KState*, const float*, const float*, const float*, const float*, uint32_t,
                                 hipStream_t);
 }
@@ -487,6 +487,9 @@ int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* str
     return fail(LRL_E_INVALID, "push_robots on but injected push uniforms not set");
   if (s->hk.p.terrain_mesh && !s->hk.terr_vtx) return fail(LRL_E_INVALID, "terrain_mesh set but no lrl_sim_set_terrain");
   s->step_counter += 1;  // common_step_counter (legged_robot.py:153)
+  if (flags & LRL_STEP_HISTORY)  // HistoryWrapper.step's shift; the env kernel appends the step's obs row
+    HIPCHECK(lrl_launch_shift_history(&s->S, s->hk.p.num_obs, s->hk.p.num_history * s->hk.p.num_obs, 0,
+                                      (hipStream_t)stream));
   HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, s->hk.p.terrain_mesh,
                                (hipStream_t)stream));
   return 0;
@@ -560,7 +563,7 @@ int32_t lrl_sim_refresh_rigid_body_state(lrl_sim* s, void* stream) {
 
 int32_t lrl_sim_shift_history(lrl_sim* s, void* stream) {
   if (!s) return fail(LRL_E_INVALID, "null sim");
-  HIPCHECK(lrl_launch_shift_history(&s->S, s->hk.p.num_obs, s->hk.p.num_history * s->hk.p.num_obs,
+  HIPCHECK(lrl_launch_shift_history(&s->S, s->hk.p.num_obs, s->hk.p.num_history * s->hk.p.num_obs, 1,
                                     (hipStream_t)stream));
   return 0;
 }

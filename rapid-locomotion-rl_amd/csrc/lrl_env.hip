@@ -2293,45 +2293,13 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     for (int i = lane; i < ENVS * LRL_NUM_PRIV; i += BLOCK) pgp[i] = ptile[i];
   }
   if (flags & LRL_STEP_HISTORY) {
+    // HistoryWrapper.step (history_wrapper.py:17-21): lrl_sim_step launched the shift of the older slots before this
+    // kernel (shift_history_kernel, append 0); the newest slot is this step's obs row, from the tile
     const int H = K->num_history * NO;
-    // in place: new[r][k] = old[r][k + NO] (k < H - NO) else obs[r][k - (H - NO)].  The wave's 16 rows are
-    // contiguous; a pass covers HCW 64-wide column blocks of every row (8-B pairs), all its loads before any
-    // of its stores, and passes run left to right, so a pass only reads pairs no earlier pass has written.
-    if (((H | NO) & 1) == 0) {
-      const int H2 = H >> 1, S2 = (H - NO) >> 1, NO2 = NO >> 1;
-      float2* hg2 = reinterpret_cast<float2*>(S.hist + row0 * H);
-      const float2* ot2 = reinterpret_cast<const float2*>(otile);
-      // HCW column blocks per pass: HCW x 16 pairs per lane in flight (the physics registers are dead here), so
-      // the 630-float history takes 2 passes instead of 5 (each pass pays one HBM round trip)
-      constexpr int HCW = 3;
-      for (int c0 = 0; c0 < H2; c0 += HCW * BLOCK) {
-        float2 v[HCW][ENVS];
-#pragma unroll
-        for (int w = 0; w < HCW; ++w) {
-          const int k2 = c0 + w * BLOCK + lane;
-#pragma unroll
-          for (int r = 0; r < ENVS; ++r)
-            if (k2 < H2) v[w][r] = k2 < S2 ? hg2[r * H2 + k2 + NO2] : ot2[r * NO2 + (k2 - S2)];
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int w = 0; w < HCW; ++w) {
-          const int k2 = c0 + w * BLOCK + lane;
-#pragma unroll
-          for (int r = 0; r < ENVS; ++r)
-            if (k2 < H2) hg2[r * H2 + k2] = v[w][r];
-        }
-      }
-    } else {
-      float* hg = S.hist + row0 * H;
-      for (int i0 = 0; i0 < ENVS * H; i0 += BLOCK) {
-        const int i = i0 + lane;
-        const int r = i / H, k = i - r * H;
-        float v = 0.f;
-        if (i < ENVS * H) v = (k < H - NO) ? hg[i + NO] : otile[r * NO + (k - (H - NO))];
-        __builtin_amdgcn_wave_barrier();
-        if (i < ENVS * H) hg[i] = v;
-      }
+    float* hg = S.hist + row0 * H + (H - NO);
+    for (int i = lane; i < ENVS * NO; i += BLOCK) {
+      const int r = i / NO, c = i - r * NO;
+      hg[(size_t)r * H + c] = otile[i];
     }
   }
   LRL_PROF(7)  // obs / priv tiles + history shift
