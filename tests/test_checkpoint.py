@@ -78,3 +78,25 @@ def test_trained_policy_walks_in_this_physics():
     vx = vel[150:, :, 0].mean()
     assert 0.75 < vx < 1.1, vx
     assert upright >= 0.95, upright
+
+
+def test_runner_save_torchscript_export_reproduces_student(tmp_path):
+    """Runner.save (mini_gym_learn/ppo/__init__.py:220-242): the state dict plus TorchScript exports of the
+    adaptation module and the actor body, the pair the reference's deployment loads (play scripts: latent =
+    adaptation_module(history), action = body(cat(obs, latent))).  Reloaded from disk, the exports of the trained
+    checkpoint reproduce the reference's student means."""
+    import types
+    from lrl.ppo.runner import Logger, Runner
+    ac, g = _trained()
+    fake = types.SimpleNamespace(logger=Logger(str(tmp_path)), alg=types.SimpleNamespace(actor_critic=ac))
+    Runner.save(fake, 7)
+    ck = tmp_path / "checkpoints"
+    assert (ck / "ac_weights_000007.pt").exists() and (ck / "ac_weights_last.pt").exists()
+    sd = torch.load(ck / "ac_weights_last.pt", weights_only=True)
+    assert list(sd) == list(ac.state_dict())
+    adapt = torch.jit.load(str(ck / "adaptation_module_latest.jit"))
+    body = torch.jit.load(str(ck / "body_latest.jit"))
+    obs, hist = torch.from_numpy(g["obs"]), torch.from_numpy(g["hist"])
+    with torch.no_grad():
+        mean = body(torch.cat((obs, adapt(hist)), dim=-1))
+    np.testing.assert_allclose(mean.numpy(), g["mean_student"], rtol=1e-5, atol=1e-5)
