@@ -43,6 +43,16 @@ def pmc_traffic(*kernels):
     return None, None
 
 
+def env_kernel_timing(env, start):
+    """HIP events around each env-kernel launch of lrl_sim_step, on its launch stream (lrl_sim_timing; the history
+    shift launched before it is outside): start=True begins recording, start=False stops and returns the mean ms."""
+    import ctypes as C
+    from lrl import _abi
+    ms, n = C.c_double(0.0), C.c_int64(0)
+    _abi.check(_abi.lib().lrl_sim_timing(env._sim, C.c_int32(1 if start else 0), C.byref(ms), C.byref(n)))
+    return ms.value / n.value if n.value else float("nan")
+
+
 def _cpu_info():
     """(threads this process may use, CPU model) — the GPU box's CPU share is its OMP_NUM_THREADS (16), nproc shows
     the whole machine."""
@@ -123,15 +133,13 @@ def bench_go1_rough(dev, iters=3, warmup=1):
     env = HistoryWrapper(LeggedRobotEnv(dev, cfg=cfg, seed=4321, legacy_fork=False))
     runner = R.Runner(env, device=dev, seed=4321)
     runner.learn(warmup, init_at_random_ep_len=True)
-    timer = []
-    env.env.kernel_timer = timer
     torch.cuda.synchronize()
+    env_kernel_timing(env.env, True)
     t0 = time.perf_counter()
     runner.learn(iters)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    env.env.kernel_timer = None
-    k_ms = float(np.mean([a.elapsed_time(b) for a, b in timer]))
+    k_ms = env_kernel_timing(env.env, False)
     out = {"workload": "4096 Go1 envs, trimesh rough terrain (curriculum tiles) + terrain curriculum + upstream resets "
                        "with the grid-adaptive command curriculum (BASELINE configs[2])",
            "env_steps_per_s": round(ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env * iters / dt, 1),
@@ -257,11 +265,10 @@ def main():
     env.env.commands[:, 2] = cmd[:, 2] * 2.0 - 1.0
     runner = R.Runner(env, device=dev, seed=1234)
     runner.learn(args.warmup, init_at_random_ep_len=True)
-    timer = []
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    env.env.kernel_timer = timer
+    env_kernel_timing(env.env, True)
     import ctypes as C
     from lrl import _abi
     _abi.check(_abi.lib().lrl_ppo_timing(1, None, None))  # events around the update's largest GEMM
@@ -273,12 +280,11 @@ def main():
     _abi.check(_abi.lib().lrl_ppo_timing(0, C.byref(g_ms), C.byref(g_n)))
     if world > 1:
         dist.barrier()
-    env.env.kernel_timer = None
+    k_ms = env_kernel_timing(env.env, False)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    k_ms = float(np.mean([a.elapsed_time(b) for a, b in timer]))
     # env-only rate: the fused step kernel alone, random actions, same env
     a = torch.randn(ENVS_PER_GPU, 12, device=dev) * 0.3
     for _ in range(10):
@@ -326,9 +332,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel<false> (plane ground)", "achieved": round(achieved, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
-                         "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (the fused history "
-                                 f"shift adds 4872 B/env-step = {4872 * ENVS_PER_GPU} B per launch); the kernel is "
-                                 "latency-bound (4 lanes per env, one single-wave workgroup per 16 envs), see DESIGN.md"},
+                         "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (+ the newest history "
+                                 f"slot, 168 B/env-step; the older slots move in the separate shift_history_kernel launch "
+                                 "before it); the kernel is latency-bound (4 lanes per env, one single-wave workgroup "
+                                 "per 16 envs, the slowest wave sets the launch), see DESIGN.md"},
             "roofline_update_gemm": {
                 "bound": "mfma", "kernel": f"{gemm_kernel} (dW2: 2 x 256x512, {mb_rows} rows)",
                 "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": MFMA_F32_PEAK_TF,

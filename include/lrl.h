@@ -266,6 +266,12 @@ int32_t lrl_sim_randomize(lrl_sim* sim, const float* friction_range, const float
 /* One policy step for all envs: the fused LeggedRobot.step hot path. `actions` [N,12] f32 device. */
 int32_t lrl_sim_step(lrl_sim* sim, const float* actions, uint32_t flags, void* stream);
 
+/* Launch timing of the fused env kernel (bench.py roofline): enable = 1 starts recording HIP events around each
+ * env-kernel launch of lrl_sim_step on its stream (the history-shift launch before it is outside); the next call
+ * returns the summed milliseconds and the launch count of the recorded launches (waiting for them) and
+ * restarts (enable = 1) or stops (enable = 0) recording. */
+int32_t lrl_sim_timing(lrl_sim* sim, int32_t enable, double* total_ms, int64_t* launches);
+
 /* Injected uniforms for parity tests: noise_u [N,num_obs], dr_u [N] (NaN = no redraw). */
 int32_t lrl_sim_inject_uniforms(lrl_sim* sim, const float* noise_u, const float* dr_u);
 /* Injected push uniforms for parity tests: u [N,2] f32 device, row e = env e's (x, y) draw of _push_robots when it is

@@ -60,6 +60,10 @@ struct lrl_sim {
   int32_t* d_body_link = nullptr;
   float* d_foot_xyz = nullptr;
   void* terr = nullptr;  // terrain mesh buffers (lrl_sim_set_terrain)
+  // lrl_sim_timing: HIP events around each env-kernel launch of lrl_sim_step (not the history-shift launch before it)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t ev_used = 0;
 };
 
 static void quat_to_rowmajor(const float* q, float* R) {
@@ -456,6 +460,10 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->d_body_link);
   (void)hipFree(s->d_foot_xyz);
   (void)hipFree(s->terr);
+  for (auto& pr : s->ev) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
   delete s;
   return 0;
 }
@@ -490,8 +498,38 @@ int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* str
   if (flags & LRL_STEP_HISTORY)  // HistoryWrapper.step's shift; the env kernel appends the step's obs row
     HIPCHECK(lrl_launch_shift_history(&s->S, s->hk.p.num_obs, s->hk.p.num_history * s->hk.p.num_obs, 0,
                                       (hipStream_t)stream));
+  std::pair<hipEvent_t, hipEvent_t>* tp = nullptr;
+  if (s->timing) {
+    if (s->ev_used == s->ev.size()) {
+      hipEvent_t a = nullptr, b = nullptr;
+      HIPCHECK(hipEventCreate(&a));
+      HIPCHECK(hipEventCreate(&b));
+      s->ev.emplace_back(a, b);
+    }
+    tp = &s->ev[s->ev_used++];
+    HIPCHECK(hipEventRecord(tp->first, (hipStream_t)stream));
+  }
   HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, s->hk.p.terrain_mesh,
                                (hipStream_t)stream));
+  if (tp) HIPCHECK(hipEventRecord(tp->second, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_timing(lrl_sim* s, int32_t enable, double* total_ms, int64_t* launches) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  if (total_ms) {
+    double t = 0.0;
+    for (size_t i = 0; i < s->ev_used; ++i) {
+      float ms = 0.f;
+      HIPCHECK(hipEventSynchronize(s->ev[i].second));
+      HIPCHECK(hipEventElapsedTime(&ms, s->ev[i].first, s->ev[i].second));
+      t += ms;
+    }
+    *total_ms = t;
+  }
+  if (launches) *launches = (int64_t)s->ev_used;
+  s->ev_used = 0;
+  s->timing = enable != 0;
   return 0;
 }
 
