@@ -167,8 +167,9 @@ def _self_states(rng, n, M, root, dof):
     return root, dof
 
 
-def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True):
+def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True, extra=None):
     over = {} if self_on else {"asset.self_collisions": 1}
+    over.update(extra or {})
     cfg, rob, M, P = make(robot, **{"env.num_envs": n}, **over)
     env = _env(robot, n, **over)
     assert P.self_collisions == int(self_on) and env._P.self_collisions == int(self_on)  # presets: asset.self_collisions 0
@@ -212,11 +213,16 @@ def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True)
             act = np.where(picked, act_lim, act).astype(np.float32)
         noise = rng.random((n, P.num_obs)).astype(np.float32)
         dr = rng.random(n).astype(np.float32)
+        pu = None
+        if P.push_robots:  # _push_robots draws of the envs pushed in this step (both sides read the same rows)
+            pu = rng.random((n, 2)).astype(np.float32)
+            env._inj_push = _dev(pu)
+            _abi.check(_abi.lib().lrl_sim_inject_push_uniforms(env._sim, C.c_void_p(env._inj_push.data_ptr())))
         _step_raw(env, _dev(act), flags, _dev(noise), _dev(dr))
         m = np.zeros((n, 2))
-        oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr, common_step_counter=s + 1, margins=m)
+        oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr, common_step_counter=s + 1, margins=m, push_u=pu)
         for i in range(len(st_p)):
-            oracle.env_step(M, P, st_p[i], act, flags, noise_u=noise, dr_u=dr, common_step_counter=s + 1)
+            oracle.env_step(M, P, st_p[i], act, flags, noise_u=noise, dr_u=dr, common_step_counter=s + 1, push_u=pu)
             if s + 1 < steps:
                 st_p[i] = perturb_state(st_p[i], rng_p[i])
         margins = np.minimum(margins, m)
@@ -257,6 +263,18 @@ def test_physics_matches_oracle(robot, n, steps):
     tolerances of helpers.physics_mismatch except the envs the oracle reports on a contact-model discontinuity
     (counted and bounded)."""
     _physics_vs_oracle(robot, n, steps)
+
+
+@pytest.mark.parametrize("robot,ctl,steps", [("go1", "V", 1), ("go1", "V", 3), ("mc", "T", 1), ("mc", "T", 3)])
+def test_control_types_and_pushes_match_oracle(robot, ctl, steps):
+    """Velocity ('V') and torque ('T') control (legged_robot.py:672-676) through the physics, with _push_robots
+    (:757-766) every step (push_interval_s = dt): the pushed root velocities enter the next step's dynamics.  Kernel
+    and oracle agree within the physics tolerances (every env outside the oracle's discontinuity margins)."""
+    extra = {"control.control_type": ctl, "domain_rand.push_robots": True, "domain_rand.push_interval_s": 0.02,
+             "domain_rand.max_push_vel_xy": 0.5}
+    if ctl == "V":  # velocity-loop gains (the presets' position gains saturate every joint in 'V')
+        extra.update({"control.stiffness": {"joint": 2.0}, "control.damping": {"joint": 0.002}})
+    _physics_vs_oracle(robot, 128, steps, extra=extra)
 
 
 @pytest.mark.parametrize("robot,steps", [("mc", 1), ("go1", 1), ("mc", 10), ("go1", 10)])
