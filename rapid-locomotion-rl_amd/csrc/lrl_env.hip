@@ -812,6 +812,11 @@ __device__ __forceinline__ SphLegs sph_legs(const KParams* __restrict__ K) {
   }
   return r;
 }
+// L.b[l] / L.e[l] for a lane-varying l as masked ORs: a select chain over l is turned into a lookup table in a private
+// (scratch) array by the compiler
+__device__ __forceinline__ int sel4(const int* v, int l) {
+  return (v[0] & -(int)(l == 0)) | (v[1] & -(int)(l == 1)) | (v[2] & -(int)(l == 2)) | (v[3] & -(int)(l == 3));
+}
 __device__ __forceinline__ int sph_leg_of(const SphLegs& L, int s) {
   int l = -1;
 #pragma unroll
@@ -938,8 +943,8 @@ struct SelfGate {
 };
 __device__ __forceinline__ SelfGate self_gate(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, int ql,
                                               float co) {
-  const int b = ql == 0 ? SL.b[0] : ql == 1 ? SL.b[1] : ql == 2 ? SL.b[2] : SL.b[3];
-  const int e = ql == 0 ? SL.e[0] : ql == 1 ? SL.e[1] : ql == 2 ? SL.e[2] : SL.e[3];
+  const int b = sel4(SL.b, ql);
+  const int e = sel4(SL.e, ql);
   const int kmax = __builtin_amdgcn_readfirstlane(K->self_kmax);  // (wave-uniform loop bound)
   const int nhip = K->self_nhip[ql];
   float cx[8], cy[8], cz[8], r[8];
@@ -1325,8 +1330,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       const V3 c = o + mul(Rj, v3(kl.com[j][0], kl.com[j][1], kl.com[j][2]));
       Ij[j] = make_si(kl.mass[j], c, Rj, kl.inertia[j]);
       // contact detection for this link's spheres (needs only a_j', o_j' for j' <= j, already in LDS)
-      const int sb = l == 0 ? SL.b[0] : l == 1 ? SL.b[1] : l == 2 ? SL.b[2] : SL.b[3];
-      const int se = l == 0 ? SL.e[0] : l == 1 ? SL.e[1] : l == 2 ? SL.e[2] : SL.e[3];
+      const int sb = sel4(SL.b, l);
+      const int se = sel4(SL.e, l);
       for (int s = sb; s < se; ++s)
         if (M.slink(s) == j) {
           const float4 sp = M.sph4(s);
