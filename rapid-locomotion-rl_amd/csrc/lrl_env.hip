@@ -1811,6 +1811,20 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       act[j] = fminf(fmaxf(a, -c), c);
     }
   }
+  // per-env inputs read before the LDS staging barrier below, so their memory latency overlaps the table copy
+  const int ctl = P.control_type;
+  const float payload = S.payload[e];
+  const V3 cb = v3(S.com[e], S.com[N + e], S.com[2 * N + e]);
+  const float fr_e = S.friction[e], rs_e = S.restitution[e];
+  float kpf3[3], kdf3[3], ms3[3], lqd3[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int jj = 3 * ql + j;
+    kpf3[j] = S.kp[jj * N + e];
+    kdf3[j] = S.kd[jj * N + e];
+    ms3[j] = S.motor_strength[jj * N + e];
+    lqd3[j] = ctl == 1 ? S.last_dof_vel[jj * N + e] : 0.f;
+  }
   // leg blocks first, then the contact rows, (terrain: the query's vertex block), then the model tables
   const int nsph = K->num_spheres;
   static_assert(LRL_NUM_DOF * LIMF * ENVS <= 64 * BLOCK, "joint-limit rows must fit the terrain vertex blocks");
@@ -1835,8 +1849,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     }
     __syncthreads();
   }
-  const float payload = S.payload[e];
-  const V3 cb = v3(S.com[e], S.com[N + e], S.com[2 * N + e]);
   const float mb = K->base_mass + payload;
   float Ib[6];
   {
@@ -1844,10 +1856,10 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 #pragma unroll
     for (int k = 0; k < 6; ++k) Ib[k] = K->base_inertia[k] * sc;
   }
-  const float mu = 0.5f * (S.friction[e] + P.ground_friction);
-  const float rest = 0.5f * (S.restitution[e] + P.ground_restitution);
+  const float mu = 0.5f * (fr_e + P.ground_friction);
+  const float rest = 0.5f * (rs_e + P.ground_restitution);
   // self-contacts: both shapes carry the env's robot material, so PhysX's average combine is that material
-  const float mu_s = S.friction[e], rest_s = S.restitution[e];
+  const float mu_s = fr_e, rest_s = rs_e;
   const bool physics = flags & LRL_STEP_PHYSICS;
   uint64_t active = 0;
   uint64_t own = 0;  // spheres whose detection / Delassus rows / warm start this lane owns
@@ -1865,18 +1877,15 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   // 'P': kp3 / kd3 = gains x Kp / Kd factors, tg3 = position target; 'V': kp3 / kd3 = the bare gains, tg3 = the
   // scaled action (a velocity target), lqd3 = last_dof_vel (constant over the sub-steps: post_physics_step sets it);
   // 'T': tg3 = the scaled action (a torque)
-  const int ctl = P.control_type;
-  float kp3[3], kd3[3], ms3[3], tg3[3], lim3[3], tau3[3], lqd3[3];
+  float kp3[3], kd3[3], tg3[3], lim3[3], tau3[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int jj = 3 * ql + j;
     const bool pos = ctl == 0;
-    kp3[j] = pos ? P.p_gains[jj] * S.kp[jj * N + e] : P.p_gains[jj];
-    kd3[j] = pos ? P.d_gains[jj] * S.kd[jj * N + e] : P.d_gains[jj];
-    ms3[j] = S.motor_strength[jj * N + e];
+    kp3[j] = pos ? P.p_gains[jj] * kpf3[j] : P.p_gains[jj];
+    kd3[j] = pos ? P.d_gains[jj] * kdf3[j] : P.d_gains[jj];
     tg3[j] = pos ? pos_target(P, act, jj) : act_scaled(P, act, jj);
     lim3[j] = P.torque_limits[jj];
-    lqd3[j] = ctl == 1 ? S.last_dof_vel[jj * N + e] : 0.f;
   }
   for (int sub = 0; sub < P.decimation; ++sub) {
 #pragma unroll
