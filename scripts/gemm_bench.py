@@ -13,6 +13,7 @@ dev = "cuda:0"
 SHAPES = [
     ("AC2 fwd  NT 512->256 x2", 0, 2, B, 256, 512),
     ("AC1 fwd  NT 60->1024", 0, 2, B, 1024, 60),
+    ("AC1 fwd  NT 64->1024 (padded X)", 0, 2, B, 1024, 64),
     ("D1 fwd   NT 630->256 gather", 0, 2, B, 256, 630),
     ("E1 fwd   NT 18->256 gather", 0, 2, B, 256, 18),
     ("E1 noelu NT 18->256 gather", 0, 1, B, 256, 18),
