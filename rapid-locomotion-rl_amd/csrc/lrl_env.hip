@@ -1004,18 +1004,21 @@ __device__ void self_detect(const KParams* __restrict__ K, const Lds& M, const S
   const lrl_env_params& P = K->p;
   const float co = P.contact_offset;
   const int* G = M.sgrp() + 10 * ql;
+  const uint64_t freem = free_spheres(M, quad_or(active));
+  const int cap = min(LRL_SELF_SLOTS, __builtin_popcountll(freem) >> 1);  // the env's slots
+  // the count stops at cap: a lane's count only places the lanes after it, and a prefix that reaches cap leaves
+  // them no slot either way, so the capped counts assign exactly the slots the full counts would
   int cnt = 0;
 #pragma unroll
   for (int g = 0; g < 5; ++g)
     if ((live >> g) & 1u)
-      for (int p = G[2 * g]; p < G[2 * g + 1]; ++p) {
+      for (int p = G[2 * g]; p < G[2 * g + 1] && cnt < cap; ++p) {
         V3 n, x;
         cnt += self_geom(K, M, M.spair(p), n, x) < co ? 1 : 0;
       }
   const int c0 = quad_bcast_i(cnt, 0), c1 = quad_bcast_i(cnt, 1), c2 = quad_bcast_i(cnt, 2);
   int slot = ql == 0 ? 0 : ql == 1 ? c0 : ql == 2 ? c0 + c1 : c0 + c1 + c2;
-  const uint64_t freem = free_spheres(M, quad_or(active));
-  const int end = min(slot + cnt, min(LRL_SELF_SLOTS, __builtin_popcountll(freem) >> 1));
+  const int end = min(slot + cnt, cap);
   if (slot >= end) return;
 #pragma unroll
   for (int g = 0; g < 5; ++g)
