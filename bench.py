@@ -116,7 +116,7 @@ def cpu_baseline(env_seconds=4.0):
                         "reference's Isaac Gym CPU pipeline is proprietary and absent (BASELINE.md §3)"))
 
 
-def bench_go1_rough(dev, iters=3, warmup=1):
+def bench_go1_rough(dev, iters=6, warmup=2):
     """Secondary line, BASELINE configs[2]: 4096 Go1 envs on the curriculum trimesh (stairs, slopes, obstacles,
     stepping stones; terrain curriculum) with the upstream reset path (legacy_fork=False: time-outs, reset_idx
     inside step, grid-adaptive command curriculum) — full PPO iterations, same timing rules as the headline."""
