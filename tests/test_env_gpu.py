@@ -389,49 +389,6 @@ def test_upstream_resets_timeouts_and_command_resampling():
     inner.close()
 
 
-def test_resampling_after_caller_writes_episode_length():
-    """ADVICE r1 (env.py step): when a caller writes episode_length_buf between two steps (an upstream-style
-    init_at_random_ep_len), the envs due for command resampling are re-derived on the device AND on the host, so
-    _resample_commands (legged_robot.py:595-626) updates bins, curriculum and commands of exactly those envs."""
-    import copy
-    from lrl.env import LeggedRobotEnv
-    n = 64
-    cfg = _cfg("mc", n, **{"commands.resampling_time": 0.1, "noise.add_noise": False})
-    env = LeggedRobotEnv("cuda:0", cfg=cfg, legacy_fork=False)
-    interval = int(cfg.commands.resampling_time / env.dt)
-    assert interval == 5
-    env.reset()
-    zero = torch.zeros(n, 12, device="cuda:0")
-    env.step(zero)
-    env.step(zero)  # the previous step's cached host ids now name the envs due by the OLD episode lengths
-    due_ids = np.array([3, 7, 19, 40])
-    elen = torch.zeros(n, dtype=torch.int32, device="cuda:0")
-    elen[torch.from_numpy(due_ids).cuda()] = interval - 1
-    env.episode_length_buf[:] = elen
-    cur = copy.deepcopy(env.curriculum)
-    old_bins = env.env_command_bins[due_ids].copy()
-    timesteps = int(cfg.commands.resampling_time / env.dt)
-    ep_len = min(cfg.env.max_episode_length, timesteps)
-    lin, ang = (env._command_sums[env._track_rows][:, torch.from_numpy(due_ids).cuda()] / ep_len).cpu().numpy()
-    cmd0 = env.commands.clone()
-    env.step(zero)
-    torch.cuda.synchronize()
-    assert not bool(env.reset_buf.any())
-    changed = np.flatnonzero((env.commands != cmd0).any(dim=1).cpu().numpy())
-    assert set(changed) <= set(due_ids.tolist())
-    lin_thr = cfg.commands.forward_curriculum_threshold * env.reward_scales["tracking_lin_vel"]
-    ang_thr = cfg.commands.yaw_curriculum_threshold * env.reward_scales["tracking_ang_vel"]
-    cur.update(old_bins, lin, ang, lin_thr, ang_thr, local_range=0.5)
-    new_cmds, new_bins = cur.sample(batch_size=len(due_ids))
-    np.testing.assert_array_equal(env.env_command_bins[due_ids], new_bins)
-    c = new_cmds.astype(np.float32)
-    keep = (np.sqrt(c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]) > np.float32(0.2)).astype(np.float32)
-    c[:, 0] *= keep
-    c[:, 1] *= keep
-    np.testing.assert_array_equal(env.commands[torch.from_numpy(due_ids).cuda(), :3].cpu().numpy(), c)
-    env.close()
-
-
 def test_train_eval_split():
     """eval_cfg (base_task.py:43-50, legged_robot.py:204-290, 456-469): eval envs follow the train envs in one
     sim; resets log train envs into extras['train/episode'] and keep each eval env's first finished episode;
