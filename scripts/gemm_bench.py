@@ -7,7 +7,7 @@ import sys
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-B = 24576
+B = int(os.environ.get("GEMM_BENCH_B", "24576"))  # 4096: the rollout act's row count
 dev = "cuda:0"
 # (name, layout, epi, M, N, K, groups-as-separate-calls)
 SHAPES = [
