@@ -63,19 +63,31 @@ def run(libpath):
         ws = torch.empty(128 * (M * N + M), device=dev) if lay == 3 else None
 
         def call():
+            cs = C.c_void_p(torch.cuda.current_stream().cuda_stream)  # (the capture stream under GEMM_BENCH_GRAPH)
             rc = L.lrl_gemm_f32(lay, epi, M, N, K, p(A), C.c_int64(lda), p(Bm), C.c_int64(ldb), p(Cm),
                                 C.c_int64(N), p(bias), p(aux), C.c_int64(N), p(rows), p(ws),
-                                C.c_int64(ws.numel() if ws is not None else 0), st)
+                                C.c_int64(ws.numel() if ws is not None else 0), cs)
             assert rc == 0, rc
         for _ in range(3):
             call()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         n = 20
-        e0.record()
-        for _ in range(n):
-            call()
-        e1.record()
+        if os.environ.get("GEMM_BENCH_GRAPH"):  # the n launches captured once as a HIP graph, replayed
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    call()
+            g.replay()
+            torch.cuda.synchronize()
+            e0.record()
+            g.replay()
+            e1.record()
+        else:
+            e0.record()
+            for _ in range(n):
+                call()
+            e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n * 1e3
         tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
