@@ -44,13 +44,10 @@ def pmc_traffic(*kernels):
 
 
 def env_kernel_timing(env, start):
-    """HIP events around each env-kernel launch of lrl_sim_step, on its launch stream (lrl_sim_timing; the history
-    shift launched before it is outside): start=True begins recording, start=False stops and returns the mean ms."""
-    import ctypes as C
-    from lrl import _abi
-    ms, n = C.c_double(0.0), C.c_int64(0)
-    _abi.check(_abi.lib().lrl_sim_timing(env._sim, C.c_int32(1 if start else 0), C.byref(ms), C.byref(n)))
-    return ms.value / n.value if n.value else float("nan")
+    """HIP events around each env-kernel launch of lrl_sim_step, on its launch stream (LeggedRobotEnv.kernel_timing;
+    the history shift launched before it is outside): start=True begins recording, start=False returns the mean ms."""
+    r = env.kernel_timing(start)
+    return None if start else r[0]
 
 
 def _cpu_info():
@@ -108,7 +105,9 @@ def cpu_baseline(env_seconds=4.0):
                 ppo_iter_s=round(dt, 3),
                 env_only_all_cores_env_steps_per_s=round(env_all, 1),
                 env_only_1_core_env_steps_per_s=round(env_one, 1),
-                cpu_model=model, cpus_visible=os.cpu_count(), cpus_usable=avail,
+                cpu_model=model, threads_used=threads, cpus_visible_machine=os.cpu_count(), cpus_in_affinity_mask=avail,
+                cores_note=(f"cores = the {threads} threads every leg ran on (this box's CPU share, OMP_NUM_THREADS); "
+                            "the affinity mask shows the whole machine's CPUs, which this job may not use"),
                 sample=(f"one PPO iteration of {ENVS_PER_GPU} Mini Cheetah envs x {R.RunnerArgs.num_steps_per_env} steps "
                         f"+ update ({dt:.1f} s; env: oracle/lrl_oracle.c float + OpenMP, {threads} threads; policy / "
                         f"update: torch CPU, {threads} threads); env-only: {ENVS_PER_GPU} envs x {n_all} steps on "
@@ -154,6 +153,11 @@ WORKLOADS = {
     "go1": lambda w: (f"{w * ENVS_PER_GPU} Go1 envs on the plane ({ENVS_PER_GPU} per GPU), teacher PPO + student "
                       "(adaptation-module) distillation update (BASELINE configs[4] at 2 GPUs)"),
 }
+
+
+# BASELINE.json's metric (the headline, Mini Cheetah); the Go1 workload names its own robot
+METRICS = {"mc": "env-steps/sec, 4096 Mini Cheetah envs, 1/2/4/8 MI355X; PPO iters/sec",
+           "go1": "env-steps/sec, 4096 Go1 envs per GPU (teacher-student update), 1/2 MI355X; PPO iters/sec"}
 
 
 def _free_port():
@@ -215,10 +219,12 @@ def main():
                     help="mc: 4096 Mini Cheetah envs per GPU, flat (configs[1] / [3]); go1: 4096 Go1 envs per GPU, "
                          "plane, teacher + student update (configs[4] at --gpus 2)")
     ap.add_argument("--world-check", action="store_true",
-                    help="join the process group, print the world every rank sees and exit (no GPU work)")
+                    help="join a gloo process group, print the world every rank sees and exit (no GPU work)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.world_check:
+        os.environ["LRL_DIST_BACKEND"] = "gloo"  # CPU tensors, no device context
     backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
     if backend == "nccl":
         ndev = torch.cuda.device_count()
@@ -315,15 +321,17 @@ def main():
         rows_iter = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env
         iter_flop = rows_iter * (5 * 3.92e6 + 0.94e6)
         iter_tf = iter_flop / (elapsed / args.steps) / 1e12
+        # distinct physical devices the ranks ran on (a gloo rehearsal puts several ranks on one GPU)
+        n_dev = world if backend == "nccl" else min(world, ndev)
         out = {
-            "metric": "env-steps/sec, 4096 Mini Cheetah envs, 1/2/4/8 MI355X; PPO iters/sec",
-            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRICS[args.workload],
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": n_dev, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": WORKLOADS[args.workload](world),
                        "envs_per_gpu": ENVS_PER_GPU, "global_envs": world * ENVS_PER_GPU,
                        "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
-                       "parallelism": f"dp{world}", "world_size": dist.get_world_size() if world > 1 else 1,
+                       "parallelism": f"dp{world}", "world_size": world,
                        "backend": (backend if world > 1 else None),
                        "policy": "ActorCritic 42/18/630->12, random init; teacher PPO + student adaptation update"},
             "ppo_iters_per_s": round(args.steps / elapsed, 3),

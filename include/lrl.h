@@ -251,6 +251,9 @@ enum lrl_tensor_id {
 #define LRL_STEP_INJECT_UNIFORM 4u /* read noise / DR uniforms from lrl_sim_inject_uniforms buffers */
 
 int32_t lrl_abi_version(void);
+/* First 16 hex digits of the sha256 of the csrc sources + headers the library was built from (csrc/Makefile
+   SRC_HASH); lrl/_abi.py refuses to load a library whose hash differs from the sources beside it. */
+const char* lrl_build_hash(void);
 const char* lrl_last_error(void);
 int32_t lrl_device_count(void);
 

@@ -133,14 +133,35 @@ def _fill_array(arr, v):
 
 _lib = None
 
+_CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+# the files and order of csrc/Makefile's SRC_HASH (SRCS then HDRS)
+_HASHED = ["lrl_env.hip", "lrl_aux.hip", "lrl_gae.hip", "lrl_gemm.hip", "lrl_ppo.hip", "lrl_capi.cpp",
+           "lrl_kparams.h", "lrl_gemm.h", "../../include/lrl.h", "../../include/lrl_philox.h"]
+
+
+def source_hash():
+    """sha256 (first 16 hex digits) of the sources liblrl.so must have been built from."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in _HASHED:
+        with open(os.path.join(_CSRC, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
 
 def lib():
-    """liblrl.so, loaded once.  Raises (no fallback) if it was not built."""
+    """liblrl.so, loaded once.  Raises (no fallback) if it was not built, or was built from other sources than the
+    ones in this tree (a stale binary)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"liblrl.so not built ({LIB_PATH}); run __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)
+        L.lrl_build_hash.restype = C.c_char_p
+        built, want = L.lrl_build_hash().decode(), source_hash()
+        if built != want:
+            raise RuntimeError(f"{LIB_PATH} was built from other sources (hash {built}, tree {want}); "
+                               "rebuild it: __graft_entry__.build()")
         L.lrl_last_error.restype = C.c_char_p
         for name in ["lrl_sim_create", "lrl_sim_destroy", "lrl_sim_tensor", "lrl_sim_step", "lrl_sim_reset_idx",
                      "lrl_sim_set_root_state_indexed", "lrl_sim_set_dof_state_indexed", "lrl_sim_inject_uniforms",

@@ -228,7 +228,6 @@ class LeggedRobotEnv:
         self.extras = _LazyExtras(self)
         self.record_now = False
         self.complete_video_frames = []
-        self.kernel_timer = None
 
         # ---- origins, DR draws at creation (legged_robot.py:1216-1231, 1385-1415, 519-542) ----
         self._set_env_origins()
@@ -447,14 +446,7 @@ class LeggedRobotEnv:
             if (len(due) > 0) if self._dist is None else (self._dist_count(len(due)) > 0):
                 self.resample_commands(due, due_np)
         self._sums_host = None  # the kernel below changes the command sums
-        timer = self.kernel_timer
-        if timer is not None:  # HIP events on the launch stream around the fused kernel (bench.py)
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
         _abi.check(self._L.lrl_sim_step(self._sim, C.c_void_p(actions.data_ptr()), C.c_uint32(flags), self._stream()))
-        if timer is not None:
-            ev1.record()
-            timer.append((ev0, ev1))
         self.common_step_counter += 1
         if not self.legacy_fork:  # reset_idx of the terminated / timed-out envs, then their observations
             # one device->host copy per step: bit 0 = reset now, bit 1 = due for resampling next step (episode
@@ -495,6 +487,16 @@ class LeggedRobotEnv:
         ex.set_lazy("body_pos", lambda: self.root_states[:, 0:3].cpu().numpy())
         ex.set_lazy("torques", lambda: self.torques.cpu().numpy())
         return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
+
+    def kernel_timing(self, start):
+        """Env-kernel launch time, the one definition bench.py and the scripts use: HIP events around each
+        env_step_kernel launch of lrl_sim_step on its own stream (lrl_sim_timing; the history-shift launch before it
+        is outside).  start=True begins recording; start=False stops and returns (mean ms, total ms, launches)."""
+        ms, n = C.c_double(0.0), C.c_int64(0)
+        _abi.check(self._L.lrl_sim_timing(self._sim, C.c_int32(1 if start else 0), C.byref(ms), C.byref(n)))
+        if start:
+            return None
+        return (ms.value / n.value if n.value else float("nan")), ms.value, n.value
 
     def _foot_positions(self):
         self.refresh_rigid_body_state()

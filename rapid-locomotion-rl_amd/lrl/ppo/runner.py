@@ -119,6 +119,8 @@ class Runner:
             if RunnerArgs.save_interval and it % RunnerArgs.save_interval == 0:
                 self.save(it)
         self.current_learning_iteration += num_learning_iterations
+        if num_learning_iterations > 0:  # the reference always saves after the loop (__init__.py:246-265)
+            self.save(tot_iter - 1)
 
     def _eval_actions(self, obs, priv, hist, n_train, eval_expert):
         ac = self.alg.actor_critic

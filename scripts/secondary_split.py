@@ -7,7 +7,6 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from lrl import config as lcfg  # noqa: E402
@@ -31,8 +30,7 @@ obs_dict = env.get_observations()
 obs, priv, hist = obs_dict["obs"], obs_dict["privileged_obs"], obs_dict["obs_history"]
 for it in range(iters):
     torch.cuda.synchronize()
-    timer = []
-    env.env.kernel_timer = timer
+    env.env.kernel_timing(True)
     t0 = time.perf_counter()
     t_act = t_step = t_proc = 0.0
     with torch.inference_mode():
@@ -51,11 +49,10 @@ for it in range(iters):
         alg.compute_returns(obs, priv)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    env.env.kernel_timer = None
+    k = env.env.kernel_timing(False)[1]
     alg.update()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    k = float(np.sum([a.elapsed_time(b) for a, b in timer]))
     print(f"iter {it}: rollout {1e3 * (t1 - t0):.2f} ms (host: act {1e3 * t_act:.2f}, env.step {1e3 * t_step:.2f}, "
           f"process {1e3 * t_proc:.2f}; env kernels {k:.2f} ms GPU) update {1e3 * (t2 - t1):.2f} ms", flush=True)
 env.env.close()

@@ -9,7 +9,6 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from lrl import config as lcfg  # noqa: E402
@@ -37,12 +36,11 @@ def env_kernel_ms(rough, steps=60):
     a = torch.randn(N, 12, device="cuda:0") * 0.3
     for _ in range(20):
         env.step(a)
-    timer = []
-    env.env.kernel_timer = timer
+    env.env.kernel_timing(True)
     for _ in range(steps):
         env.step(a)
     torch.cuda.synchronize()
-    ms = float(np.mean([x.elapsed_time(y) for x, y in timer]))
+    ms = env.env.kernel_timing(False)[0]
     env.env.close()
     return ms
 

@@ -28,6 +28,25 @@ def test_library_exports_every_declared_symbol():
     assert lib.lrl_abi_version() == 1
 
 
+def test_library_matches_the_sources_beside_it():
+    """Stale-binary guard: the hash baked into liblrl.so (csrc/Makefile SRC_HASH) equals the hash of the tree's
+    sources, and the loader refuses a library whose hash differs."""
+    if not os.path.exists(_abi.LIB_PATH):
+        pytest.skip("liblrl.so not built")
+    lib = C.CDLL(_abi.LIB_PATH)
+    lib.lrl_build_hash.restype = C.c_char_p
+    assert lib.lrl_build_hash().decode() == _abi.source_hash()
+    assert _abi.lib() is not None
+    saved, _abi._lib = _abi._lib, None
+    real = _abi.source_hash
+    try:
+        _abi.source_hash = lambda: "0" * 16
+        with pytest.raises(RuntimeError, match="other sources"):
+            _abi.lib()
+    finally:
+        _abi.source_hash, _abi._lib = real, saved
+
+
 def test_struct_layout_matches_header():
     code = r"""
 #include <stdio.h>

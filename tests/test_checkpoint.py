@@ -80,6 +80,26 @@ def test_trained_policy_walks_in_this_physics():
     assert upright >= 0.95, upright
 
 
+def test_learn_saves_after_the_loop(tmp_path):
+    """The reference saves after the iteration loop whatever save_interval is (mini_gym_learn/ppo/__init__.py:
+    246-265): learn(3) with save_interval 400 leaves ac_weights_000002.pt, ac_weights_last.pt and both TorchScript
+    exports (iteration 0 is also a save_interval iteration, as in the reference).  CPU env: the oracle's build."""
+    from oracle.cpu_env import CpuVecEnv, cpu_compute_returns
+    from lrl.ppo import runner as R
+    env = CpuVecEnv(16, threads=1)
+    runner = R.Runner(env, device="cpu", seed=3, logger=R.Logger(str(tmp_path)))
+    runner.alg.storage.compute_returns = cpu_compute_returns(runner.alg.storage)
+    runner.learn(3)
+    ck = tmp_path / "checkpoints"
+    names = sorted(p.name for p in ck.iterdir())
+    assert names == ["ac_weights_000000.pt", "ac_weights_000002.pt", "ac_weights_last.pt",
+                     "adaptation_module_latest.jit", "body_latest.jit"], names
+    last = torch.load(ck / "ac_weights_last.pt", weights_only=True)
+    for k, v in runner.alg.actor_critic.state_dict().items():
+        assert torch.equal(last[k], v.cpu()), k
+    assert runner.current_learning_iteration == 3
+
+
 def test_runner_save_torchscript_export_reproduces_student(tmp_path):
     """Runner.save (mini_gym_learn/ppo/__init__.py:220-242): the state dict plus TorchScript exports of the
     adaptation module and the actor body, the pair the reference's deployment loads (play scripts: latent =
