@@ -291,6 +291,13 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    # self-contact slot statistics under the bench's own workload (one more, untimed, iteration with the counters on)
+    env.env.self_contact_stats(True)
+    runner.learn(1)
+    torch.cuda.synchronize()
+    sc = env.env.self_contact_stats(False)
+    sc["env_substeps"] = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env * 4
+    sc["dropped_fraction_of_pairs"] = sc["self_pairs_dropped"] / max(1, sc["self_pairs_in_contact"])
     # env-only rate: the fused step kernel alone, random actions, same env
     a = torch.randn(ENVS_PER_GPU, 12, device=dev) * 0.3
     for _ in range(10):
@@ -337,6 +344,8 @@ def main():
             "ppo_iters_per_s": round(args.steps / elapsed, 3),
             "env_only_env_steps_per_s_per_gpu": round(env_only, 1),
             "env_step_kernel_ms": round(k_ms, 4),
+            "self_contact": dict(sc, note="one untimed PPO iteration after the timed ones; a pair without a slot is "
+                                          "one PhysX would solve and this solver skips in that sub-step (DESIGN.md §4)"),
             "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel<false> (plane ground)", "achieved": round(achieved, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,

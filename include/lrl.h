@@ -275,6 +275,13 @@ int32_t lrl_sim_step(lrl_sim* sim, const float* actions, uint32_t flags, void* s
  * restarts (enable = 1) or stops (enable = 0) recording. */
 int32_t lrl_sim_timing(lrl_sim* sim, int32_t enable, double* total_ms, int64_t* launches);
 
+/* Self-contact slot statistics (no reference counterpart: PhysX solves every self-pair, this solver gives an env
+   min(8, free spheres / 2) slots per sub-step).  enable = 1 zeroes the counters and starts counting
+   (the detection then counts every pair in contact; the slots and results are unchanged); enable = 0 stops.  Either
+   way `out` (may be null) receives the counters before the call: [0] env-sub-steps with a self-contact, [1] pairs in
+   contact summed over them, [2] env-sub-steps with more pairs than slots, [3] pairs left without a slot. */
+int32_t lrl_sim_self_contact_stats(lrl_sim* sim, int32_t enable, uint64_t* out);
+
 /* Injected uniforms for parity tests: noise_u [N,num_obs], dr_u [N] (NaN = no redraw). */
 int32_t lrl_sim_inject_uniforms(lrl_sim* sim, const float* noise_u, const float* dr_u);
 /* Injected push uniforms for parity tests: u [N,2] f32 device, row e = env e's (x, y) draw of _push_robots when it is

@@ -60,6 +60,7 @@ struct lrl_sim {
   int32_t* d_body_link = nullptr;
   float* d_foot_xyz = nullptr;
   void* terr = nullptr;  // terrain mesh buffers (lrl_sim_set_terrain)
+  uint32_t* self_stats = nullptr;  // lrl_sim_self_contact_stats counters
   // lrl_sim_timing: HIP events around each env-kernel launch of lrl_sim_step (not the history-shift launch before it)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -460,6 +461,7 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->d_body_link);
   (void)hipFree(s->d_foot_xyz);
   (void)hipFree(s->terr);
+  (void)hipFree(s->self_stats);
   for (auto& pr : s->ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -530,6 +532,25 @@ int32_t lrl_sim_timing(lrl_sim* s, int32_t enable, double* total_ms, int64_t* la
   if (launches) *launches = (int64_t)s->ev_used;
   s->ev_used = 0;
   s->timing = enable != 0;
+  return 0;
+}
+
+int32_t lrl_sim_self_contact_stats(lrl_sim* s, int32_t enable, uint64_t* out) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  HIPCHECK(hipSetDevice(s->device));
+  HIPCHECK(hipDeviceSynchronize());  // no env kernel in flight reads the parameter block below
+  if (out) {
+    uint32_t c[4] = {0, 0, 0, 0};
+    if (s->self_stats) HIPCHECK(hipMemcpy(c, s->self_stats, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out[i] = c[i];
+  }
+  if (enable) {
+    if (!s->self_stats && hipMalloc(&s->self_stats, 4 * sizeof(uint32_t)) != hipSuccess)
+      return fail(LRL_E_NOMEM, "hipMalloc (self-contact counters)");
+    HIPCHECK(hipMemset(s->self_stats, 0, 4 * sizeof(uint32_t)));
+  }
+  s->hk.self_stats = enable ? s->self_stats : nullptr;
+  HIPCHECK(hipMemcpy(s->dk, &s->hk, sizeof(KParams), hipMemcpyHostToDevice));
   return 0;
 }
 

@@ -1008,15 +1008,29 @@ __device__ void self_detect(const KParams* __restrict__ K, const Lds& M, const S
   const int cap = min(LRL_SELF_SLOTS, __builtin_popcountll(freem) >> 1);  // the env's slots
   // the count stops at cap: a lane's count only places the lanes after it, and a prefix that reaches cap leaves
   // them no slot either way, so the capped counts assign exactly the slots the full counts would
+  // (lrl_sim_self_contact_stats on: the full count, so the pairs the cap drops are counted; the slots are the same)
+  uint32_t* const stats = K->self_stats;
+  const int lim = stats ? 0x7fffffff : cap;
   int cnt = 0;
 #pragma unroll
   for (int g = 0; g < 5; ++g)
     if ((live >> g) & 1u)
-      for (int p = G[2 * g]; p < G[2 * g + 1] && cnt < cap; ++p) {
+      for (int p = G[2 * g]; p < G[2 * g + 1] && cnt < lim; ++p) {
         V3 n, x;
         cnt += self_geom(K, M, M.spair(p), n, x) < co ? 1 : 0;
       }
   const int c0 = quad_bcast_i(cnt, 0), c1 = quad_bcast_i(cnt, 1), c2 = quad_bcast_i(cnt, 2);
+  if (stats) {
+    const int total = c0 + c1 + c2 + quad_bcast_i(cnt, 3);
+    if (ql == 0 && total > 0) {  // per env and sub-step: pairs in contact, pairs without a slot
+      atomicAdd(stats + 0, 1u);
+      atomicAdd(stats + 1, (uint32_t)total);
+      if (total > cap) {
+        atomicAdd(stats + 2, 1u);
+        atomicAdd(stats + 3, (uint32_t)(total - cap));
+      }
+    }
+  }
   int slot = ql == 0 ? 0 : ql == 1 ? c0 : ql == 2 ? c0 + c1 : c0 + c1 + c2;
   const int end = min(slot + cnt, cap);
   if (slot >= end) return;

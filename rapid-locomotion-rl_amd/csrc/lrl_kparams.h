@@ -58,6 +58,9 @@ struct KParams {
   const float* terr_wmax;  // max vertex z over the window around a base cell (terrain_window_max)
   int32_t terr_rows, terr_cols;
   float terr_inv_hs;
+  // lrl_sim_self_contact_stats: null (off), or 4 device counters [env-sub-steps with a self-contact, pairs in contact,
+  // env-sub-steps with more pairs than slots, pairs without a slot]
+  uint32_t* self_stats;
 };
 
 // SoA device buffers of a sim (each [.][N] with N = padded env count unless noted).

@@ -498,6 +498,16 @@ class LeggedRobotEnv:
             return None
         return (ms.value / n.value if n.value else float("nan")), ms.value, n.value
 
+    def self_contact_stats(self, start):
+        """lrl_sim_self_contact_stats: start=True zeroes the device counters and starts counting; start=False stops and
+        returns {env_substeps_in_self_contact, self_pairs_in_contact, env_substeps_over_cap, self_pairs_dropped}."""
+        out = (C.c_uint64 * 4)()
+        _abi.check(self._L.lrl_sim_self_contact_stats(self._sim, C.c_int32(1 if start else 0), out))
+        if start:
+            return None
+        return dict(zip(("env_substeps_in_self_contact", "self_pairs_in_contact", "env_substeps_over_cap",
+                         "self_pairs_dropped"), (int(x) for x in out)))
+
     def _foot_positions(self):
         self.refresh_rigid_body_state()
         return self.rigid_body_state[:, self.feet_indices, 0:3]

@@ -21,6 +21,7 @@ def run_env(num_envs=16, steps=1000):
         actions = 0.0 * torch.ones(env.num_envs, env.num_actions, device=env.device)
         obs, rew, done, info = env.step(actions)
     print("Done")
+    return env
 
 
 if __name__ == "__main__":
