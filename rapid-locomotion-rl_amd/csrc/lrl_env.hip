@@ -595,7 +595,7 @@ struct Body {  // per-lane env state during the step: the base in every lane of 
   float pos[3], quat[4], V[3], W[3];
   float q[3], qd[3];  // joints 3 ql .. 3 ql + 2 (the whole 12 are gathered over the quad for the post-physics)
   float lo[3], hi[3];  // their position limits (KParams::dof_lo / dof_hi)
-  float llam[3];       // their limit-row impulses after the last sub-step (warm start; on the terrain mesh the
+  float llam[3];       // their limit-row impulses x sigma after the last sub-step (warm start; on the terrain mesh the
                        // rows' LDS is the next sub-step's query scratch)
 };
 
@@ -748,10 +748,12 @@ __device__ __forceinline__ void limit_setup(const Lds& M, const float* Si, int r
   row[LIM_IW * ENVS] = 1.f / w;
 }
 
-// warm start of a limit row in its owner lane with the carried impulse lam: v_b += lam z (summed over the quad by
-// the caller), Y_L += lam e
-__device__ __forceinline__ void limit_apply(const Lds& M, int r, int L, float lam, float* dvb) {
+// warm start of a limit row in its owner lane with the carried impulse: v_b += lam z (summed over the quad by the
+// caller), Y_L += lam e.  The carried value is lam x the sigma it was solved with (lam >= 0): a row whose nearer limit
+// switched since the previous sub-step (sigma flipped) starts cold instead of pushing the wrong way.
+__device__ __forceinline__ void limit_apply(const Lds& M, int r, int L, float lam_sg, float* dvb) {
   float* const row = M.lm(r);
+  const float lam = fmaxf(lam_sg * row[LIM_SG * ENVS], 0.f);
   float z[6], ev[3], y[3];
 #pragma unroll
   for (int c = 0; c < 6; ++c) z[c] = row[(LIM_Z + c) * ENVS];
@@ -1631,7 +1633,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   __syncthreads();  // the leg accumulators each lane owned are read by the whole quad below
   if (P.joint_limits) {  // this leg's limit impulses, carried to the next sub-step in registers
 #pragma unroll
-    for (int j = 0; j < 3; ++j) st.llam[j] = M.lm(3 * ql + j)[LIM_LAM * ENVS];
+    for (int j = 0; j < 3; ++j) st.llam[j] = M.lm(3 * ql + j)[LIM_LAM * ENVS] * M.lm(3 * ql + j)[LIM_SG * ENVS];
   }
   LRL_PROF(3)  // PGS iterations
   // materialise the lazily propagated joint rates of this lane's leg

@@ -35,3 +35,31 @@ def test_oracle_joint_limits_hold(robot):
         out[on] = np.maximum(st["dof_pos"] - hi, lo - st["dof_pos"]).max()
     assert out[1] < 1e-3, out  # held at the limit
     assert out[0] > 0.05, out  # the same drive crosses it without the rows
+
+
+def test_oracle_narrow_joint_range_holds_when_the_nearer_limit_switches():
+    """A joint range narrower than 2 (margin + 2 dt |qd|) puts both limits inside the detection window: the nearer
+    limit (sigma) can switch between sub-steps while the row stays active.  The carried impulse is stored with its
+    sigma and a switched row starts cold, so the joint is held inside the range instead of being pushed
+    out by the previous limit's impulse."""
+    n = 4
+    cfg, rob, M, P = make("mc", **{"env.num_envs": n})
+    P.self_collisions = 0
+    default = np.array(P.default_dof_pos[:], np.float32)
+    lo = np.array(M.dof_lower[:], np.float32)
+    hi = np.array(M.dof_upper[:], np.float32)
+    j = 1  # front-right thigh
+    lo[j], hi[j] = default[j] - 0.004, default[j] + 0.004
+    for k in range(12):
+        M.dof_lower[k], M.dof_upper[k] = float(lo[k]), float(hi[k])
+    st = oracle.make_state(n, M.num_bodies, P.num_obs, P.num_history, P.num_sum_keys + 1, P.num_sum_keys + 5)
+    st["root"][:, 2] = 0.6
+    st["dof_pos"][:] = default
+    st["dof_vel"][:] = 0.0
+    st["dof_vel"][:, j] = np.array([4.0, -4.0, 8.0, -8.0], np.float32)
+    act = np.zeros((n, 12), np.float32)
+    for s in range(5):
+        oracle.env_step(M, P, st, act, _abi.STEP_PHYSICS, common_step_counter=s + 1)
+        assert np.isfinite(st["dof_pos"]).all()
+        over = np.maximum(st["dof_pos"][:, j] - hi[j], lo[j] - st["dof_pos"][:, j]).max()
+        assert over < 0.01, (s, over)
