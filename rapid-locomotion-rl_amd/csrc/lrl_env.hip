@@ -38,6 +38,15 @@
 
 namespace lrl {
 
+// XCD-aware env blocks: the hardware deals workgroup ids round-robin over the 8 XCDs, so block b is renumbered to
+// the env block it covers with consecutive env blocks on one XCD.  A wave's SoA field access is 16 envs x 4 B = half
+// a 128-B line; with the plain mapping the two halves of each line were read (and written) through two different
+// XCD L2s, each fetching the whole line.
+__device__ __forceinline__ int env_block() {
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // Phase timers (build with -DLRL_ENV_PROFILE; read with lrl_debug_env_profile): per-wave shader-clock
 // cycles of the step kernel's phases, summed over waves.
 #ifdef LRL_ENV_PROFILE
@@ -1287,7 +1296,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       if (pw.z - rad - P.contact_offset <= hwin) cand |= 1ull << s;
 #ifdef LRL_ENV_DEBUG
       {
-        const int e_ = blockIdx.x * ENVS + (int)(threadIdx.x >> 2);
+        const int e_ = env_block() * ENVS + (int)(threadIdx.x >> 2);
         float* d = g_env_dbg + ((size_t)e_ * 64 + s) * 8;
         d[0] = (float)((cand >> s) & 1ull); d[1] = 1e30f; d[2] = pw.x; d[3] = pw.y; d[4] = pw.z; d[5] = hwin;
         d[6] = rad; d[7] = 1.f;
@@ -1417,7 +1426,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
                                       reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS),
                                       (int)threadIdx.x);
 #ifdef LRL_ENV_DEBUG
-        g_env_dbg[((size_t)(blockIdx.x * ENVS + (int)(threadIdx.x >> 2)) * 64 + s) * 8 + 1] = th.sep;
+        g_env_dbg[((size_t)(env_block() * ENVS + (int)(threadIdx.x >> 2)) * 64 + s) * 8 + 1] = th.sep;
 #endif
         if (th.sep < P.contact_offset) {
           M.sph(s, 3) = th.n.x;
@@ -1799,7 +1808,8 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   const lrl_env_params& P = K->p;
   const int lane = threadIdx.x;
   const int es = lane >> 2, ql = lane & 3;  // env slot, owned leg
-  const int e = blockIdx.x * ENVS + es;
+  const int blk = env_block();
+  const int e = blk * ENVS + es;
   const int N = S.stride;
   const bool valid = e < S.n;
   const uint64_t genv = (uint64_t)(S.env_offset + e);
@@ -2318,7 +2328,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   LRL_PROF(6)  // contact forces + post_physics_step + SoA write-back
   // ---- AoS tiles (obs, priv) and the history shift: coalesced over the wave's contiguous rows ----
   __syncthreads();
-  const size_t row0 = (size_t)blockIdx.x * ENVS;
+  const size_t row0 = (size_t)blk * ENVS;
   {
     float* og = S.obs + row0 * NO;
     for (int i = lane; i < ENVS * NO; i += BLOCK) og[i] = otile[i];

@@ -42,16 +42,6 @@ constexpr int MAX_LAT = 32;
 __device__ __forceinline__ float delu(float h) { return h > 0.f ? 1.f : h + 1.f; }  // elu'(y) from h = elu(y)
 
 // ---------------------------------------------------------------------------------------------------
-// gather obs rows into the actor/critic input X = [obs | latent | 0-pad] ([B][64])
-__global__ void ppo_prep_kernel(const float* __restrict__ obs, const int64_t* __restrict__ rows, int B, int no,
-                                int xs, float* __restrict__ X) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)B * xs) return;
-  const int b = (int)(i / xs), c = (int)(i - (int64_t)b * xs);
-  X[i] = c < no ? obs[(rows ? rows[b] : (int64_t)b) * no + c] : 0.f;
-}
-
-// ---------------------------------------------------------------------------------------------------
 // PPO head: mu = H3a W4a^T + b4a, v = H3c W4c^T + b4c, Normal(mu, std) log-prob / entropy, clipped
 // surrogate, clipped value loss, KL(old || new) (ppo.py:98-147, actor_critic.py:126-135); gradient of
 // loss = surrogate + c_v value - c_e entropy w.r.t. mu, v and std; dH3 = (dmu W4a | dv W4c) * elu'(H3);
@@ -79,11 +69,14 @@ __host__ __device__ constexpr int hp_kl(int na) { return na * HEAD_W + na + HEAD
 __host__ __device__ constexpr int hp_len(int na) { return hp_kl(na) + 3; }  // kl, surrogate, value
 
 __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
-  // phases: (0) stage H3 / head weights  (1) mu, v  (2) per (row, action): log-prob and KL terms
-  // (3) per row: ratio, clipped surrogate, clipped value loss, their gradients  (4) per (row, action):
-  // d loss / d mu, d loss / d std  (5) per column: dH3 and the head weight-gradient partials
+  // phases: (0) stage H3 / head weights and the minibatch rows' indices, then issue the gathered per-(row, action)
+  // and per-row loads (old actions / mu / sigma, advantage, old log-prob, target value, return) so their latency
+  // hides under (1) mu, v; (2) per (row, action): log-prob and KL terms  (3) per row: ratio, clipped surrogate,
+  // clipped value loss, their gradients  (4) per (row, action): d loss / d mu, d loss / d std  (5) per column: dH3
+  // and the head weight-gradient partials.  Two global round trips in all (rows, then the gathered rows).
   constexpr int HP = 2 * HEAD_W + 1;  // odd pitch: row-per-lane reads conflict-free
   constexpr int NA = HEAD_NA;
+  constexpr int NG = (HEAD_ROWS * NA + HEAD_THREADS - 1) / HEAD_THREADS;  // gathered (row, action) items per thread
   __shared__ float H[HEAD_ROWS][HP];
   __shared__ float W4[NA + 1][HEAD_W];
   __shared__ float MU[HEAD_ROWS][NA + 1];   // mu_j, then d = a_j - mu_j
@@ -93,9 +86,13 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
   __shared__ float DR[HEAD_ROWS][2];        // d loss / d logp, d loss / d v
   __shared__ float SC[HEAD_ROWS][3];        // kl, surrogate, value loss per row
   __shared__ float SD[3][NA];               // std, log std, 1/std^2
+  __shared__ float GA[3][HEAD_ROWS][NA];    // gathered old actions, old mu, old sigma
+  __shared__ float GR[4][HEAD_ROWS];        // gathered advantage, old log-prob, target value, return
+  __shared__ int64_t RW[HEAD_ROWS];
   const int t = threadIdx.x;
   const int r0 = blockIdx.x * HEAD_ROWS;
   const int nrows = min(HEAD_ROWS, a.B - r0);
+  if (t < HEAD_ROWS) RW[t] = t < nrows ? a.rows[r0 + t] : a.rows[r0];
   if (t < NA) {
     const float sd = a.stdv[t];
     SD[0][t] = sd;
@@ -122,6 +119,23 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
     W4[j][k] = j < NA ? a.w4a[j * HEAD_W + k] : a.w4c[k];
   }
   __syncthreads();
+  // (0b) the gathered loads, all issued before (1) uses none of them
+  float ga[3][NG], gr = 0.f;
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    const int i = t + u * HEAD_THREADS;
+    const int r = i / NA, j = i - r * NA;
+    const bool ok = i < HEAD_ROWS * NA;
+    const int64_t o = RW[ok ? r : 0] * NA + j;
+    ga[0][u] = ok ? a.actions[o] : 0.f;
+    ga[1][u] = ok ? a.old_mu[o] : 0.f;
+    ga[2][u] = ok ? a.old_sigma[o] : 1.f;
+  }
+  if (t < 4 * HEAD_ROWS) {
+    const int q = t / HEAD_ROWS, r = t - q * HEAD_ROWS;
+    const float* src = q == 0 ? a.adv : q == 1 ? a.old_logp : q == 2 ? a.tv : a.ret;
+    gr = src[RW[r]];
+  }
   // (1) thread (r, q): actions q, q+8 and an eighth of the value dot
   {
     const int r = t & (HEAD_ROWS - 1), q = t / HEAD_ROWS;
@@ -134,17 +148,27 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
     for (int k = q * (HEAD_W / 8); k < (q + 1) * (HEAD_W / 8); ++k) s = fmaf(H[r][HEAD_W + k], W4[NA][k], s);
     VP[r][q] = s;
   }
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    const int i = t + u * HEAD_THREADS;
+    if (i < HEAD_ROWS * NA) {
+      const int r = i / NA, j = i - r * NA;
+      GA[0][r][j] = ga[0][u];
+      GA[1][r][j] = ga[1][u];
+      GA[2][r][j] = ga[2][u];
+    }
+  }
+  if (t < 4 * HEAD_ROWS) GR[t / HEAD_ROWS][t & (HEAD_ROWS - 1)] = gr;
   __syncthreads();
   // (2) per (row, action): Normal log-prob term and KL(old || new) term (ppo.py:111-114)
   for (int i = t; i < HEAD_ROWS * NA; i += HEAD_THREADS) {
     const int r = i / NA, j = i - r * NA;
     float lp = 0.f, kt = 0.f, d = 0.f;
     if (r < nrows) {
-      const int64_t g = a.rows[r0 + r];
       const float s = SD[0][j], mu = MU[r][j];
-      d = a.actions[g * NA + j] - mu;
+      d = GA[0][r][j] - mu;
       lp = -(d * d) / (2.f * (s * s)) - SD[1][j] - LOG_SQRT_2PI;
-      const float so = a.old_sigma[g * NA + j], dm = a.old_mu[g * NA + j] - mu;
+      const float so = GA[2][r][j], dm = GA[1][r][j] - mu;
       kt = logf(s / so + 1.e-5f) + (so * so + dm * dm) / (2.f * (s * s)) - 0.5f;
     }
     MU[r][j] = d;
@@ -158,7 +182,6 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
     const int r = t;
     float kl = 0.f, surr_loss = 0.f, vloss = 0.f, dv = 0.f, dlogp = 0.f;
     if (r < nrows) {
-      const int64_t g = a.rows[r0 + r];
       const float v = (((VP[r][0] + VP[r][1]) + (VP[r][2] + VP[r][3])) + ((VP[r][4] + VP[r][5]) + (VP[r][6] + VP[r][7]))) +
                       a.b4c[0];
       float logp = 0.f;
@@ -167,8 +190,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
         logp += LP[r][j];
         kl += KT[r][j];
       }
-      const float adv = a.adv[g];
-      const float ratio = expf(logp - a.old_logp[g]);
+      const float adv = GR[0][r];
+      const float ratio = expf(logp - GR[1][r]);
       const float surr = -adv * ratio;
       const float rc = fminf(fmaxf(ratio, 1.f - a.clip), 1.f + a.clip);
       const float surr_c = -adv * rc;
@@ -180,7 +203,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
       const float dratio = -adv * ga + (in_rng ? -adv * gb : 0.f);
       dlogp = dratio * ratio;
       // value loss (ppo.py:133-143)
-      const float tv = a.tv[g], ret = a.ret[g];
+      const float tv = GR[2][r], ret = GR[3][r];
       const float gv = a.vcoef * invB;
       if (a.clipped_value) {
         const float dvt = v - tv;
@@ -444,9 +467,12 @@ struct AdaptHeadArgs {
 };
 
 __global__ __launch_bounds__(HEAD_THREADS) void adapt_head_kernel(AdaptHeadArgs a) {
+  // every global load (HD2 tile, weights, the encoder targets) issued up front; the prediction dots spread over
+  // (row, output) pairs; per-row squared errors summed in output order (as a sequential loop would)
   __shared__ float HS[HEAD_ROWS][MAX_LAT + 1];
   __shared__ float DP[HEAD_ROWS][MAX_LAT + 1];
   __shared__ float WS[MAX_LAT][MAX_LAT + 1];
+  __shared__ float TG[HEAD_ROWS][MAX_LAT + 1];  // targets, then squared errors
   __shared__ float ERR[HEAD_ROWS];
   const int t = threadIdx.x;
   const int r0 = blockIdx.x * HEAD_ROWS;
@@ -456,23 +482,29 @@ __global__ __launch_bounds__(HEAD_THREADS) void adapt_head_kernel(AdaptHeadArgs 
     HS[r][c] = r < nrows ? a.hd2[(int64_t)(r0 + r) * a.ldh + c] : 0.f;
   }
   for (int i = t; i < a.L * a.H; i += HEAD_THREADS) WS[i / a.H][i % a.H] = a.w[i];
+  for (int i = t; i < HEAD_ROWS * a.L; i += HEAD_THREADS) {
+    const int r = i / a.L, j = i - r * a.L;
+    TG[r][j] = r < nrows ? a.tgt[(int64_t)(r0 + r) * a.ldt + j] : 0.f;
+  }
   __syncthreads();
   const float scale = 2.f / ((float)a.B * (float)a.L);
-  if (t < HEAD_ROWS) {
-    const int r = t;
-    float e = 0.f;
-    for (int j = 0; j < a.L; ++j) {
-      float d = 0.f;
-      if (r < nrows) {
-        float s = 0.f;
-        for (int k = 0; k < a.H; ++k) s = fmaf(HS[r][k], WS[j][k], s);
-        const float pred = s + a.b[j];
-        d = pred - a.tgt[(int64_t)(r0 + r) * a.ldt + j];
-      }
-      e += d * d;
-      DP[r][j] = scale * d;
+  for (int i = t; i < HEAD_ROWS * a.L; i += HEAD_THREADS) {
+    const int r = i / a.L, j = i - r * a.L;
+    float d = 0.f;
+    if (r < nrows) {
+      float s = 0.f;
+      for (int k = 0; k < a.H; ++k) s = fmaf(HS[r][k], WS[j][k], s);
+      const float pred = s + a.b[j];
+      d = pred - TG[r][j];
     }
-    ERR[r] = e;
+    TG[r][j] = d * d;
+    DP[r][j] = scale * d;
+  }
+  __syncthreads();
+  if (t < HEAD_ROWS) {
+    float e = 0.f;
+    for (int j = 0; j < a.L; ++j) e += TG[t][j];
+    ERR[t] = e;
   }
   __syncthreads();
   float* P = a.part + (int64_t)blockIdx.x * a.part_len;
@@ -758,6 +790,16 @@ struct G {
     p.ga = ga; p.gb = gw; p.gc = gc; p.gbias = gbias;
     rc = gemm_launch(p, GEMM_NT, elu ? EPI_BIAS_ELU : EPI_BIAS, groups, st);
   }
+  // the latent layer writing whole actor / critic input rows X = [obs(rows) | latent | 0 .. XS) (GemmP::cat)
+  void nt_cat(const float* A, int64_t lda, const float* W, int64_t ldw, float* X, int XS, const float* bias, int M,
+              int N, int K, const float* obs, const int64_t* obs_rows, int num_obs) {
+    if (rc) return;
+    GemmP p{};
+    p.A = A; p.lda = lda; p.B = W; p.ldb = ldw; p.C = X + num_obs; p.ldc = XS; p.bias = bias;
+    p.M = M; p.N = N; p.K = K; p.splits = 1;
+    p.cat = obs; p.cat_rows = obs_rows; p.ld_cat = num_obs; p.cat_cols = num_obs; p.cat_pad = XS - num_obs - N;
+    rc = gemm_launch(p, GEMM_NT, EPI_BIAS, 1, st);
+  }
   // dX = dY W (* elu'(aux) if aux)
   void nn(const float* dY, int64_t ldy, const float* W, int64_t ldw, float* dX, int64_t ldx, const float* aux,
           int64_t ldaux, int M, int N, int K, int groups = 1, int64_t gy = 0, int64_t gw = 0, int64_t gx = 0,
@@ -857,11 +899,10 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
-                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
   g.nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1, nt.enc_h0, true);
-  g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, false);
+  g.nt_cat(P.he2, nt.enc_h1, w + nt.e3w, nt.enc_h1, P.xa, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, obs, nullptr,
+           nt.num_obs);
   g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, XS, true);  // see phase 1
   g.nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true, 2,
        nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);
@@ -923,8 +964,6 @@ extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* para
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
-                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   if (hld >= hpad && hld % 4 == 0 && ((uintptr_t)hist & 15) == 0 && hpad != nt.num_hist) {
     const int64_t cnt = (int64_t)nt.ad_h0 * hpad;
     hipLaunchKernelGGL(pad_cols_kernel, dim3((unsigned)std::min<int64_t>((cnt + 255) / 256, 1024)), dim3(256), 0, st,
@@ -934,7 +973,7 @@ extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* para
     g.nt(hist, hld, nullptr, w + nt.d1w, nt.num_hist, P.hd1, nt.ad_h0, w + nt.d1b, n, nt.ad_h0, nt.num_hist, true);
   }
   g.nt(P.hd1, nt.ad_h0, nullptr, w + nt.d2w, nt.ad_h0, P.hd2, HD2S, w + nt.d2b, n, nt.ad_h1, nt.ad_h0, true);
-  g.nt(P.hd2, HD2S, nullptr, w + nt.d3w, nt.ad_h1, P.xa + nt.num_obs, XS, w + nt.d3b, n, nt.latent, nt.ad_h1, false);
+  g.nt_cat(P.hd2, HD2S, w + nt.d3w, nt.ad_h1, P.xa, XS, w + nt.d3b, n, nt.latent, nt.ad_h1, obs, nullptr, nt.num_obs);
   // actor half of the grouped actor/critic layers (rows [0, h) of each grouped weight / bias)
   g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, nt.ac_h0, w + nt.b1, n, nt.ac_h0, XS, true);  // k-padding: see phase 1
   g.nt(P.h1, nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true);
@@ -968,11 +1007,11 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   const float* w = params;
   const int nx = n.num_obs + n.latent, XS = xs_of(n);
   // ---- forward ----
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)B * XS + 255) / 256)), dim3(256), 0, st, bt->obs,
-                     bt->rows, B, n.num_obs, XS, P.xa);
   g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
   g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
-  g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.xa + n.num_obs, XS, w + n.e3b, B, n.latent, n.enc_h1, false);
+  // X = [obs(rows) | latent | 0] written by the latent layer's epilogue
+  g.nt_cat(P.he2, n.enc_h1, w + n.e3w, n.enc_h1, P.xa, XS, w + n.e3b, B, n.latent, n.enc_h1, bt->obs, bt->rows,
+           n.num_obs);
   // k runs over all XS columns of X: columns nx..XS-1 are zero, so the extra products (with the next
   // row's first weights, or the first biases after the last row — finite values) add exactly 0, and the
   // product takes the unguarded float4 path

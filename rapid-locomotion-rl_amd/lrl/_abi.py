@@ -159,7 +159,8 @@ def lib():
         L = C.CDLL(LIB_PATH)
         L.lrl_build_hash.restype = C.c_char_p
         built, want = L.lrl_build_hash().decode(), source_hash()
-        if built != want:
+        # (an explicit LRL_LIB — an instrumented or A/B development build — is loaded as named)
+        if built != want and not os.environ.get("LRL_LIB"):
             raise RuntimeError(f"{LIB_PATH} was built from other sources (hash {built}, tree {want}); "
                                "rebuild it: __graft_entry__.build()")
         L.lrl_last_error.restype = C.c_char_p

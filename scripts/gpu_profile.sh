@@ -14,6 +14,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/l
 find /tmp/lrlprof/trace -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 KT=$(find /tmp/lrlprof/trace -name "*kernel_trace.csv" | head -n 1)
 python3 "$ROOT/scripts/trace_reduce.py" "$KT" > "$OUT/kernel_by_grid.csv"
+python3 "$ROOT/scripts/timeline.py" "$KT" > "$OUT/timeline.csv"
 [ "${NO_PMC:-0}" = 1 ] && exit 0
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d /tmp/lrlprof/$C -o run -- \
