@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define LRL_ABI_VERSION 1
+#define LRL_ABI_VERSION 2
 
 #define LRL_OK 0
 #define LRL_E_INVALID (-1)  /* bad argument / unsupported configuration */
@@ -438,10 +438,12 @@ int32_t lrl_ppo_optimizer_step(const lrl_ppo_net* net, float* params, const floa
                                float* exp_avg_sq, int64_t step, float grad_scale, const lrl_ppo_hparams* hp,
                                void* workspace, lrl_ppo_ctrl* ctrl, void* stream);
 /* Adaptation-module regression (ppo.py:157-171): forward/backward -> grads[adapt_begin:adapt_end),
- * ctrl->mb[2] = MSE. */
-int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, const float* params, float* grads,
-                                            const lrl_ppo_batch* batch, void* workspace, lrl_ppo_ctrl* ctrl,
-                                            void* stream);
+ * ctrl->mb[2] = MSE.  The encoder target reads the encoder weights at enc_params + net->e1w .. (a snapshot
+ * of the flat parameters' encoder range taken after the optimiser step; NULL = params), the adaptation module
+ * its own weights in params. */
+int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, const float* params, const float* enc_params,
+                                            float* grads, const lrl_ppo_batch* batch, void* workspace,
+                                            lrl_ppo_ctrl* ctrl, void* stream);
 /* Adam step of the adaptation optimiser (fixed lr) over the adaptation region. */
 int32_t lrl_ppo_adaptation_step(const lrl_ppo_net* net, float* params, const float* grads, float* exp_avg,
                                 float* exp_avg_sq, int64_t step, double lr, float grad_scale,

@@ -49,13 +49,6 @@ struct GemmP {
   int64_t lda, ldb, ldc, ld_aux;
   int64_t ga, gb, gc, gbias, gaux;  // per-group element offsets
   int64_t part_stride;              // EPI_PARTIAL: elements between split slices of C ([split][group][M][N])
-  // optional row concatenation (register-staged path, single group): output row m also gets
-  // C[m][-cat_cols .. -1] = cat[cat_rows ? cat_rows[m] : m][0 .. cat_cols) and C[m][N .. N + cat_pad) = 0 — the
-  // encoder's last layer writes the whole actor / critic input row X = [obs | latent | 0] (no separate gather pass)
-  const float* cat;
-  const int64_t* cat_rows;
-  int64_t ld_cat;
-  int cat_cols, cat_pad;
 };
 
 // layout: bit0 = A m-contiguous, bit1 = B n-contiguous

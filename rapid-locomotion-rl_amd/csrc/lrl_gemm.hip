@@ -202,21 +202,6 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
   const bool do_bsum = EPI == EPI_PARTIAL && p.bias_part != nullptr && tn_ == 0;
   float bsum = 0.f;
 
-  // GemmP::cat values of this tile's rows, loaded up front so their latency hides under the main loop: GTHREADS / BM
-  // threads per row, CATV floats each (cat_cols <= CATV * GTHREADS / BM, else the epilogue loops)
-  constexpr int CAT_TPR = GTHREADS / BM > 0 ? GTHREADS / BM : 1;
-  constexpr int CATV = (48 + CAT_TPR - 1) / CAT_TPR;
-  const bool catv_ok = p.cat != nullptr && tn_ == 0 && BM <= GTHREADS && p.cat_cols <= CATV * CAT_TPR;
-  const int cat_row = m0 + (int)threadIdx.x / CAT_TPR, cat_c0 = (int)threadIdx.x % CAT_TPR;
-  float catv[CATV];
-  if (catv_ok && cat_row < p.M) {
-    const float* src = p.cat + (p.cat_rows ? p.cat_rows[cat_row] : (int64_t)cat_row) * p.ld_cat;
-#pragma unroll
-    for (int u = 0; u < CATV; ++u) {
-      const int c = cat_c0 + u * CAT_TPR;
-      catv[u] = c < p.cat_cols ? src[c] : 0.f;
-    }
-  }
   float4 ra[T::NA], rb[T::NB];
   Stager<BM, T::NA, T::AMC> sa;
   Stager<BN, T::NB, T::BNC> sb;
@@ -332,26 +317,6 @@ __global__ __launch_bounds__(GTHREADS) void gemm_kernel(GemmP p) {
           C[(int64_t)row * p.ldc + col] = v;
         }
       }
-    }
-  }
-  if (p.cat != nullptr && tn_ == 0) {  // [obs | C | 0] rows (GemmP::cat), values loaded before the main loop
-    if (catv_ok) {
-#pragma unroll
-      for (int u = 0; u < CATV; ++u) {
-        const int c = cat_c0 + u * CAT_TPR;
-        if (cat_row < p.M && c < p.cat_cols) C[(int64_t)cat_row * p.ldc + c - p.cat_cols] = catv[u];
-      }
-    } else {
-      for (int i = threadIdx.x; i < BM * 16; i += GTHREADS) {
-        const int r = i >> 4, c0 = i & 15, row = m0 + r;
-        if (row >= p.M) continue;
-        const float* src = p.cat + (p.cat_rows ? p.cat_rows[row] : (int64_t)row) * p.ld_cat;
-        for (int c = c0; c < p.cat_cols; c += 16) C[(int64_t)row * p.ldc + c - p.cat_cols] = src[c];
-      }
-    }
-    for (int i = threadIdx.x; i < BM * p.cat_pad; i += GTHREADS) {
-      const int r = i / p.cat_pad, row = m0 + r;
-      if (row < p.M) C[(int64_t)row * p.ldc + p.N + (i - r * p.cat_pad)] = 0.f;
     }
   }
   // bias partial layout [split][group][M] (contiguous per split, like the C partials)
@@ -982,9 +947,8 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   if (trace)
     fprintf(stderr, "gemm layout=%d epi=%d M=%d N=%d K=%d groups=%d splits=%d avec=%d bvec=%d arows=%d brows=%d\n",
             layout, epi, p.M, p.N, p.K, groups, p.splits, p.avec, p.bvec, p.a_rows != nullptr, p.b_rows != nullptr);
-  if (p.cat != nullptr && (groups != 1 || layout != GEMM_NT || bn < p.N)) return LRL_E_INVALID;
   // LDS-DMA path: batch-major product, every tile interior, float4-aligned operands, single split
-  if (p.cat == nullptr && layout != GEMM_TN && p.splits == 1 && p.M % 64 == 0 && p.N % 64 == 0 && p.K % 16 == 0 && p.K >= 32 &&
+  if (layout != GEMM_TN && p.splits == 1 && p.M % 64 == 0 && p.N % 64 == 0 && p.K % 16 == 0 && p.K >= 32 &&
       p.avec == 4 && p.bvec == 4 && epi != EPI_PARTIAL && (layout == GEMM_NT || layout == GEMM_NN)) {
     dim3 g1((p.M / 64) * (p.N / 64) * groups);
 #ifndef LRL_GLDS_BK32
@@ -1019,7 +983,7 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   }
   // thin output (N <= 32): B staged whole in LDS, k split over the workgroup's waves
   const int kb128 = p.K / 128;
-  if (p.cat == nullptr && layout != GEMM_TN && p.splits == 1 && p.N <= 32 && p.K % 128 == 0 && p.avec == 4 && p.M >= 256 &&
+  if (layout != GEMM_TN && p.splits == 1 && p.N <= 32 && p.K % 128 == 0 && p.avec == 4 && p.M >= 256 &&
       (kb128 == 4 || kb128 == 8) &&  // (shorter k: the register-staged 128 x 32 tile is as fast)
       (epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_ELU)) {
     int trc = LRL_E_INVALID;

@@ -42,6 +42,16 @@ constexpr int MAX_LAT = 32;
 __device__ __forceinline__ float delu(float h) { return h > 0.f ? 1.f : h + 1.f; }  // elu'(y) from h = elu(y)
 
 // ---------------------------------------------------------------------------------------------------
+// gather obs rows into the actor/critic input X = [obs | latent | 0-pad] ([B][64])
+__global__ void ppo_prep_kernel(const float* __restrict__ obs, const int64_t* __restrict__ rows, int B, int no,
+                                int xs, float* __restrict__ X) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * xs) return;
+  const int b = (int)(i / xs), c = (int)(i - (int64_t)b * xs);
+  X[i] = c < no ? obs[(rows ? rows[b] : (int64_t)b) * no + c] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------------
 // PPO head: mu = H3a W4a^T + b4a, v = H3c W4c^T + b4c, Normal(mu, std) log-prob / entropy, clipped
 // surrogate, clipped value loss, KL(old || new) (ppo.py:98-147, actor_critic.py:126-135); gradient of
 // loss = surrogate + c_v value - c_e entropy w.r.t. mu, v and std; dH3 = (dmu W4a | dv W4c) * elu'(H3);
@@ -790,16 +800,6 @@ struct G {
     p.ga = ga; p.gb = gw; p.gc = gc; p.gbias = gbias;
     rc = gemm_launch(p, GEMM_NT, elu ? EPI_BIAS_ELU : EPI_BIAS, groups, st);
   }
-  // the latent layer writing whole actor / critic input rows X = [obs(rows) | latent | 0 .. XS) (GemmP::cat)
-  void nt_cat(const float* A, int64_t lda, const float* W, int64_t ldw, float* X, int XS, const float* bias, int M,
-              int N, int K, const float* obs, const int64_t* obs_rows, int num_obs) {
-    if (rc) return;
-    GemmP p{};
-    p.A = A; p.lda = lda; p.B = W; p.ldb = ldw; p.C = X + num_obs; p.ldc = XS; p.bias = bias;
-    p.M = M; p.N = N; p.K = K; p.splits = 1;
-    p.cat = obs; p.cat_rows = obs_rows; p.ld_cat = num_obs; p.cat_cols = num_obs; p.cat_pad = XS - num_obs - N;
-    rc = gemm_launch(p, GEMM_NT, EPI_BIAS, 1, st);
-  }
   // dX = dY W (* elu'(aux) if aux)
   void nn(const float* dY, int64_t ldy, const float* W, int64_t ldw, float* dX, int64_t ldx, const float* aux,
           int64_t ldaux, int M, int N, int K, int groups = 1, int64_t gy = 0, int64_t gw = 0, int64_t gx = 0,
@@ -899,10 +899,11 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
+                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
   g.nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1, nt.enc_h0, true);
-  g.nt_cat(P.he2, nt.enc_h1, w + nt.e3w, nt.enc_h1, P.xa, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, obs, nullptr,
-           nt.num_obs);
+  g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, false);
   g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, XS, true);  // see phase 1
   g.nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true, 2,
        nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);
@@ -964,6 +965,8 @@ extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* para
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
+                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   if (hld >= hpad && hld % 4 == 0 && ((uintptr_t)hist & 15) == 0 && hpad != nt.num_hist) {
     const int64_t cnt = (int64_t)nt.ad_h0 * hpad;
     hipLaunchKernelGGL(pad_cols_kernel, dim3((unsigned)std::min<int64_t>((cnt + 255) / 256, 1024)), dim3(256), 0, st,
@@ -973,7 +976,7 @@ extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* para
     g.nt(hist, hld, nullptr, w + nt.d1w, nt.num_hist, P.hd1, nt.ad_h0, w + nt.d1b, n, nt.ad_h0, nt.num_hist, true);
   }
   g.nt(P.hd1, nt.ad_h0, nullptr, w + nt.d2w, nt.ad_h0, P.hd2, HD2S, w + nt.d2b, n, nt.ad_h1, nt.ad_h0, true);
-  g.nt_cat(P.hd2, HD2S, w + nt.d3w, nt.ad_h1, P.xa, XS, w + nt.d3b, n, nt.latent, nt.ad_h1, obs, nullptr, nt.num_obs);
+  g.nt(P.hd2, HD2S, nullptr, w + nt.d3w, nt.ad_h1, P.xa + nt.num_obs, XS, w + nt.d3b, n, nt.latent, nt.ad_h1, false);
   // actor half of the grouped actor/critic layers (rows [0, h) of each grouped weight / bias)
   g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, nt.ac_h0, w + nt.b1, n, nt.ac_h0, XS, true);  // k-padding: see phase 1
   g.nt(P.h1, nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true);
@@ -1007,11 +1010,11 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   const float* w = params;
   const int nx = n.num_obs + n.latent, XS = xs_of(n);
   // ---- forward ----
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)B * XS + 255) / 256)), dim3(256), 0, st, bt->obs,
+                     bt->rows, B, n.num_obs, XS, P.xa);
   g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
   g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
-  // X = [obs(rows) | latent | 0] written by the latent layer's epilogue
-  g.nt_cat(P.he2, n.enc_h1, w + n.e3w, n.enc_h1, P.xa, XS, w + n.e3b, B, n.latent, n.enc_h1, bt->obs, bt->rows,
-           n.num_obs);
+  g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.xa + n.num_obs, XS, w + n.e3b, B, n.latent, n.enc_h1, false);
   // k runs over all XS columns of X: columns nx..XS-1 are zero, so the extra products (with the next
   // row's first weights, or the first biases after the last row — finite values) add exactly 0, and the
   // product takes the unguarded float4 path
@@ -1096,9 +1099,9 @@ extern "C" int32_t lrl_ppo_optimizer_step(const lrl_ppo_net* net, float* params,
   return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_optimizer_step: launch failed");
 }
 
-extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, const float* params, float* grads,
-                                                       const lrl_ppo_batch* bt, void* workspace, lrl_ppo_ctrl* ctrl,
-                                                       void* stream) {
+extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, const float* params,
+                                                       const float* enc_params, float* grads, const lrl_ppo_batch* bt,
+                                                       void* workspace, lrl_ppo_ctrl* ctrl, void* stream) {
   if (int rc = check_net(net)) return rc;
   if (!bt || !params || !grads || !workspace || !ctrl || bt->batch <= 0)
     return lrl_set_error(LRL_E_INVALID, "lrl_ppo_adaptation_forward_backward: null argument");
@@ -1108,10 +1111,12 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
   hipStream_t st = static_cast<hipStream_t>(stream);
   G g{st, P.part + P.part_floats};
   const float* w = params;
-  // target = env_factor_encoder(priv) with the just-updated weights (torch.no_grad, ppo.py:159-160)
-  g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
-  g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
-  g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.tgt, LATS, w + n.e3b, B, n.latent, n.enc_h1, false);
+  // target = env_factor_encoder(priv) with the just-updated weights (torch.no_grad, ppo.py:159-160), read from
+  // enc_params (a snapshot of them taken right after the optimiser step, so the next step may proceed) or params
+  const float* we = enc_params ? enc_params : params;
+  g.nt(bt->priv, n.num_priv, bt->rows, we + n.e1w, n.num_priv, P.he1, n.enc_h0, we + n.e1b, B, n.enc_h0, n.num_priv, true);
+  g.nt(P.he1, n.enc_h0, nullptr, we + n.e2w, n.enc_h0, P.he2, n.enc_h1, we + n.e2b, B, n.enc_h1, n.enc_h0, true);
+  g.nt(P.he2, n.enc_h1, nullptr, we + n.e3w, n.enc_h1, P.tgt, LATS, we + n.e3b, B, n.latent, n.enc_h1, false);
   // prediction = adaptation_module(obs_history)
   const int hld = bt->hist_ld ? bt->hist_ld : n.num_hist, hpad = hist_pad(n.num_hist);
   if (hld < n.num_hist) return lrl_set_error(LRL_E_INVALID, "lrl_ppo_adaptation: hist_ld < num_hist");

@@ -208,22 +208,28 @@ class PPO:
         scale = 1.0 / world
         # The adaptation-module regression of minibatch i (phases 3 / 4) reads the encoder weights phase 2 of i wrote
         # and touches only the adaptation module's parameters, gradients and Adam moments, which phases 1 / 2 never
-        # read or write.  So it runs on a second stream, overlapping phases 1 / 2 of minibatch i + 1 (the GEMM tails
-        # and small launches of one chain leave the CUs the other fills); phase 2 of i + 1 waits for it, since it
-        # overwrites the encoder weights phase 3 of i reads.  Each chain keeps its own launch order, so the result is
-        # bit-identical to the sequential order of ppo.py:94-178.
+        # read or write.  So it runs on a second stream, overlapping phases 1 / 2 of the next minibatches (the GEMM
+        # tails and small launches of one chain leave the CUs the other fills).  Its encoder target reads a snapshot
+        # of the encoder weights copied right after phase 2 of i (two buffers, alternating), so phase 2 of i + 1 may
+        # overwrite the live ones without waiting for it; the copy for i + 2 waits until phase 3 of i has read its
+        # buffer.  Each chain keeps its own launch order, so the result is bit-identical to the sequential order of
+        # ppo.py:94-178.
         cur = torch.cuda.current_stream(params.device)
         if self.overlap_adaptation:
             sb = st.get("stream_b")
             if sb is None:
                 sb = st["stream_b"] = torch.cuda.Stream(params.device)
             stream_b, ws_b = C.c_void_p(sb.cuda_stream), st["ws_b"]
+            if "enc_snap" not in st:
+                st["enc_snap"] = [torch.zeros(net.total, device=params.device) for _ in range(2)]
+            e0, e1 = net.e1w, net.std_off  # the encoder's weights and biases: one contiguous range
         else:
             sb, stream_b, ws_b = cur, stream, ws
         # the adaptation chain's batch descriptor: the rows pointer of minibatch i must outlive the next C call
         batch_b = _abi.LrlPpoBatch()
         C.memmove(C.byref(batch_b), C.byref(batch), C.sizeof(batch))
-        adapt_done = None
+        read_done = [None, None]  # per snapshot buffer: phase 3 of the minibatch that last read it has run
+        k = 0
         for epoch in range(PPO_Args.num_learning_epochs):
             for i in range(nmb):
                 rows = indices[i * mb:(i + 1) * mb]
@@ -232,19 +238,23 @@ class PPO:
                                                       C.byref(hp), ptr(ws), ptr(ctrl), stream))
                 if world > 1:
                     dist.all_reduce(main)
-                if adapt_done is not None:
-                    cur.wait_event(adapt_done)
                 st["steps"][0] += 1
                 _abi.check(L.lrl_ppo_optimizer_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
                                                     C.c_int64(st["steps"][0]), C.c_float(scale), C.byref(hp),
                                                     ptr(ws), ptr(ctrl), stream))
                 if self.record_lr:
                     trace.append(ctrl[0].clone())
+                enc = None
                 if sb is not cur:
+                    snap = st["enc_snap"][k & 1]
+                    if read_done[k & 1] is not None:
+                        cur.wait_event(read_done[k & 1])
+                    snap[e0:e1].copy_(params[e0:e1])
+                    enc = ptr(snap)
                     sb.wait_stream(cur)
                 batch_b.rows = rows.data_ptr()
                 for _ in range(PPO_Args.num_adaptation_module_substeps):
-                    _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), ptr(params), ptr(grads),
+                    _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), ptr(params), enc, ptr(grads),
                                                                      C.byref(batch_b), ptr(ws_b), ptr(ctrl), stream_b))
                     if world > 1:
                         with torch.cuda.stream(sb):
@@ -255,8 +265,9 @@ class PPO:
                                                          C.c_double(PPO_Args.adaptation_module_learning_rate),
                                                          C.c_float(scale), C.byref(hp), ptr(ctrl), stream_b))
                 if sb is not cur:
-                    adapt_done = torch.cuda.Event()
-                    adapt_done.record(sb)
+                    read_done[k & 1] = torch.cuda.Event()
+                    read_done[k & 1].record(sb)
+                k += 1
         if sb is not cur:
             cur.wait_stream(sb)
             indices.record_stream(sb)

@@ -42,7 +42,7 @@ def union(ks):
     return busy
 
 
-print("iter,wall_ms,busy_ms,idle_ms,rollout_ms,update_ms,kernels,gaps_over_5us_ms")
+print("iter,wall_ms,busy_ms,idle_ms,rollout_ms,rollout_idle_ms,update_ms,update_idle_ms,kernels,gaps_over_5us_ms")
 for i, it in enumerate(iters):
     t0, t1 = it[0][0], max(e for _, e, _, _ in it)
     busy = union(it)
@@ -56,8 +56,11 @@ for i, it in enumerate(iters):
         if end is not None and s - end > 5000:
             gaps += s - end
         end = e if end is None else max(end, e)
+    r_idle = (first_upd - t0) - union([(s, min(e, first_upd), n, q) for s, e, n, q in roll])
+    u_idle = (t1 - first_upd) - union(upd) if upd else 0
     print(f"{i},{(t1 - t0) / 1e6:.3f},{busy / 1e6:.3f},{(t1 - t0 - busy) / 1e6:.3f},"
-          f"{(first_upd - t0) / 1e6:.3f},{(t1 - first_upd) / 1e6:.3f},{len(it)},{gaps / 1e6:.3f}")
+          f"{(first_upd - t0) / 1e6:.3f},{r_idle / 1e6:.3f},{(t1 - first_upd) / 1e6:.3f},{u_idle / 1e6:.3f},{len(it)},"
+          f"{gaps / 1e6:.3f}")
 # per-stream busy inside the updates of the last iterations
 per = defaultdict(int)
 for it in iters[-5:]:

@@ -267,8 +267,8 @@ def test_native_minibatch_gradients_match_autograd(padded_hist, no):
     L = _abi.lib()
     _abi.check(L.lrl_ppo_forward_backward(C.byref(net), p(ac._flat), p(grads), C.byref(batch), C.byref(hp), p(ws),
                                           p(ctrl), stream))
-    _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), p(ac._flat), p(grads), C.byref(batch), p(ws),
-                                                     p(ctrl), stream))
+    _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), p(ac._flat), None, p(grads), C.byref(batch),
+                                                     p(ws), p(ctrl), stream))
     torch.cuda.synchronize()
     mbf = ctrl.view(torch.float32)[8:12].tolist()  # value, surrogate, adaptation, (kl in grads)
     kl_native = grads[net.kl_slot].item()
