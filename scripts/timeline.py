@@ -12,7 +12,8 @@ with open(sys.argv[1]) as f:
         if "lrl::" not in r["Kernel_Name"]:
             continue
         q = r.get("Stream_Id") or r.get("Queue_Id") or "0"
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60], q))
+        grid = r.get("Grid_Size_X") or r.get("Grid_Size") or ""
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60] + "@" + grid, q))
 rows.sort()
 # iterations: an env-step launch that follows a non-env, non-act kernel of the update starts one
 iters, cur, in_update = [], [], False
@@ -70,3 +71,35 @@ for it in iters[-5:]:
     for q in set(k[3] for k in it):
         per[q] += union([k for k in it if k[3] == q and k[0] >= first_upd])
 print("update busy per stream over the last 5 iterations (ms):", {q: round(v / 1e6 / 5, 3) for q, v in per.items()})
+# one minibatch of the last full iteration's update, in launch order (stream, start offset, duration)
+if len(iters) >= 2:
+    it = iters[-2]
+    heads = [k for k in it if "ppo_head_kernel" in k[2]]
+    if len(heads) >= 3:
+        t0, t1 = heads[1][0], heads[2][0]
+        # from the end of the previous head's launch group to the next: the phase-1 tail, phase 2, phase 3/4 and
+        # the next phase-1 head
+        sel = [k for k in it if t0 - 2_000_000 <= k[0] < t1]
+        base = sel[0][0]
+        print("minibatch sequence: start_us,dur_us,stream,kernel")
+        for s, e, n, q in sel:
+            print(f"{(s - base) / 1e3:9.1f},{(e - s) / 1e3:7.1f},{q},{n}")
+# the largest idle gaps inside the last full iteration's rollout (what ran before / after each)
+if len(iters) >= 2:
+    it = sorted(iters[-2])
+    first_upd = next((s for s, _, n, _ in it if "ppo_head_kernel" in n), it[-1][1])
+    roll = [k for k in it if k[0] < first_upd]
+    gaps, end, prev = [], None, None
+    for k in roll:
+        if end is not None and k[0] > end:
+            gaps.append((k[0] - end, prev[2].split("(")[0][-40:], k[2].split("(")[0][-40:]))
+        if end is None or k[1] > end:
+            end, prev = k[1], k
+    gaps.sort(reverse=True)
+    print("rollout gaps: count", len(gaps), "total_us", round(sum(g[0] for g in gaps) / 1e3, 1))
+    agg = defaultdict(lambda: [0, 0])
+    for d, a, b in gaps:
+        agg[(a, b)][0] += d
+        agg[(a, b)][1] += 1
+    for (a, b), (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:12]:
+        print(f"  {d / 1e3:8.1f} us over {c:3d} gaps: after {a} -> before {b}")
