@@ -354,6 +354,13 @@ int32_t lrl_gae_partial(const float* rewards, const uint8_t* dones, const float*
                         float* workspace, double* stats /*[3] device*/, void* stream);
 int32_t lrl_adv_normalize(float* advantages, int64_t total, const double* stats /*[3] device*/, void* stream);
 
+/* PPO.process_env_step + RolloutStorage.add_transitions for the env outputs (ppo.py:76-88, rollout_storage.py:
+ * 57-71) in one launch: dst_rew = rew (+ gamma * values * time_out when time_outs != NULL), dst_done = done (bool
+ * bytes), dst_env_bins = env_bins (when given); all [n] device, the dst pointers = storage row t. */
+int32_t lrl_ppo_store_step(const float* rew, const uint8_t* done, const float* env_bins, const float* values,
+                           const uint8_t* time_outs, float gamma, int32_t n, float* dst_rew, uint8_t* dst_done,
+                           float* dst_env_bins, void* stream);
+
 /* ---------------- PPO update (ppo.py:94-178) ----------------
  * All ActorCritic parameters live in ONE flat fp32 buffer (the nn.Module's tensors are views of it);
  * gradients and the Adam moments (exp_avg / exp_avg_sq) are flat buffers of the same layout.  Actor and

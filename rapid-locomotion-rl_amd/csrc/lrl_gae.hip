@@ -139,3 +139,35 @@ extern "C" int32_t lrl_gae_partial(const float* rewards, const uint8_t* dones, c
 extern "C" int32_t lrl_adv_normalize(float* advantages, int64_t total, const double* stats, void* stream) {
   return adv_normalize(advantages, total, stats, (hipStream_t)stream);
 }
+
+// PPO.process_env_step + RolloutStorage.add_transitions (ppo.py:76-88, rollout_storage.py:57-71) of the env outputs
+// in one launch: rewards (+ gamma * V * time_out, the time-out bootstrap, when time_outs is given), dones (bool
+// bytes) and env_bins into storage row t.  The bootstrap is rounded as torch computes it: v * time_out, then
+// gamma * that, then the add (no fused multiply-add).
+namespace lrl {
+__global__ void store_step_kernel(const float* __restrict__ rew, const uint8_t* __restrict__ done,
+                                  const float* __restrict__ bins, const float* __restrict__ values,
+                                  const uint8_t* __restrict__ time_outs, float gamma, int32_t n,
+                                  float* __restrict__ dst_rew, uint8_t* __restrict__ dst_done,
+                                  float* __restrict__ dst_bins) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float r = rew[i];
+  if (time_outs) r = __fadd_rn(r, __fmul_rn(gamma, __fmul_rn(values[i], time_outs[i] ? 1.f : 0.f)));
+  dst_rew[i] = r;
+  dst_done[i] = done[i] ? 1 : 0;
+  if (bins) dst_bins[i] = bins[i];
+}
+}  // namespace lrl
+
+extern "C" int32_t lrl_ppo_store_step(const float* rew, const uint8_t* done, const float* env_bins,
+                                      const float* values, const uint8_t* time_outs, float gamma, int32_t n,
+                                      float* dst_rew, uint8_t* dst_done, float* dst_env_bins, void* stream) {
+  if (!rew || !done || !dst_rew || !dst_done || n < 0 || (env_bins && !dst_env_bins) || (time_outs && !values))
+    return lrl_set_error(LRL_E_INVALID, "lrl_ppo_store_step: bad argument");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(lrl::store_step_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, rew, done,
+                     env_bins, values, time_outs, gamma, n, dst_rew, dst_done, dst_env_bins);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, hipGetErrorString(e));
+}

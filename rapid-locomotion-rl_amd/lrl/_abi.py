@@ -172,7 +172,7 @@ def lib():
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
                      "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student", "lrl_sim_set_terrain",
                      "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms", "lrl_sim_inject_push_uniforms", "lrl_sim_timing",
-                     "lrl_sim_self_contact_stats"]:
+                     "lrl_sim_self_contact_stats", "lrl_ppo_store_step"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_ppo_workspace_bytes.restype = C.c_int64
         L.lrl_ppo_act_workspace_bytes.restype = C.c_int64

@@ -108,6 +108,10 @@ class PPO:
 
     def process_env_step(self, rewards, dones, infos):
         t = self.transition
+        if self.fused and self._store_step(rewards, dones, infos):  # one launch for the three storage rows
+            t.clear()
+            self.actor_critic.reset(dones)
+            return
         t.rewards = rewards.clone()
         t.dones = dones
         t.env_bins = infos["env_bins"]
@@ -116,6 +120,28 @@ class PPO:
         self.storage.add_transitions(t, fused=self.fused)
         t.clear()
         self.actor_critic.reset(dones)
+
+    def _store_step(self, rewards, dones, infos):
+        """process_env_step's rewards (+ the time-out bootstrap), dones and env bins into storage row `step` in one
+        launch (lrl_ppo_store_step); False (the torch form runs) for inputs outside its dtypes / layouts."""
+        s, t = self.storage, self.transition
+        bins, tout = infos["env_bins"], infos.get("time_outs")
+        n = s.num_envs
+        ok = lambda x, dt: (x.dtype == dt and x.is_cuda and x.is_contiguous() and x.numel() == n)
+        if not (ok(rewards, torch.float32) and ok(dones, torch.bool) and ok(bins, torch.float32)):
+            return False
+        if tout is not None and not (ok(tout, torch.bool) and ok(t.values, torch.float32)):
+            return False
+        if s.step >= s.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        i = s.step
+        p = lambda x: C.c_void_p(x.data_ptr()) if x is not None else None
+        stream = C.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+        _abi.check(_abi.lib().lrl_ppo_store_step(p(rewards), p(dones), p(bins), p(t.values if tout is not None else None),
+                                                 p(tout), C.c_float(PPO_Args.gamma), C.c_int32(n), p(s.rewards[i]),
+                                                 p(s.dones[i]), p(s.env_bins[i]), stream))
+        s.step += 1
+        return True
 
     def compute_returns(self, last_critic_obs, last_critic_privileged_obs):
         if self.fused:

@@ -1,5 +1,7 @@
 """Host-side cost of one rollout step of the bench workload (development tool): cProfile over Runner.learn's
-rollout loop (4096 Mini Cheetah envs), top functions by own time.  usage: python scripts/host_profile.py"""
+rollout loop, top functions by own time.  usage: python scripts/host_profile.py [mc|go1_rough]
+(mc: 4096 Mini Cheetah envs, flat, fork semantics — the headline; go1_rough: bench.py's secondary line, 4096 Go1
+envs on the curriculum trimesh with the upstream reset path)"""
 import cProfile
 import os
 import pstats
@@ -15,11 +17,20 @@ from lrl.env import LeggedRobotEnv  # noqa: E402
 from lrl.history import HistoryWrapper  # noqa: E402
 from lrl.ppo import runner as R  # noqa: E402
 
+which = sys.argv[1] if len(sys.argv) > 1 else "mc"
 cfg = lcfg.make_cfg()
-lcfg.config_mini_cheetah(cfg)
-cfg.env.num_envs = 4096
 R.RunnerArgs.save_interval = 0
-env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=1234))
+if which == "go1_rough":
+    lcfg.config_go1(cfg)
+    cfg.env.num_envs = 4096
+    cfg.terrain.mesh_type = "trimesh"
+    cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]
+    cfg.terrain.curriculum = True
+    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=4321, legacy_fork=False))
+else:
+    lcfg.config_mini_cheetah(cfg)
+    cfg.env.num_envs = 4096
+    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=1234))
 runner = R.Runner(env, device="cuda:0", seed=1234)
 runner.learn(2, init_at_random_ep_len=True)
 alg = runner.alg
@@ -54,4 +65,4 @@ rollout()
 torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(25)
+st.sort_stats("tottime").print_stats(40)

@@ -308,3 +308,36 @@ def test_native_minibatch_gradients_match_autograd(padded_hist, no):
         if err > 1e-4 * (ref.abs().max().item() + 1e-6) + 1e-7:
             bad.append(f"{name}: err {err:.3g} ref max {ref.abs().max().item():.3g} got max {got.abs().max().item():.3g}")
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.parametrize("with_timeouts", [False, True])
+def test_fused_store_step_matches_torch_form(with_timeouts):
+    """PPO.process_env_step on the native path (one lrl_ppo_store_step launch) writes exactly what the reference's
+    torch form writes (ppo.py:76-88, rollout_storage.py:57-71): rewards plus the time-out bootstrap
+    gamma * V * time_out, dones, env bins."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.ppo import PPO
+    N, T = 1000, 3
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    outs = []
+    for fused in (True, False):
+        alg = PPO(ActorCritic(42, 18, 630, 12).cuda(), device="cuda:0", fused=True)
+        alg.init_storage(N, T, [42], [18], [630], [12])
+        if not fused:
+            alg._store_step = lambda *a: False
+        g.manual_seed(4)
+        for _ in range(T):
+            alg.transition.values = torch.randn(N, 1, device="cuda:0", generator=g)
+            rew = torch.randn(N, device="cuda:0", generator=g)
+            dones = torch.rand(N, device="cuda:0", generator=g) < 0.3
+            infos = {"env_bins": torch.randint(0, 5202, (N,), device="cuda:0", generator=g).float()}
+            tout = torch.rand(N, device="cuda:0", generator=g) < 0.5
+            if with_timeouts:
+                infos["time_outs"] = tout
+            alg.transition.observations = None
+            alg.process_env_step(rew, dones, infos)
+        s = alg.storage
+        assert s.step == T
+        outs.append([s.rewards.clone(), s.dones.clone(), s.env_bins.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
