@@ -150,10 +150,15 @@ __global__ void store_step_kernel(const float* __restrict__ rew, const uint8_t* 
                                   const uint8_t* __restrict__ time_outs, float gamma, int32_t n,
                                   float* __restrict__ dst_rew, uint8_t* __restrict__ dst_done,
                                   float* __restrict__ dst_bins) {
+#pragma clang fp contract(off)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float r = rew[i];
-  if (time_outs) r = __fadd_rn(r, __fmul_rn(gamma, __fmul_rn(values[i], time_outs[i] ? 1.f : 0.f)));
+  if (time_outs) {
+    const float vt = values[i] * (time_outs[i] ? 1.f : 0.f);
+    const float b = gamma * vt;
+    r = r + b;
+  }
   dst_rew[i] = r;
   dst_done[i] = done[i] ? 1 : 0;
   if (bins) dst_bins[i] = bins[i];
