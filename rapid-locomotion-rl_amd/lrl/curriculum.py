@@ -67,6 +67,46 @@ class RewardThresholdCurriculum(GridCurriculum):
 
     def update(self, bin_inds, lin_vel_rewards, ang_vel_rewards, lin_vel_threshold, ang_vel_threshold,
                local_range=0.5):
+        """curriculum.py:105-115 with the same result, element for element.  The reference adds 0.2 (clipped to 1)
+        to the successful bins, then once per successful entry to every bin of its +-local_range neighbourhood —
+        a [3, n_ok, bins] comparison and a Python loop over the entries.  A bin's updates are all the same clipped
+        add, so only their COUNT matters: the neighbourhood is a product of per-axis memberships (the same float
+        comparisons on the same grid values), the counts are one einsum over the entries, and the clipped add is
+        applied count times per bin."""
+        self.episode_reward_lin[bin_inds] = lin_vel_rewards
+        self.episode_reward_ang[bin_inds] = ang_vel_rewards
+        ok = (lin_vel_rewards > lin_vel_threshold) * (ang_vel_rewards > ang_vel_threshold)
+        self.weights[bin_inds[ok]] = np.clip(self.weights[bin_inds[ok]] + 0.2, 0, 1)
+        centres = bin_inds[ok]
+        if len(centres) == 0:
+            return
+        if len(self.keys) != 3:  # (the einsum below is written for the three command axes)
+            for adj in self.get_local_bins(centres, range=local_range):
+                idx = np.array(adj.nonzero()[0])
+                self.weights[idx] = np.clip(self.weights[idx] + 0.2, 0, 1)
+            return
+        shape = tuple(self.ls[k] for k in self.keys)
+        cidx = np.unravel_index(centres, shape)
+        member = []
+        for d, k in enumerate(self.keys):
+            v = self.cfg[k]  # the axis' grid values (self.grid holds exactly these)
+            c = v[cidx[d]][:, None]
+            member.append(np.logical_and(v[None, :] >= c - local_range, v[None, :] <= c + local_range))
+        m01 = (member[0][:, :, None] & member[1][:, None, :]).reshape(len(centres), -1).astype(np.float64)
+        counts = (m01.T @ member[2].astype(np.float64)).reshape(-1)  # exact small integers
+        idx = np.flatnonzero(counts > 0)
+        cnt = counts[idx]
+        step = 1
+        while len(idx):  # the step-th add reaches the bins counted at least step times; 1.0 is a fixed point
+            w = np.clip(self.weights[idx] + 0.2, 0, 1)
+            self.weights[idx] = w
+            keep = (cnt > step) & (w < 1.0)
+            idx, cnt = idx[keep], cnt[keep]
+            step += 1
+
+    def _update_literal(self, bin_inds, lin_vel_rewards, ang_vel_rewards, lin_vel_threshold, ang_vel_threshold,
+                        local_range=0.5):
+        """curriculum.py:105-115 as written (the check for ``update``)."""
         self.episode_reward_lin[bin_inds] = lin_vel_rewards
         self.episode_reward_ang[bin_inds] = ang_vel_rewards
         ok = (lin_vel_rewards > lin_vel_threshold) * (ang_vel_rewards > ang_vel_threshold)
