@@ -1103,8 +1103,8 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
     return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: incomplete rollout store");
   const lrl_ppo_net& nt = *net;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  static const bool chain = getenv("LRL_ACT_CHAIN") != nullptr;  // the layer-by-layer form (A/B timing, tests)
-  if (!chain && act_fused_ok(nt)) {
+  static const bool fused = getenv("LRL_ACT_FUSED") != nullptr;  // (opt-in until measured on the GPU)
+  if (fused && act_fused_ok(nt)) {
     ActFusedArgs af{};
     af.w = params; af.net = nt; af.obs = obs; af.priv = priv; af.hist = hist; af.eps = eps; af.n = n;
     af.seed = seed; af.counter = counter; af.actions = actions; af.mu = mu; af.values = values; af.logp = logp;
