@@ -462,214 +462,6 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// The whole rollout act of the blind teacher policy (PPO.act, ppo.py:62-74 -> actor_critic.py:126-147,170-173) in
-// ONE launch: a workgroup takes 16 rows and runs encoder (18 -> 256 -> 128 -> 18), the actor / critic layers
-// ([obs | latent] 64 -> 512 | 512 -> 256 | 256 -> 128 | 128 each) and the heads on v_mfma_f32_16x16x4_f32, with every
-// activation in LDS and the weights streamed from L2 (each weight is used once per workgroup: 16 rows, no reuse to
-// stage); then the Normal sample, log-prob and the storage row as act_head_kernel does.  Replaces the prep pass, six
-// GEMM launches and the head launch of the layer-by-layer chain (their per-launch latency, not their FLOPs, set the
-// act's time at 4096 rows).  MFMA k-order: at step t of a 16-k block lane l (row / column l & 15, slot q = l >> 4)
-// feeds k = 16 b + 4 q + t on both operands, so W is read as one float4 per lane per block.
-constexpr int AF_ROWS = 16;
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-
-// C[16][ncols of this wave] = act(A[16][K] W^T + bias) for the column tiles [c0, c0 + 16 NT) of the layer; A in LDS
-// (row pitch lda, k columns past K_valid hold zeros), W row-major [N][ldw] in global memory (rows past n_valid and
-// k past K_valid are not read), output columns < n_valid to LDS (pitch ldc).
-template <int NT, bool ELU>
-__device__ __forceinline__ void af_layer(const float* __restrict__ A, int lda, int K, int K_valid,
-                                         const float* __restrict__ W, int ldw, int n_valid,
-                                         const float* __restrict__ bias, float* __restrict__ C, int ldc, int c0) {
-  const int lane = threadIdx.x & 63, li = lane & 15, q = lane >> 4;
-  f32x4_t acc[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int nb = K / 16;
-  float4 wcur[NT], wnxt[NT];
-  auto wload = [&](int b, float4 (&dst)[NT]) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = c0 + 16 * j + li, k = 16 * b + 4 * q;
-      if (n < n_valid && k + 3 < K_valid && (ldw & 3) == 0) {
-        dst[j] = *reinterpret_cast<const float4*>(W + (int64_t)n * ldw + k);
-      } else {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (n < n_valid) {
-          if (k + 0 < K_valid) v.x = W[(int64_t)n * ldw + k];
-          if (k + 1 < K_valid) v.y = W[(int64_t)n * ldw + k + 1];
-          if (k + 2 < K_valid) v.z = W[(int64_t)n * ldw + k + 2];
-          if (k + 3 < K_valid) v.w = W[(int64_t)n * ldw + k + 3];
-        }
-        dst[j] = v;
-      }
-    }
-  };
-  wload(0, wcur);
-  for (int b = 0; b < nb; ++b) {
-    if (b + 1 < nb) wload(b + 1, wnxt);
-    const float4 a = *reinterpret_cast<const float4*>(A + li * lda + 16 * b + 4 * q);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wcur[j].x, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wcur[j].y, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wcur[j].z, acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wcur[j].w, acc[j], 0, 0, 0);
-    }
-    if (b + 1 < nb) {
-#pragma unroll
-      for (int j = 0; j < NT; ++j) wcur[j] = wnxt[j];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int col = c0 + 16 * j + li;
-    const float bj = col < n_valid ? bias[col] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = acc[j][r] + bj;
-      if (ELU) v = v > 0.f ? v : expm1f(v);
-      if (col < n_valid) C[(4 * q + r) * ldc + col] = v;
-    }
-  }
-}
-
-struct ActFusedArgs {
-  const float* w;       // flat parameters
-  lrl_ppo_net net;
-  const float *obs, *priv, *hist, *eps;
-  int n;
-  uint64_t seed, counter;
-  float *actions, *mu, *values, *logp;
-  lrl_rollout_store store;
-  int store_row, do_store;
-};
-
-constexpr int AF_XP = 68, AF_E1P = 260, AF_E2P = 132, AF_H1P = 1028, AF_H2P = 516, AF_H3P = 260, AF_PP = 36;
-__global__ __launch_bounds__(HEAD_THREADS) void act_fused_kernel(ActFusedArgs a) {
-  __shared__ __attribute__((aligned(16))) float X[AF_ROWS * AF_XP];      // [obs | latent | 0]
-  __shared__ __attribute__((aligned(16))) float PR[AF_ROWS * AF_PP];     // priv (zero-padded to 32)
-  __shared__ __attribute__((aligned(16))) float BUF[AF_ROWS * (AF_H1P + AF_H2P)];  // HE1 / HE2 / H1 / H2 / H3
-  __shared__ float MU[AF_ROWS][16];
-  __shared__ float VV[AF_ROWS];
-  const lrl_ppo_net& nt = a.net;
-  const float* w = a.w;
-  const int t = threadIdx.x, wv = t >> 6;
-  const int r0 = blockIdx.x * AF_ROWS;
-  const int nrows = min(AF_ROWS, a.n - r0);
-  const int no = nt.num_obs, np = nt.num_priv;
-  // stage 0: obs rows -> X[:, 0:no), X[:, no+latent : 64) = 0; priv -> PR[:, 0:np), zeros to 32
-  for (int i = t; i < AF_ROWS * 64; i += HEAD_THREADS) {
-    const int r = i >> 6, c = i & 63;
-    float v = 0.f;
-    if (r < nrows && c < no) v = a.obs[(int64_t)(r0 + r) * no + c];
-    X[r * AF_XP + c] = v;
-  }
-  for (int i = t; i < AF_ROWS * 32; i += HEAD_THREADS) {
-    const int r = i >> 5, c = i & 31;
-    PR[r * AF_PP + c] = (r < nrows && c < np) ? a.priv[(int64_t)(r0 + r) * np + c] : 0.f;
-  }
-  __syncthreads();
-  float* HE1 = BUF;                       // [16][260]
-  float* HE2 = BUF + AF_ROWS * AF_E1P;    // [16][132]
-  // encoder: 18 -> 256 (4 waves x 4 tiles), 256 -> 128 (4 x 2), 128 -> 18 (waves 0, 1: one tile each)
-  af_layer<4, true>(PR, AF_PP, 32, np, w + nt.e1w, np, nt.enc_h0, w + nt.e1b, HE1, AF_E1P, 64 * wv);
-  __syncthreads();
-  af_layer<2, true>(HE1, AF_E1P, nt.enc_h0, nt.enc_h0, w + nt.e2w, nt.enc_h0, nt.enc_h1, w + nt.e2b, HE2, AF_E2P,
-                    32 * wv);
-  __syncthreads();
-  if (wv < 2)  // latent -> X[:, no : no + latent)
-    af_layer<1, false>(HE2, AF_E2P, nt.enc_h1, nt.enc_h1, w + nt.e3w, nt.enc_h1, nt.latent, w + nt.e3b, X + no,
-                       AF_XP, 16 * wv);
-  __syncthreads();
-  // actor / critic layer 1: X (64, zero-padded past no + latent) -> H1 [16][1024] (actor | critic), 4 x 16 tiles
-  float* H1 = BUF;                        // [16][1028]
-  float* H2 = BUF + AF_ROWS * AF_H1P;     // [16][516]
-  const int nx = no + nt.latent, h0 = nt.ac_h0, h1 = nt.ac_h1, h2 = nt.ac_h2;
-  af_layer<16, true>(X, AF_XP, 64, 64, w + nt.w1, nx, 2 * h0, w + nt.b1, H1, AF_H1P, 256 * wv);
-  __syncthreads();
-  // layer 2 (grouped): waves 0, 1 actor half, 2, 3 critic half, 128 columns each
-  {
-    const int g = wv >> 1, c0 = 128 * (wv & 1);
-    af_layer<8, true>(H1 + g * h0, AF_H1P, h0, h0, w + nt.w2 + (int64_t)g * h1 * h0, h0, h1, w + nt.b2 + g * h1,
-                      H2 + g * h1, AF_H2P, c0);
-  }
-  __syncthreads();
-  float* H3 = BUF;                        // [16][260] (H1 is dead)
-  {
-    const int g = wv >> 1, c0 = 64 * (wv & 1);
-    af_layer<4, true>(H2 + g * h1, AF_H2P, h1, h1, w + nt.w3 + (int64_t)g * h2 * h1, h1, h2, w + nt.b3 + g * h2,
-                      H3 + g * h2, AF_H3P, c0);
-  }
-  __syncthreads();
-  // heads: wave 0 mu (12 of 16 columns), wave 1 the value (column 0)
-  if (wv == 0) af_layer<1, false>(H3, AF_H3P, h2, h2, w + nt.w4a, h2, nt.num_actions, w + nt.b4a, &MU[0][0], 16, 0);
-  if (wv == 1) {
-    float* vt = BUF + AF_ROWS * AF_H3P;   // [16][16] scratch after H3
-    af_layer<1, false>(H3 + h2, AF_H3P, h2, h2, w + nt.w4c, h2, 1, w + nt.b4c, vt, 16, 0);
-  }
-  __syncthreads();
-  if (t < AF_ROWS) VV[t] = BUF[AF_ROWS * AF_H3P + t * 16];
-  // sample, log-prob terms and the outputs (act_head_kernel's order of operations)
-  const int na = nt.num_actions;
-  const int64_t so = (int64_t)a.store_row * a.n;
-  const float* stdv = w + nt.std_off;
-  for (int i = t; i < nrows * na; i += HEAD_THREADS) {
-    const int r = i / na, j = i - r * na, g = r0 + r;
-    float e;
-    if (a.eps) {
-      e = a.eps[(int64_t)g * na + j];
-    } else {
-      lrl_u32x4 u = lrl_philox((uint32_t)g, (uint32_t)a.counter, (LRL_RNG_POLICY << 16) ^ (uint32_t)(a.counter >> 32),
-                               (uint32_t)(j >> 1), a.seed);
-      const float u1 = fmaxf(lrl_u01(u.v[0]), 1e-7f), u2 = lrl_u01(u.v[1]);
-      const float rad = sqrtf(-2.f * logf(u1)), th = 6.283185307179586f * u2;
-      e = (j & 1) ? rad * sinf(th) : rad * cosf(th);
-    }
-    const float m = MU[r][j], sd = stdv[j];
-    const float act = m + sd * e;
-    const float d = act - m;
-    MU[r][j] = -(d * d) / (2.f * (sd * sd)) - logf(sd) - LOG_SQRT_2PI;
-    a.actions[(int64_t)g * na + j] = act;
-    if (a.mu) a.mu[(int64_t)g * na + j] = m;
-    if (a.do_store) {
-      const int64_t o = (so + g) * na + j;
-      a.store.actions[o] = act;
-      a.store.mu[o] = m;
-      a.store.sigma[o] = sd;
-    }
-  }
-  __syncthreads();
-  if (t < nrows) {
-    const int g = r0 + t;
-    float lp = 0.f;
-    for (int j = 0; j < na; ++j) lp += MU[t][j];
-    const float v = VV[t];
-    if (a.values) a.values[g] = v;
-    if (a.logp) a.logp[g] = lp;
-    if (a.do_store) {
-      a.store.values[so + g] = v;
-      a.store.logp[so + g] = lp;
-    }
-  }
-  if (a.do_store) {
-    const int64_t b = so + r0;
-    copy_rows(a.obs + (int64_t)r0 * no, no, a.store.obs + b * no, no, nrows, no, t);
-    copy_rows(a.priv + (int64_t)r0 * np, np, a.store.priv + b * np, np, nrows, np, t);
-    if (a.hist && a.store.hist) {
-      const int hd = a.store.hist_dim, ld = a.store.hist_ld > hd ? a.store.hist_ld : hd;
-      copy_rows(a.hist + (int64_t)r0 * hd, hd, a.store.hist + b * ld, ld, nrows, hd, t);
-    }
-  }
-}
-
-// the shapes act_fused_kernel is written for (the presets' blind teacher policy)
-static bool act_fused_ok(const lrl_ppo_net& n) {
-  return n.num_obs + n.latent <= 64 && n.num_priv <= 32 && n.enc_h0 == 256 && n.enc_h1 == 128 && n.latent <= 32 &&
-         n.ac_h0 == 512 && n.ac_h1 == 256 && n.ac_h2 == 128 && n.num_actions <= 16 && n.num_priv % 2 == 0 &&
-         (n.num_obs + n.latent) % 4 == 0 && n.enc_h0 % 16 == 0;
-}
-
-// ---------------------------------------------------------------------------------------------------
 // Adaptation head: pred = HD2 W_D3^T + b, MSE against the encoder target (F.mse_loss, mean over B*L),
 // dHD2 = dpred W_D3 * elu'(HD2); partials dW_D3 [L][H], db_D3 [L], sum of squared errors.
 struct AdaptHeadArgs {
@@ -1103,16 +895,6 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
     return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: incomplete rollout store");
   const lrl_ppo_net& nt = *net;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  static const bool fused = getenv("LRL_ACT_FUSED") != nullptr;  // (opt-in until measured on the GPU)
-  if (fused && act_fused_ok(nt)) {
-    ActFusedArgs af{};
-    af.w = params; af.net = nt; af.obs = obs; af.priv = priv; af.hist = hist; af.eps = eps; af.n = n;
-    af.seed = seed; af.counter = counter; af.actions = actions; af.mu = mu; af.values = values; af.logp = logp;
-    if (store) af.store = *store;
-    af.store_row = store_row; af.do_store = store ? 1 : 0;
-    hipLaunchKernelGGL(act_fused_kernel, dim3((n + AF_ROWS - 1) / AF_ROWS), dim3(HEAD_THREADS), 0, st, af);
-    return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act: launch failed");
-  }
   ActPlan P = make_act_plan(nt, n, static_cast<char*>(workspace));
   G g{st, nullptr};
   const float* w = params;
