@@ -223,14 +223,15 @@ def main():
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
-    if args.world_check:
-        os.environ["LRL_DIST_BACKEND"] = "gloo"  # CPU tensors, no device context
     backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
     if backend == "nccl":
+        # the GPU count is checked for the real launch and for --world-check alike (device_count() opens no context)
         ndev = torch.cuda.device_count()
         if args.gpus > ndev:
             print(f"bench.py: --gpus {args.gpus} requested but {ndev} GPU(s) visible", file=sys.stderr)
             raise SystemExit(2)
+    if args.world_check:
+        os.environ["LRL_DIST_BACKEND"] = "gloo"  # CPU tensors, no device context
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local, backend = init_world(args)
