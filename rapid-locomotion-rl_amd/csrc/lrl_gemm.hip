@@ -864,6 +864,361 @@ static int launch_glds_tn(const GemmP& p, int groups, hipStream_t st) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// fp32 products on the bf16 MFMA ("x6"): every operand element is split exactly into three bf16 parts,
+// x = hi + mid + lo (truncation: hi takes the top 8 significant bits, mid the next 8 of the exact remainder,
+// lo the rest — 24 bits in all, so nothing is lost), and a 32x32x16 k-step sums the six products whose
+// order is above 2^-24 (lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi, smallest first) into an fp32
+// accumulator.  The dropped products (mid*lo, lo*mid, lo*lo) are below 2^-24 of |a b|, so the result is
+// as accurate as the fp32 MFMA's (measured: max |C - C_fp64| / sum|a b| 1.6-2.1e-7 for both on the update's
+// shapes, scripts/proto_x6.hip), at 6 x 32 cycles per 32x32x16 step instead of 8 x 64 for the fp32 form.
+// The split happens once per element while staging: global -> registers (fp32), split, three bf16 plane
+// images -> LDS; each MFMA operand is then one ds_read_b128 per plane.
+//   k-contiguous operand ([r][k]: A of NT / NN, B of NT): float4 loads, thread i covers row i/4, k-quad i%4;
+//   r-contiguous operand ([k][r]: B of NN, A and B of TN): a thread loads a run of R/16 consecutive k of one
+//   row r (dword loads, coalesced over r), so its split parts land as one contiguous run of the [r][k] image.
+// Plane images are [R][16] bf16 (32-B rows); 16-B chunk c of row r sits in slot c ^ ((r >> 3) & 1), which keeps
+// the 16-lane groups of the ds_read_b128 operand reads conflict-free.
+// BM x BN tile (64 or 128 each), 4 waves in a 2 x 2 grid, wave tile (BM/2) x (BN/2) = TM x TN MFMA tiles;
+// BK = 16, two LDS stages, the next slice's global loads in flight under the current slice's MFMAs.
+constexpr int XBK = 16;
+
+__device__ __forceinline__ uint32_t x6_hi_pair(uint32_t u0, uint32_t u1) {
+  return __builtin_amdgcn_perm(u1, u0, 0x07060302u);  // (u1 & 0xffff0000) | (u0 >> 16)
+}
+// (x0, x1) -> the packed bf16 pairs of their hi / mid / lo parts
+__device__ __forceinline__ void x6_split2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+  uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+  h = x6_hi_pair(u0, u1);
+  float r0 = x0 - __uint_as_float(u0 & 0xffff0000u), r1 = x1 - __uint_as_float(u1 & 0xffff0000u);
+  u0 = __float_as_uint(r0);
+  u1 = __float_as_uint(r1);
+  m = x6_hi_pair(u0, u1);
+  r0 = r0 - __uint_as_float(u0 & 0xffff0000u);
+  r1 = r1 - __uint_as_float(u1 & 0xffff0000u);
+  l = x6_hi_pair(__float_as_uint(r0), __float_as_uint(r1));
+}
+__device__ __forceinline__ int x6_off(int r, int c) { return r * XBK + 8 * (c ^ ((r >> 3) & 1)); }
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int R, bool KC, bool KGATHER = false>
+struct X6Op {
+  static constexpr int PLANE = R * XBK;                 // bf16 elements of one plane image
+  static constexpr int NI = KC ? R / 64 : 1;             // float4 items per thread (k-contiguous)
+  static constexpr int KR = KC ? 4 : R / 16;             // k-run per thread (r-contiguous): 8 or 4
+  float v[KC ? 4 * NI : KR];
+  const float* rowp[NI];  // k-contiguous: row pointers (nullptr: row outside the operand)
+  const float* P;
+  const int64_t* krows;
+  int64_t ld;
+  int ldi, roff;  // r-contiguous: 32-bit element offsets from the (wave-uniform) operand base
+  int rr, kb;     // r-contiguous: this thread's row in the tile and k offset of its run
+  bool rok;
+
+  __device__ __forceinline__ void init(const float* P_, int64_t ld_, const int64_t* rows, const int64_t* krows_,
+                                       int r0, int R_lim) {
+    P = P_; ld = ld_; krows = krows_;
+    const int t = threadIdx.x;
+    if (KC) {
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        const int r = (t >> 2) + 64 * u, gr = r0 + r;
+        rowp[u] = gr < R_lim ? P_ + (rows ? rows[gr] : (int64_t)gr) * ld_ + 4 * (t & 3) : nullptr;
+      }
+    } else {
+      rr = t % R;
+      kb = __builtin_amdgcn_readfirstlane(KR * (t / R));  // wave-uniform: the run's row list reads are scalar
+      rok = r0 + rr < R_lim;
+      ldi = (int)ld_;
+      roff = r0 + rr;
+    }
+  }
+  __device__ __forceinline__ void load(int k0, int k_lim, bool fast) {
+    if (KC) {
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        const int k = k0 + 4 * (threadIdx.x & 3);
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (fast) {
+          q = *reinterpret_cast<const float4*>(rowp[u] + k0);
+        } else if (rowp[u]) {
+          const float* s = rowp[u] + k0;
+          if (k + 3 < k_lim) {
+            q = *reinterpret_cast<const float4*>(s);
+          } else {
+            if (k + 0 < k_lim) q.x = s[0];
+            if (k + 1 < k_lim) q.y = s[1];
+            if (k + 2 < k_lim) q.z = s[2];
+          }
+        }
+        v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < KR; ++e) {
+        const int k = k0 + kb + e;
+        const int kr = KGATHER ? (int)krows[k] : k;
+        if (fast) {
+          v[e] = P[kr * ldi + roff];
+        } else {
+          v[e] = (rok && k < k_lim) ? P[kr * ldi + roff] : 0.f;
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* img) const {
+    const int t = threadIdx.x;
+    if (KC) {
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        const int r = (t >> 2) + 64 * u, j = t & 3;
+        uint32_t h0, m0, l0, h1, m1, l1;
+        x6_split2(v[4 * u], v[4 * u + 1], h0, m0, l0);
+        x6_split2(v[4 * u + 2], v[4 * u + 3], h1, m1, l1);
+        const int off = x6_off(r, j >> 1) + 4 * (j & 1);
+        *reinterpret_cast<uint2*>(img + off) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(img + PLANE + off) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(img + 2 * PLANE + off) = make_uint2(l0, l1);
+      }
+    } else if (KR == 8) {
+      uint32_t h[4], m[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x6_split2(v[2 * e], v[2 * e + 1], h[e], m[e], l[e]);
+      const int off = x6_off(rr, kb >> 3);
+      *reinterpret_cast<uint4*>(img + off) = make_uint4(h[0], h[1], h[2], h[3]);
+      *reinterpret_cast<uint4*>(img + PLANE + off) = make_uint4(m[0], m[1], m[2], m[3]);
+      *reinterpret_cast<uint4*>(img + 2 * PLANE + off) = make_uint4(l[0], l[1], l[2], l[3]);
+    } else {
+      uint32_t h[2], m[2], l[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) x6_split2(v[2 * e], v[2 * e + 1], h[e], m[e], l[e]);
+      const int off = x6_off(rr, kb >> 3) + (kb & 4);
+      *reinterpret_cast<uint2*>(img + off) = make_uint2(h[0], h[1]);
+      *reinterpret_cast<uint2*>(img + PLANE + off) = make_uint2(m[0], m[1]);
+      *reinterpret_cast<uint2*>(img + 2 * PLANE + off) = make_uint2(l[0], l[1]);
+    }
+  }
+  // sum of this thread's staged values (bias-gradient partial of an r-contiguous A)
+  __device__ __forceinline__ float vsum() const {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < (int)(sizeof(v) / sizeof(float)); ++e) s += v[e];
+    return s;
+  }
+};
+
+template <int BM, int BN, int LAYOUT, int EPI, bool FAST, bool BGATHER>
+__global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 waves / SIMD: 3 workgroups per CU (LDS 48 KB)
+  constexpr bool AKC = (LAYOUT & 1) == 0, BKC = (LAYOUT & 2) == 0;
+  constexpr int PA = BM * XBK, PB = BN * XBK, STG = 3 * (PA + PB);
+  constexpr int TM = BM / 64, TN = BN / 64;
+  __shared__ __attribute__((aligned(16))) uint16_t S[2 * STG];
+  const int mt = (p.M + BM - 1) / BM, nt = (p.N + BN - 1) / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, zz = L / (nt * mt);
+  const int g = zz / p.splits, sp = zz - g * p.splits;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int kbeg = sp * p.kps, kend = min(p.K, kbeg + p.kps);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  X6Op<BM, AKC> oa;
+  X6Op<BN, BKC, BGATHER && !BKC> ob;
+  oa.init(p.A + g * p.ga, p.lda, AKC ? p.a_rows : nullptr, nullptr, m0, p.M);
+  ob.init(p.B + g * p.gb, p.ldb, nullptr, BKC ? nullptr : p.b_rows, n0, p.N);
+  // FAST: every tile of the launch is interior and every split's k range a whole number of slices
+  constexpr bool fast = FAST;
+  const bool do_bsum = EPI == EPI_PARTIAL && p.bias_part != nullptr && tn_ == 0;
+  float bsum = 0.f;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (kbeg < kend) {
+    oa.load(kbeg, kend, fast);
+    ob.load(kbeg, kend, fast);
+    if (do_bsum) bsum += oa.vsum();
+    oa.store(S);
+    ob.store(S + 3 * PA);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += XBK) {
+    const bool more = k0 + XBK < kend;
+    if (more) {
+      oa.load(k0 + XBK, kend, fast);
+      ob.load(k0 + XBK, kend, fast);
+    }
+    const uint16_t* As = S + buf * STG;
+    const uint16_t* Bs = As + 3 * PA;
+    bf16x8_t a[TM][3], b[TN][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = *reinterpret_cast<const bf16x8_t*>(As + pl * PA + x6_off(wm + 32 * i + li, h));
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[j][pl] = *reinterpret_cast<const bf16x8_t*>(Bs + pl * PB + x6_off(wn + 32 * j + li, h));
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+    if (more) {
+      if (do_bsum) bsum += oa.vsum();
+      oa.store(S + (buf ^ 1) * STG);
+      ob.store(S + (buf ^ 1) * STG + 3 * PA);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  float* __restrict__ C = p.C + g * p.gc;
+  if (EPI == EPI_PARTIAL) C += (int64_t)sp * p.part_stride;
+  const float* __restrict__ bias = p.bias ? p.bias + g * p.gbias : nullptr;
+  // (the backward-data epilogue's layer input is read here, not prefetched: 16 registers per MFMA tile held
+  // through the main loop would cost occupancy)
+  const float* __restrict__ ax = EPI == EPI_DELU ? p.aux + g * p.gaux : nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn + 32 * j + li;
+    if (!FAST && col >= p.N) continue;
+    float bj = 0.f;
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = bias[col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // rows 8q + 4h .. +3 of the MFMA tile: accumulator registers 4q .. 4q+3
+        const int row0 = m0 + wm + 32 * i + 8 * q + 4 * h;
+        // 32-bit element offsets from per-group base pointers (row * ld < 2^31 for every product here)
+        const int ldc = (int)p.ldc, ldx = (int)p.ld_aux;
+        float* __restrict__ crow = C + (int64_t)row0 * p.ldc + col;
+        float xa[4];
+        if constexpr (EPI == EPI_DELU) {
+          const float* __restrict__ xrow = ax + (int64_t)row0 * p.ld_aux + col;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xa[r] = (FAST || row0 + r < p.M) ? xrow[r * ldx] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (FAST || row0 + r < p.M) {
+            float v = acc[i][j][4 * q + r];
+            if (EPI == EPI_BIAS) v += bj;
+            if (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+            if constexpr (EPI == EPI_DELU) {
+              const float x = xa[r];
+              v = x > 0.f ? v : v * (x + 1.f);
+            }
+            crow[r * ldc] = v;
+          }
+        }
+        asm volatile("" ::: "memory");  // (bounds the epilogue's live loads and addresses to one row group)
+      }
+  }
+  if constexpr (EPI == EPI_PARTIAL && !AKC) {
+    // bias-gradient partial: the k-runs of one row are spread over GTHREADS / BM threads; add them in thread
+    // order through LDS (fixed order: deterministic)
+    if (do_bsum) {
+      float* red = reinterpret_cast<float*>(S);  // the loop's last barrier has retired every stage read
+      red[threadIdx.x] = bsum;
+      __syncthreads();
+      if (threadIdx.x < BM && m0 + (int)threadIdx.x < p.M) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < GTHREADS / BM; ++q) s += red[q * BM + threadIdx.x];
+        p.bias_part[((int64_t)sp * p.groups + g) * p.M + m0 + threadIdx.x] = s;
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+static int launch_x6_tile(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
+  dim3 grid(((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * groups * p.splits);
+  const bool interior = p.M % BM == 0 && p.N % BN == 0 && p.K % XBK == 0 && p.kps % XBK == 0;
+  const bool bg = p.b_rows != nullptr;
+#define LRL_X6G(L, E, G)                                                                                     \
+  do {                                                                                                       \
+    if (interior) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, L, E, true, G>), grid, dim3(GTHREADS), 0, st, p); \
+    else hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, L, E, false, G>), grid, dim3(GTHREADS), 0, st, p);        \
+  } while (0)
+#define LRL_X6(L, E) LRL_X6G(L, E, false)
+  if (layout == GEMM_NT) {
+    if (epi == EPI_STORE) LRL_X6(GEMM_NT, EPI_STORE);
+    else if (epi == EPI_BIAS) LRL_X6(GEMM_NT, EPI_BIAS);
+    else if (epi == EPI_BIAS_ELU) LRL_X6(GEMM_NT, EPI_BIAS_ELU);
+    else return LRL_E_INVALID;
+  } else if (layout == GEMM_NN) {
+    if (epi == EPI_STORE) LRL_X6(GEMM_NN, EPI_STORE);
+    else if (epi == EPI_DELU) LRL_X6(GEMM_NN, EPI_DELU);
+    else return LRL_E_INVALID;
+  } else if (layout == GEMM_TN && epi == EPI_PARTIAL) {
+    if constexpr (BM == 128) {
+      if (bg) LRL_X6G(GEMM_TN, EPI_PARTIAL, true);
+      else LRL_X6G(GEMM_TN, EPI_PARTIAL, false);
+    } else {
+      return LRL_E_INVALID;
+    }
+  } else {
+    return LRL_E_INVALID;
+  }
+#undef LRL_X6
+#undef LRL_X6G
+  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+}
+
+// x6 path switch: LRL_GEMM_X6=0 keeps every product on the fp32 MFMA kernels (A/B comparisons)
+static bool x6_enabled() {
+  static const int on = [] {
+    const char* e = getenv("LRL_GEMM_X6");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// returns 1 when the product was launched on the x6 kernel (0: not eligible, <0: error)
+static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
+  if (!x6_enabled()) return 0;
+  const bool akc = (layout & 1) == 0, bkc = (layout & 2) == 0;
+  // k-contiguous operands are staged with float4 loads
+  if ((akc && p.avec != 4) || (bkc && p.bvec != 4)) return 0;
+  int rc;
+  if (layout == GEMM_TN) {
+    if (epi != EPI_PARTIAL || p.M < 128 || p.N < 32 || p.kps % XBK) return 0;
+    rc = p.N <= 64 ? launch_x6_tile<128, 64>(p, layout, epi, groups, st)
+                   : launch_x6_tile<128, 128>(p, layout, epi, groups, st);
+  } else {
+    if (p.splits != 1 || p.N < 64 || p.M < 64 || epi == EPI_PARTIAL) return 0;
+    const int bn = p.N >= 128 ? 128 : 64;
+    // 128-row tiles when they still give two workgroups per CU, 64 otherwise
+    const int64_t wg128 = (int64_t)((p.M + 127) / 128) * ((p.N + bn - 1) / bn) * groups;
+    const int bm = wg128 >= 512 ? 128 : 64;
+    if (bm == 128 && bn == 128) rc = launch_x6_tile<128, 128>(p, layout, epi, groups, st);
+    else if (bm == 128) rc = launch_x6_tile<128, 64>(p, layout, epi, groups, st);
+    else if (bn == 128) rc = launch_x6_tile<64, 128>(p, layout, epi, groups, st);
+    else rc = launch_x6_tile<64, 64>(p, layout, epi, groups, st);
+  }
+  return rc ? rc : 1;
+}
+
 template <int BM, int BN>
 static int launch_bm(const GemmP& p, int layout, int epi, dim3 grid, hipStream_t st) {
 #define LRL_GEMM_LAUNCH(L, E) hipLaunchKernelGGL((gemm_kernel<BM, BN, L, E>), grid, dim3(GTHREADS), 0, st, p)
@@ -947,6 +1302,8 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   if (trace)
     fprintf(stderr, "gemm layout=%d epi=%d M=%d N=%d K=%d groups=%d splits=%d avec=%d bvec=%d arows=%d brows=%d\n",
             layout, epi, p.M, p.N, p.K, groups, p.splits, p.avec, p.bvec, p.a_rows != nullptr, p.b_rows != nullptr);
+  // fp32 on the bf16 MFMA (exact split, fp32-class error) wherever the tile shapes fit
+  if (int xr = try_x6(p, layout, epi, groups, st)) return xr > 0 ? 0 : xr;
   // LDS-DMA path: batch-major product, every tile interior, float4-aligned operands, single split
   if (layout != GEMM_TN && p.splits == 1 && p.M % 64 == 0 && p.N % 64 == 0 && p.K % 16 == 0 && p.K >= 32 &&
       p.avec == 4 && p.bvec == 4 && epi != EPI_PARTIAL && (layout == GEMM_NT || layout == GEMM_NN)) {

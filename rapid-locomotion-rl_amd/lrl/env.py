@@ -249,6 +249,7 @@ class LeggedRobotEnv:
         self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
         self._ids_all = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
         self._due_next = None  # (episode_length_buf version, env ids due for command resampling next step)
+        self._step_timer = None  # optional section timer of step() (scripts/step_timing.py)
         self._sums_host = None  # (command_sums version, host copy of the two tracking rows) between a step's sync
         keys = list(self.reward_scales)  # and the resampling it feeds
         self._track_rows = [keys.index("tracking_lin_vel"), keys.index("tracking_ang_vel")] \
@@ -433,6 +434,9 @@ class LeggedRobotEnv:
         if actions.shape != (self.num_envs, self.num_actions):
             raise ValueError(f"actions must be [{self.num_envs}, {self.num_actions}], got {tuple(actions.shape)}")
         flags = _abi.STEP_PHYSICS | (_abi.STEP_HISTORY if _history else 0)
+        tm = self._step_timer  # scripts/step_timing.py: host time per section of this method (None: off)
+        if tm is not None:
+            tm.mark("entry")
         if not self.legacy_fork:  # _post_physics_step_callback resampling (legged_robot.py:578-581): the
             # envs whose episode length reaches a multiple of resampling_time in this step, before its rewards
             interval = int(self.cfg.commands.resampling_time / self.dt)
@@ -446,6 +450,8 @@ class LeggedRobotEnv:
             if (len(due) > 0) if self._dist is None else (self._dist_count(len(due)) > 0):
                 self.resample_commands(due, due_np)
         self._sums_host = None  # the kernel below changes the command sums
+        if tm is not None:
+            tm.mark("pre_resample")
         _abi.check(self._L.lrl_sim_step(self._sim, C.c_void_p(actions.data_ptr()), C.c_uint32(flags), self._stream()))
         self.common_step_counter += 1
         if not self.legacy_fork:  # reset_idx of the terminated / timed-out envs, then their observations
@@ -462,6 +468,8 @@ class LeggedRobotEnv:
                 self._sums_host = (self._command_sums._version, pack[1:3])
             else:
                 code = code.cpu().numpy()
+            if tm is not None:
+                tm.mark("launch_and_sync")
             rst = code & 1
             ids_np = np.flatnonzero(rst)
             due_np = np.flatnonzero((code >> 1) & ((rst == 0) | (interval == 1)))
@@ -472,6 +480,8 @@ class LeggedRobotEnv:
                 _abi.check(self._L.lrl_sim_observe_idx(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
                                                        C.c_uint32(flags), self._stream()))
             self._due_next = (eplen._version, torch.from_numpy(due_np).to(self.device), due_np)
+            if tm is not None:
+                tm.mark("reset_idx_observe")
         ex = self.extras
         ex["privileged_obs"] = self.privileged_obs_buf
         ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())
@@ -486,6 +496,8 @@ class LeggedRobotEnv:
         ex.set_lazy("foot_positions", lambda: self._foot_positions().cpu().numpy().copy())
         ex.set_lazy("body_pos", lambda: self.root_states[:, 0:3].cpu().numpy())
         ex.set_lazy("torques", lambda: self.torques.cpu().numpy())
+        if tm is not None:
+            tm.mark("extras")
         return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
 
     def kernel_timing(self, start):

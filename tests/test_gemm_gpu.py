@@ -99,3 +99,40 @@ def test_weight_grad_tn(M, N, K, gather, ldx):
     err = (out.double() - ref).abs().max().item()
     assert err <= 4e-6 * np.sqrt(K) * (ref.abs().max().item() + 1.0), err
     assert (db.double() - dY.double().sum(0)).abs().max().item() <= 1e-5 * np.sqrt(K) * 10
+
+
+@pytest.mark.parametrize("layout,M,N,K", [(0, 24576, 256, 512), (0, 4096, 1024, 64), (2, 24576, 512, 256),
+                                          (3, 256, 512, 24576), (0, 300, 200, 60), (2, 333, 200, 50),
+                                          (3, 300, 100, 5000)])
+def test_x6_error_is_fp32_class(layout, M, N, K):
+    """Products whose tiles fit the split-bf16 kernel (csrc/lrl_gemm.hip gemm_x6_kernel: x = hi + mid + lo exactly,
+    six bf16 MFMA products, fp32 accumulation): the error against an fp64 product, relative to sum_k |a b|, stays at
+    the fp32 level (<= 1e-6 here; the fp32 MFMA measures 1.6-2.4e-7 on the same shapes, the x6 kernel 1.6-2.1e-7),
+    for interior tiles and for ragged m / n / k edges."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K + layout)
+    if layout == 0:
+        A = torch.randn(M, K, device=dev, generator=g)
+        W = torch.randn(N, K, device=dev, generator=g) * 0.1
+        out = torch.empty(M, N, device=dev)
+        _gemm(0, 0, M, N, K, A, K, W, K, out, N)
+        ref = A.double() @ W.double().T
+        mag = A.double().abs() @ W.double().abs().T
+    elif layout == 2:
+        A = torch.randn(M, K, device=dev, generator=g)
+        W = torch.randn(K, N, device=dev, generator=g) * 0.1
+        out = torch.empty(M, N, device=dev)
+        _gemm(2, 0, M, N, K, A, K, W, N, out, N)
+        ref = A.double() @ W.double()
+        mag = A.double().abs() @ W.double().abs()
+    else:
+        dY = torch.randn(K, M, device=dev, generator=g)
+        X = torch.randn(K, N, device=dev, generator=g) * 0.1
+        out = torch.empty(M, N, device=dev)
+        db = torch.empty(M, device=dev)
+        ws = torch.empty(64 * (M * N + M) * 2, device=dev)
+        _gemm(3, 4, M, N, K, dY, M, X, N, out, N, bias=db, ws=ws)
+        ref = dY.double().T @ X.double()
+        mag = dY.double().abs().T @ X.double().abs()
+        assert ((db.double() - dY.double().sum(0)).abs() / dY.double().abs().sum(0)).max().item() <= 1e-6
+    rel = ((out.double() - ref).abs() / mag).max().item()
+    assert rel <= 1e-6, rel
