@@ -915,10 +915,11 @@ struct X6Op {
   int ldi, roff;  // r-contiguous: 32-bit element offsets from the (wave-uniform) operand base
   int rr, kb;     // r-contiguous: this thread's row in the tile and k offset of its run
   bool rok;
+  bool vec4;      // k-contiguous: rows 16-B aligned (float4 loads); otherwise dword loads
 
   __device__ __forceinline__ void init(const float* P_, int64_t ld_, const int64_t* rows, const int64_t* krows_,
-                                       int r0, int R_lim) {
-    P = P_; ld = ld_; krows = krows_;
+                                       int r0, int R_lim, bool vec4_ = true) {
+    P = P_; ld = ld_; krows = krows_; vec4 = vec4_;
     const int t = threadIdx.x;
     if (KC) {
 #pragma unroll
@@ -944,8 +945,10 @@ struct X6Op {
           q = *reinterpret_cast<const float4*>(rowp[u] + k0);
         } else if (rowp[u]) {
           const float* s = rowp[u] + k0;
-          if (k + 3 < k_lim) {
+          if (k + 3 < k_lim && vec4) {
             q = *reinterpret_cast<const float4*>(s);
+          } else if (k + 3 < k_lim) {
+            q = make_float4(s[0], s[1], s[2], s[3]);
           } else {
             if (k + 0 < k_lim) q.x = s[0];
             if (k + 1 < k_lim) q.y = s[1];
@@ -1028,8 +1031,8 @@ __global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 w
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
   X6Op<BM, AKC> oa;
   X6Op<BN, BKC, BGATHER && !BKC> ob;
-  oa.init(p.A + g * p.ga, p.lda, AKC ? p.a_rows : nullptr, nullptr, m0, p.M);
-  ob.init(p.B + g * p.gb, p.ldb, nullptr, BKC ? nullptr : p.b_rows, n0, p.N);
+  oa.init(p.A + g * p.ga, p.lda, AKC ? p.a_rows : nullptr, nullptr, m0, p.M, p.avec == 4);
+  ob.init(p.B + g * p.gb, p.ldb, nullptr, BKC ? nullptr : p.b_rows, n0, p.N, p.bvec == 4);
   // FAST: every tile of the launch is interior and every split's k range a whole number of slices
   constexpr bool fast = FAST;
   const bool do_bsum = EPI == EPI_PARTIAL && p.bias_part != nullptr && tn_ == 0;
@@ -1153,7 +1156,9 @@ __global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 w
 template <int BM, int BN>
 static int launch_x6_tile(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
   dim3 grid(((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * groups * p.splits);
-  const bool interior = p.M % BM == 0 && p.N % BN == 0 && p.K % XBK == 0 && p.kps % XBK == 0;
+  const bool akc = (layout & 1) == 0, bkc = (layout & 2) == 0;
+  const bool interior = p.M % BM == 0 && p.N % BN == 0 && p.K % XBK == 0 && p.kps % XBK == 0 &&
+                        (!akc || p.avec == 4) && (!bkc || p.bvec == 4);
   const bool bg = p.b_rows != nullptr;
 #define LRL_X6G(L, E, G)                                                                                     \
   do {                                                                                                       \
@@ -1171,12 +1176,8 @@ static int launch_x6_tile(const GemmP& p, int layout, int epi, int groups, hipSt
     else if (epi == EPI_DELU) LRL_X6(GEMM_NN, EPI_DELU);
     else return LRL_E_INVALID;
   } else if (layout == GEMM_TN && epi == EPI_PARTIAL) {
-    if constexpr (BM == 128) {
-      if (bg) LRL_X6G(GEMM_TN, EPI_PARTIAL, true);
-      else LRL_X6G(GEMM_TN, EPI_PARTIAL, false);
-    } else {
-      return LRL_E_INVALID;
-    }
+    if (bg) LRL_X6G(GEMM_TN, EPI_PARTIAL, true);
+    else LRL_X6G(GEMM_TN, EPI_PARTIAL, false);
   } else {
     return LRL_E_INVALID;
   }
@@ -1197,17 +1198,22 @@ static bool x6_enabled() {
 // returns 1 when the product was launched on the x6 kernel (0: not eligible, <0: error)
 static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
   if (!x6_enabled()) return 0;
-  const bool akc = (layout & 1) == 0, bkc = (layout & 2) == 0;
-  // k-contiguous operands are staged with float4 loads
-  if ((akc && p.avec != 4) || (bkc && p.bvec != 4)) return 0;
   int rc;
   if (layout == GEMM_TN) {
-    if (epi != EPI_PARTIAL || p.M < 128 || p.N < 32 || p.kps % XBK) return 0;
-    rc = p.N <= 64 ? launch_x6_tile<128, 64>(p, layout, epi, groups, st)
-                   : launch_x6_tile<128, 128>(p, layout, epi, groups, st);
+    // (both operands r-contiguous: dword loads, any alignment)
+    if (epi != EPI_PARTIAL || p.M < 16 || p.N < 16 || p.kps % XBK) return 0;
+    const bool m64 = p.M <= 64, n64 = p.N <= 64;
+    if (m64 && n64) rc = launch_x6_tile<64, 64>(p, layout, epi, groups, st);
+    else if (m64) rc = launch_x6_tile<64, 128>(p, layout, epi, groups, st);
+    else if (n64) rc = launch_x6_tile<128, 64>(p, layout, epi, groups, st);
+    else rc = launch_x6_tile<128, 128>(p, layout, epi, groups, st);
   } else {
-    if (p.splits != 1 || p.N < 64 || p.M < 64 || epi == EPI_PARTIAL) return 0;
-    const int bn = p.N >= 128 ? 128 : 64;
+    if (p.splits != 1 || p.N < 16 || p.M < 64 || epi == EPI_PARTIAL) return 0;
+    // measured (scripts/gemm_bench.py): one or two 16-k slices do not pay the split / staging set-up, and the
+    // thin kernel (B in registers) stays faster for <= 32-wide outputs over k = 512 / 1024
+    if (p.K < 32) return 0;
+    if (p.N <= 32 && p.K % 128 == 0 && (p.K / 128 == 4 || p.K / 128 == 8) && p.avec == 4 && p.M >= 256) return 0;
+    const int bn = p.N > 64 ? 128 : 64;
     // 128-row tiles when they still give two workgroups per CU, 64 otherwise
     const int64_t wg128 = (int64_t)((p.M + 127) / 128) * ((p.N + bn - 1) / bn) * groups;
     const int bm = wg128 >= 512 ? 128 : 64;

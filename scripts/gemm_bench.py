@@ -29,6 +29,10 @@ SHAPES = [
     ("dHD1     NN 32->256", 2, 3, B, 256, 32),
     ("dW2      TN 256x512", 3, 4, 256, 512, B),
     ("dWD1     TN 256x630 gather", 3, 4, 256, 630, B),
+    ("dWe1     TN 256x18 gather", 3, 4, 256, 18, B),
+    ("dWe3     TN 18x128", 3, 4, 18, 128, B),
+    ("dW1      TN 1024x60", 3, 4, 1024, 60, B),
+    ("dWD2     TN 32x256", 3, 4, 32, 256, B),
     ("long-K   NT 4096->256", 0, 2, B, 256, 4096),
 ]
 if os.environ.get("GEMM_BENCH_FILTER"):
