@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
@@ -882,6 +883,12 @@ static int launch_glds_tn(const GemmP& p, int groups, hipStream_t st) {
 // BM x BN tile (64 or 128 each), 4 waves in a 2 x 2 grid, wave tile (BM/2) x (BN/2) = TM x TN MFMA tiles;
 // BK = 16, two LDS stages, the next slice's global loads in flight under the current slice's MFMAs.
 constexpr int XBK = 16;
+#ifndef LRL_X6_PIPE
+#define LRL_X6_PIPE 1  // software-pipelined main loop (see gemm_x6_kernel)
+#endif
+#ifndef LRL_X6_PIPE_VALU
+#define LRL_X6_PIPE_VALU 4  // VALU instructions scheduled after each MFMA of the pipelined loop
+#endif
 
 __device__ __forceinline__ uint32_t x6_hi_pair(uint32_t u0, uint32_t u1) {
   return __builtin_amdgcn_perm(u1, u0, 0x07060302u);  // (u1 & 0xffff0000) | (u0 >> 16)
@@ -907,7 +914,7 @@ struct X6Op {
   static constexpr int PLANE = R * XBK;                 // bf16 elements of one plane image
   static constexpr int NI = KC ? R / 64 : 1;             // float4 items per thread (k-contiguous)
   static constexpr int KR = KC ? 4 : R / 16;             // k-run per thread (r-contiguous): 8 or 4
-  float v[KC ? 4 * NI : KR];
+  static constexpr int NV = KC ? 4 * NI : KR;  // staged values per thread and slice
   const float* rowp[NI];  // k-contiguous: row pointers (nullptr: row outside the operand)
   const float* P;
   const int64_t* krows;
@@ -935,7 +942,7 @@ struct X6Op {
       roff = r0 + rr;
     }
   }
-  __device__ __forceinline__ void load(int k0, int k_lim, bool fast) {
+  __device__ __forceinline__ void load(float (&v)[NV], int k0, int k_lim, bool fast) const {
     if (KC) {
 #pragma unroll
       for (int u = 0; u < NI; ++u) {
@@ -970,7 +977,7 @@ struct X6Op {
       }
     }
   }
-  __device__ __forceinline__ void store(uint16_t* img) const {
+  __device__ __forceinline__ void store(const float (&v)[NV], uint16_t* img) const {
     const int t = threadIdx.x;
     if (KC) {
 #pragma unroll
@@ -1003,10 +1010,10 @@ struct X6Op {
     }
   }
   // sum of this thread's staged values (bias-gradient partial of an r-contiguous A)
-  __device__ __forceinline__ float vsum() const {
+  __device__ __forceinline__ static float vsum(const float (&v)[NV]) {
     float s = 0.f;
 #pragma unroll
-    for (int e = 0; e < (int)(sizeof(v) / sizeof(float)); ++e) s += v[e];
+    for (int e = 0; e < NV; ++e) s += v[e];
     return s;
   }
 };
@@ -1044,22 +1051,10 @@ __global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 w
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  if (kbeg < kend) {
-    oa.load(kbeg, kend, fast);
-    ob.load(kbeg, kend, fast);
-    if (do_bsum) bsum += oa.vsum();
-    oa.store(S);
-    ob.store(S + 3 * PA);
-  }
-  __syncthreads();
-  int buf = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += XBK) {
-    const bool more = k0 + XBK < kend;
-    if (more) {
-      oa.load(k0 + XBK, kend, fast);
-      ob.load(k0 + XBK, kend, fast);
-    }
-    const uint16_t* As = S + buf * STG;
+  using OA = decltype(oa);
+  using OB = decltype(ob);
+  // one k-step of the 32x32x16 products on the stage at As: six MFMAs per tile (smallest products first)
+  auto compute = [&](const uint16_t* As) {
     const uint16_t* Bs = As + 3 * PA;
     bf16x8_t a[TM][3], b[TN][3];
 #pragma unroll
@@ -1085,13 +1080,94 @@ __global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 w
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
         acc[i][j] = c;
       }
+  };
+  if constexpr (LRL_X6_PIPE && FAST) {
+  // Software pipeline: slice s + 1 waits split-ready in registers while slice s is multiplied, so its split (VALU)
+  // and LDS stores interleave with slice s's MFMAs in one scheduling region; slice s + 2 is in flight meanwhile.
+  float va[2][OA::NV], vb[2][OB::NV];
+  const int ns = (kend - kbeg + XBK - 1) / XBK;
+  if (ns > 0) {
+    oa.load(va[0], kbeg, kend, fast);
+    ob.load(vb[0], kbeg, kend, fast);
+    if (ns > 1) {
+      oa.load(va[1], kbeg + XBK, kend, fast);
+      ob.load(vb[1], kbeg + XBK, kend, fast);
+    }
+    if (do_bsum) bsum += OA::vsum(va[0]);
+    oa.store(va[0], S);
+    ob.store(vb[0], S + 3 * PA);
+    if (ns > 2) {
+      oa.load(va[0], kbeg + 2 * XBK, kend, fast);
+      ob.load(vb[0], kbeg + 2 * XBK, kend, fast);
+    }
+  }
+  __syncthreads();
+  // step s: multiply stage s & 1, split + store slice s + 1 (register set (s + 1) & 1) into the other stage, then
+  // load slice s + 3 into that register set
+  auto step = [&](int s, auto par, auto full) {
+    constexpr int P = decltype(par)::value;
+    constexpr bool F = decltype(full)::value;  // s + 3 < ns: no guards
+    compute(S + P * STG);
+    if (F || s + 1 < ns) {
+      if (do_bsum) bsum += OA::vsum(va[P ^ 1]);
+      oa.store(va[P ^ 1], S + (P ^ 1) * STG);
+      ob.store(vb[P ^ 1], S + (P ^ 1) * STG + 3 * PA);
+    }
+    if (F || s + 3 < ns) {
+      oa.load(va[P ^ 1], kbeg + (s + 3) * XBK, kend, fast);
+      ob.load(vb[P ^ 1], kbeg + (s + 3) * XBK, kend, fast);
+    }
+    if constexpr (F) {
+      // interleave: the operand reads, then each MFMA followed by split / address VALU, then the stores and loads
+      constexpr int NMF = TM * TN * 6;
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * (TM + TN), 0);
+#pragma unroll
+      for (int q = 0; q < NMF; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, LRL_X6_PIPE_VALU, 0);
+      }
+    }
+    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  int s = 0;
+  for (; s + 4 < ns; s += 2) {
+    step(s, I0{}, BT{});
+    step(s + 1, I1{}, BT{});
+  }
+  for (; s < ns; s += 2) {
+    step(s, I0{}, BF{});
+    if (s + 1 < ns) step(s + 1, I1{}, BF{});
+  }
+  } else {
+  float va[OA::NV], vb[OB::NV];
+  if (kbeg < kend) {
+    oa.load(va, kbeg, kend, fast);
+    ob.load(vb, kbeg, kend, fast);
+    if (do_bsum) bsum += OA::vsum(va);
+    oa.store(va, S);
+    ob.store(vb, S + 3 * PA);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += XBK) {
+    const bool more = k0 + XBK < kend;
     if (more) {
-      if (do_bsum) bsum += oa.vsum();
-      oa.store(S + (buf ^ 1) * STG);
-      ob.store(S + (buf ^ 1) * STG + 3 * PA);
+      oa.load(va, k0 + XBK, kend, fast);
+      ob.load(vb, k0 + XBK, kend, fast);
+    }
+    compute(S + buf * STG);
+    if (more) {
+      if (do_bsum) bsum += OA::vsum(va);
+      oa.store(va, S + (buf ^ 1) * STG);
+      ob.store(vb, S + (buf ^ 1) * STG + 3 * PA);
     }
     __syncthreads();
     buf ^= 1;
+  }
   }
 
   float* __restrict__ C = p.C + g * p.gc;
