@@ -471,6 +471,31 @@ int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t N, int32_t 
                      const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, const float* aux,
                      int64_t ld_aux, const int64_t* rows, float* workspace, int64_t workspace_floats, void* stream);
 
+/* reset_idx's episode logging (legged_robot.py:261-276) for `rows` rows of a [rows][ld] f32 device table at once:
+ * means[r] = mean over the n env ids of table[r][ids] (fixed-order reduction), then, when `zero`, those entries are
+ * set to 0 (the reset envs' episode sums).  One launch on `stream`; means is a device array of `rows` floats (NaN for
+ * n == 0, as torch.mean of an empty selection).  Returns 0, or non-zero on a bad argument / launch failure. */
+int32_t lrl_rows_mean_zero(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t n, float* means,
+                           int32_t zero, void* stream);
+
+/* ---- host-side grid-adaptive command curriculum (CPU functions, no device work) ----
+ * Native form of RewardThresholdCurriculum.sample / .update (mini_gym/envs/base/curriculum.py:56-68, 105-115), which
+ * the reference runs in numpy on every resampling (legged_robot.py:595-626; lrl/curriculum.py restates it): bit-exact
+ * with numpy.random.RandomState.  mt_key / mt_pos: the generator's MT19937 state (624 words + position, numpy's
+ * RandomState.get_state()[1:3]), advanced in place.
+ * sample: bins[j] = choice(nbins, p = weights / weights.sum()) for j < n, then cmds[j][d] = uniform(grid[d][bin] +
+ * half[d], grid[d][bin] - half[d]) in C order; grid is [3][nbins] f64.  Errors as numpy's choice (p not
+ * non-negative / NaN / not summing to 1). */
+int32_t lrl_curriculum_sample(uint32_t* mt_key, int32_t* mt_pos, const double* weights, int32_t nbins,
+                              const double* grid, const double* half, int32_t n, double* cmds, int64_t* bins);
+/* update's weight adds for the successful bins `centres`: weights[centres] = clip(weights[centres] + 0.2, 0, 1), then
+ * every bin within +-local_range of each centre on all three axes (axes: the nx, ny, nz axis values, concatenated;
+ * bin = (ix * ny + iy) * nz + iz) gets one clipped add per centre, in centre order. */
+int32_t lrl_curriculum_update_weights(double* weights, const double* axes, int32_t nx, int32_t ny, int32_t nz,
+                                      const int64_t* centres, int32_t n, double local_range);
+/* numpy's np.sum of a contiguous f64 array (pairwise summation), the normaliser of the sample's p */
+double lrl_np_sum_f64(const double* a, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

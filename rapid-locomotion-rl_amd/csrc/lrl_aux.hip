@@ -250,9 +250,38 @@ __global__ void randomize_kernel(KState S, float f0, float f1, float r0, float r
   if (which & 8u) S.restitution[e] = lrl_u01(b.v[1]) * (r1 - r0) + r0;
 }
 
+// reset_idx's episode logging (legged_robot.py:261-276: torch.mean(episode_sums[key][env_ids]), then the sums of
+// those envs zeroed) for every row of a [rows][ld] table in one launch: workgroup r sums row r over the ids in a
+// fixed order (strided per-thread partials, then an LDS tree), writes the mean, and after a barrier zeroes the
+// entries it read.
+__global__ void rows_mean_zero_kernel(float* __restrict__ tab, int64_t ld, const int32_t* __restrict__ ids, int32_t n,
+                                      float* __restrict__ means, int32_t zero) {
+  __shared__ float red[256];
+  float* row = tab + (int64_t)blockIdx.x * ld;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += row[ids[i]];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) means[blockIdx.x] = n > 0 ? red[0] / (float)n : NAN;
+  if (zero)
+    for (int i = threadIdx.x; i < n; i += 256) row[ids[i]] = 0.f;
+}
+
 }  // namespace lrl
 
 extern "C" {
+int32_t lrl_rows_mean_zero(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t n, float* means,
+                           int32_t zero, void* stream) {
+  if (!table || !means || rows < 0 || n < 0 || (n > 0 && !ids)) return 1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(lrl::rows_mean_zero_kernel, dim3(rows), dim3(256), 0, static_cast<hipStream_t>(stream), table,
+                     ld, ids, n, means, zero);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* ids, int32_t n, int32_t root_mode,
                             float xy_lo, float xy_span, float x_off, float y_off, int32_t inject, int64_t counter,
                             hipStream_t st) {

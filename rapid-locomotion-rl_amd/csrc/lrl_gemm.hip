@@ -1362,7 +1362,10 @@ int gemm_pick_splits(int M, int N, int K, int groups) {
   // per split and <= 256 splits
   // per split; the partial slices (written and re-read once) stay under 12M floats
   const int64_t out = (int64_t)groups * M * N;
-  while (tiles * splits < 1024 && splits < 256 && (K / (splits * 2)) >= 128 && out * splits * 2 <= (12ll << 20))
+  // (LRL_SPLIT_WG / LRL_SPLIT_MAXF: development overrides of the workgroup target and the partial-size cap)
+  static const int wg_target = getenv("LRL_SPLIT_WG") ? atoi(getenv("LRL_SPLIT_WG")) : 512;
+  static const int64_t max_f = getenv("LRL_SPLIT_MAXF") ? atoll(getenv("LRL_SPLIT_MAXF")) : (12ll << 20);
+  while (tiles * splits < wg_target && splits < 256 && (K / (splits * 2)) >= 128 && out * splits * 2 <= max_f)
     splits *= 2;
   return splits;
 }

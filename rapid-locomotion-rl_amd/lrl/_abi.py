@@ -135,7 +135,7 @@ _lib = None
 
 _CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 # the files and order of csrc/Makefile's SRC_HASH (SRCS then HDRS)
-_HASHED = ["lrl_env.hip", "lrl_aux.hip", "lrl_gae.hip", "lrl_gemm.hip", "lrl_ppo.hip", "lrl_capi.cpp",
+_HASHED = ["lrl_env.hip", "lrl_aux.hip", "lrl_gae.hip", "lrl_gemm.hip", "lrl_ppo.hip", "lrl_capi.cpp", "lrl_curriculum.cpp",
            "lrl_kparams.h", "lrl_gemm.h", "../../include/lrl.h", "../../include/lrl_philox.h"]
 
 
@@ -172,8 +172,11 @@ def lib():
                      "lrl_ppo_optimizer_step", "lrl_ppo_adaptation_forward_backward", "lrl_ppo_adaptation_step",
                      "lrl_gemm_f32", "lrl_ppo_timing", "lrl_ppo_act_student", "lrl_sim_set_terrain",
                      "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms", "lrl_sim_inject_push_uniforms", "lrl_sim_timing",
-                     "lrl_sim_self_contact_stats", "lrl_ppo_store_step"]:
+                     "lrl_sim_self_contact_stats", "lrl_ppo_store_step", "lrl_curriculum_sample",
+                     "lrl_curriculum_update_weights", "lrl_rows_mean_zero"]:
             getattr(L, name).restype = C.c_int32
+        L.lrl_np_sum_f64.restype = C.c_double
+        L.lrl_np_sum_f64.argtypes = [C.c_void_p, C.c_int64]
         L.lrl_ppo_workspace_bytes.restype = C.c_int64
         L.lrl_ppo_act_workspace_bytes.restype = C.c_int64
         L.lrl_ppo_act_student_workspace_bytes.restype = C.c_int64
@@ -186,3 +189,19 @@ def check(rc):
         msg = lib().lrl_last_error()
         raise RuntimeError(f"liblrl error {rc}: {msg.decode() if msg else ''}")
     return rc
+
+
+_dev_index_cache = {}
+
+
+def stream_of(device):
+    """The current HIP stream of `device` as a c_void_p (torch's raw-stream accessor: no Stream object built per call —
+    a few microseconds less per launch on the host-bound upstream-reset path)."""
+    idx = _dev_index_cache.get(device)
+    if idx is None:
+        import torch
+        d = torch.device(device)
+        idx = d.index if d.index is not None else torch.cuda.current_device()
+        _dev_index_cache[device] = idx
+    import torch
+    return C.c_void_p(torch._C._cuda_getCurrentRawStream(idx))

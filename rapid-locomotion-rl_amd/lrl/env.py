@@ -60,6 +60,42 @@ class _LazyExtras(dict):
         return list(dict.keys(self)) + [k for k in self._lazy if not dict.__contains__(self, k)]
 
 
+class _Upload:
+    """Host -> device staging through pinned buffers: each put() packs numpy arrays into one pinned slot and issues one
+    non-blocking copy on the current stream, returning typed device views of it.  A ring of slots, each rewritten only
+    after its previous copy ran (an event per slot); the views are for stream-ordered use right away (a slot comes
+    round again after len(slots) puts)."""
+
+    _TD = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32, np.dtype(np.float32): torch.float32}
+
+    def __init__(self, device, nbytes, slots=4):
+        self.host = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(slots)]
+        self.hnp = [h.numpy() for h in self.host]
+        self.dev = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(slots)]
+        self.ev = [torch.cuda.Event() for _ in range(slots)]
+        self.used = [False] * slots
+        self.i = 0
+
+    def put(self, *arrays):
+        i = self.i
+        self.i = (i + 1) % len(self.host)
+        if self.used[i]:
+            self.ev[i].synchronize()
+        h, off, spans = self.hnp[i], 0, []
+        for a in arrays:
+            a = np.ascontiguousarray(a)
+            nb = a.nbytes
+            h[off:off + nb] = a.reshape(-1).view(np.uint8)
+            spans.append((off, nb, a.dtype, a.shape))
+            off = (off + nb + 255) // 256 * 256
+        if off > h.shape[0]:
+            raise ValueError("_Upload: slot too small")
+        self.dev[i][:off].copy_(self.host[i][:off], non_blocking=True)
+        self.ev[i].record()
+        self.used[i] = True
+        return [self.dev[i][o:o + nb].view(self._TD[dt]).view(shape) for o, nb, dt, shape in spans]
+
+
 class LeggedRobotEnv:
     def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
                  eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=0,
@@ -250,6 +286,8 @@ class LeggedRobotEnv:
         self._ids_all = torch.arange(self.num_envs, dtype=torch.int32, device=self.device)
         self._due_next = None  # (episode_length_buf version, env ids due for command resampling next step)
         self._step_timer = None  # optional section timer of step() (scripts/step_timing.py)
+        # pinned staging of the upstream-reset path's host->device data (ids, resampled commands, command bins)
+        self._up = _Upload(self.device, 64 * self.num_envs + 4096) if str(self.device).startswith("cuda") else None
         self._sums_host = None  # (command_sums version, host copy of the two tracking rows) between a step's sync
         keys = list(self.reward_scales)  # and the resampling it feeds
         self._track_rows = [keys.index("tracking_lin_vel"), keys.index("tracking_ang_vel")] \
@@ -263,7 +301,7 @@ class LeggedRobotEnv:
         return _dlpack.wrap(d, self._dev_index)
 
     def _stream(self):
-        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return _abi.stream_of(self.device)
 
     def close(self):
         if getattr(self, "_sim", None):
@@ -386,9 +424,12 @@ class LeggedRobotEnv:
     def resample_commands(self, env_ids, _ids_host=None):
         """_resample_commands (legged_robot.py:595-626); disconnected in the fork (Q3), callable here.
         ``_ids_host``: the same ids as a numpy array when the caller already has them on the host."""
-        if len(env_ids) == 0 and self._dist is None:  # (ranks join the collective update with no envs of their own)
+        if env_ids is not None and len(env_ids) == 0 and self._dist is None:  # (ranks join the collective update
+            return  # with no envs of their own)
+        if _ids_host is not None and len(_ids_host) == 0 and self._dist is None:
             return
-        ids = torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
+        # env_ids None: the ids exist only on the host (_ids_host) and travel with the commands' upload
+        ids = None if env_ids is None else torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
         timesteps = int(self.cfg.commands.resampling_time / self.dt)
         ep_len = min(self.cfg.env.max_episode_length, timesteps)
         # both tracking sums in one device->host copy (float32 division on the device, as torch does)
@@ -399,7 +440,8 @@ class LeggedRobotEnv:
             lin, ang = hs[1][:, ids_np] / np.float32(ep_len)
             hs[1][:, ids_np] = 0.0  # mirrors the zeroing below
         else:
-            lin, ang = (self._command_sums[self._track_rows][:, ids] / ep_len).cpu().numpy()
+            ids_d = ids if ids is not None else torch.as_tensor(ids_np, device=self.device, dtype=torch.long)
+            lin, ang = (self._command_sums[self._track_rows][:, ids_d] / ep_len).cpu().numpy()
         lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
         ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
         old_bins = self.env_command_bins[ids_np]
@@ -421,7 +463,15 @@ class LeggedRobotEnv:
         keep = (np.sqrt(c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]) > np.float32(0.2)).astype(np.float32)
         c[:, 0] *= keep
         c[:, 1] *= keep
-        self.commands[ids, :3] = torch.from_numpy(c).to(self.device)
+        if self._up is not None:  # one pinned upload of the commands (and of the ids when the caller had them on the host)
+            if ids is None:
+                ids, cd = self._up.put(np.asarray(ids_np, np.int64), c)
+            else:
+                cd, = self._up.put(c)
+        else:
+            ids = ids if ids is not None else torch.as_tensor(ids_np, device=self.device, dtype=torch.long)
+            cd = torch.from_numpy(c).to(self.device)
+        self.commands[ids, :3] = cd
         self._command_sums[:, ids] = 0.0
         if hs is not None and _ids_host is not None and hs[0] + 1 == self._command_sums._version:
             self._sums_host = (self._command_sums._version, hs[1])  # the host copy was zeroed alike
@@ -442,12 +492,13 @@ class LeggedRobotEnv:
             interval = int(self.cfg.commands.resampling_time / self.dt)
             cached = self._due_next
             if cached is not None and cached[0] == self.episode_length_buf._version:
-                due, due_np = cached[1], cached[2]  # known from the previous step's single device->host copy
+                due, due_np = None, cached[1]  # known from the previous step's single device->host copy (the ids
+                # reach the device with the resampled commands' upload)
             else:  # first step, or episode_length_buf written by a caller since: host ids from the fresh set
                 due = ((self.episode_length_buf + 1) % interval == 0).nonzero(as_tuple=False).flatten()
                 due_np = due.cpu().numpy()
             # (with several ranks every rank takes part whenever any rank has envs to resample)
-            if (len(due) > 0) if self._dist is None else (self._dist_count(len(due)) > 0):
+            if (len(due_np) > 0) if self._dist is None else (self._dist_count(len(due_np)) > 0):
                 self.resample_commands(due, due_np)
         self._sums_host = None  # the kernel below changes the command sums
         if tm is not None:
@@ -474,12 +525,13 @@ class LeggedRobotEnv:
             ids_np = np.flatnonzero(rst)
             due_np = np.flatnonzero((code >> 1) & ((rst == 0) | (interval == 1)))
             if (len(ids_np) > 0) if self._dist is None else (self._dist_count(len(ids_np)) > 0):
-                ids = torch.from_numpy(ids_np).to(self.device)
-                self.reset_idx(ids, ids_np)
-                ids32 = ids.to(torch.int32).contiguous()
+                ids, ids32 = self._up.put(ids_np.astype(np.int64), ids_np.astype(np.int32))  # one pinned upload
+                if tm is not None:
+                    tm.mark("ids_h2d")
+                self.reset_idx(ids, ids_np, _ids32=ids32)
                 _abi.check(self._L.lrl_sim_observe_idx(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
                                                        C.c_uint32(flags), self._stream()))
-            self._due_next = (eplen._version, torch.from_numpy(due_np).to(self.device), due_np)
+            self._due_next = (eplen._version, due_np)
             if tm is not None:
                 tm.mark("reset_idx_observe")
         ex = self.extras
@@ -539,34 +591,52 @@ class LeggedRobotEnv:
         obs, _, _, _ = self.step(torch.zeros(self.num_envs, self.num_actions, device=self.device))
         return obs
 
-    def reset_idx(self, env_ids, _ids_host=None):
+    def reset_idx(self, env_ids, _ids_host=None, _ids32=None):
         """legged_robot.py:227-290; train and eval envs (env id >= num_train_envs) go through their own cfg
-        for the command curriculum (_call_train_eval, :456-469) and their own episode logging."""
+        for the command curriculum (_call_train_eval, :456-469) and their own episode logging.  (_ids_host / _ids32:
+        the same ids on the host and as a device int32 array, from step's upload.)"""
         env_ids = torch.as_tensor(env_ids, device=self.device).long()
         if len(env_ids) == 0 and self._dist is None:  # (ranks join the collective curriculum steps with no envs)
             return
         self._due_next = None  # episode lengths change: the next step re-derives its resampling set
+        tm = self._step_timer
         n_tr = self.num_train_envs
         if self.num_eval_envs:
             tr, ev = env_ids[env_ids < n_tr], env_ids[env_ids >= n_tr]
         else:
             tr, ev = env_ids, env_ids[:0]
+        one_group = self.eval_cfg is None
+        if _ids32 is None or not one_group:
+            _ids32 = None
         if self.custom_origins:
             for ids, c in self._groups(env_ids):
-                self._update_terrain_curriculum(ids, c)
+                self._update_terrain_curriculum(ids, c, _ids32)
         if len(tr) or self._dist is not None:
             self.update_command_curriculum(tr, self.cfg)
         if len(ev) or (self._dist is not None and self.num_eval_envs):
             self.update_command_curriculum(ev, self.eval_cfg)
+        if tm is not None:
+            tm.mark("r_terrain_cmdcurr")
         if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
             self.resample_commands(env_ids, _ids_host)
+        if tm is not None:
+            tm.mark("r_resample")
         # episode logging before the per-env sums are zeroed (:261-276)
         if len(tr):
             ep = {}
-            means = self._episode_sums[:, tr].mean(dim=1)
+            es = self._episode_sums
+            if es.stride(1) == 1 and es.is_cuda:  # means and zeroing in one launch (lrl_rows_mean_zero)
+                tr32 = _ids32 if _ids32 is not None else tr.to(torch.int32).contiguous()
+                means = torch.empty(es.shape[0], device=self.device)
+                _abi.check(self._L.lrl_rows_mean_zero(C.c_void_p(es.data_ptr()), C.c_int64(es.stride(0)),
+                                                      C.c_int32(es.shape[0]), C.c_void_p(tr32.data_ptr()),
+                                                      C.c_int32(len(tr32)), C.c_void_p(means.data_ptr()), C.c_int32(1),
+                                                      self._stream()))
+            else:
+                means = es[:, tr].mean(dim=1)
+                es[:, tr] = 0.0
             for k, m in zip(self.episode_sums, means.unbind(0)):  # (one call for all the 0-d views)
                 ep["rew_" + k] = m
-            self._episode_sums[:, tr] = 0.0
             self.extras["train/episode"] = ep
         if len(ev):
             self.extras["eval/episode"] = {}
@@ -574,14 +644,23 @@ class LeggedRobotEnv:
                 unset = ev[self.episode_sums_eval[k][ev] == -1]
                 self.episode_sums_eval[k][unset] = self.episode_sums[k][unset]
             self._episode_sums[:, ev] = 0.0
-        self._reset_device(env_ids)
+        if tm is not None:
+            tm.mark("r_episode_log")
+        self._reset_device(env_ids, _ids32)
+        if tm is not None:
+            tm.mark("r_reset_device")
         ep = self.extras.get("train/episode")
         if ep is None:
             ep = self.extras["train/episode"] = {}
         if self.cfg.terrain.curriculum:  # :278-280
             ep["terrain_level"] = torch.mean(self.terrain_levels[:self.num_train_envs].float())
-        if self.cfg.commands.command_curriculum:
-            self.env_command_bins_t = torch.tensor(self.env_command_bins, dtype=torch.float, device=self.device)
+        if self.cfg.commands.command_curriculum:  # (torch.tensor(env_command_bins, dtype=float), via the pinned slot)
+            if self._up is not None:
+                if self.env_command_bins_t.shape != (self.num_envs,):
+                    self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
+                self.env_command_bins_t.copy_(self._up.put(self.env_command_bins.astype(np.float32))[0])
+            else:
+                self.env_command_bins_t = torch.tensor(self.env_command_bins, dtype=torch.float, device=self.device)
             self.extras["env_bins"] = self.env_command_bins_t[:self.num_train_envs]
             ep["command_area"] = np.sum(self.curriculum.weights) / self.curriculum.weights.shape[0]
         if self.cfg.commands.yaw_command_curriculum:  # :283-286
@@ -593,6 +672,8 @@ class LeggedRobotEnv:
                 ev_ep["max_command_yaw"] = self.eval_cfg.command_ranges["ang_vel_yaw"][1]
         if self.cfg.env.send_timeouts:
             self.extras["time_outs"] = self.time_out_buf[:self.num_train_envs]
+        if tm is not None:
+            tm.mark("r_extras")
 
     def _root_mode(self):
         """_reset_root_states (legged_robot.py:714-755) as a reset_kernel root mode (lrl.h): the plane path writes
@@ -603,15 +684,16 @@ class LeggedRobotEnv:
             return 1
         return 0 if self.legacy_fork else 2
 
-    def _reset_device(self, env_ids):
+    def _reset_device(self, env_ids, _ids32=None):
         """The device part of reset_idx, one launch per train / eval group (each with its cfg's init ranges):
         _randomize_dof_props, _reset_dofs, _reset_root_states and the buffer zeroing (:247-259).  A test may set
         ``reset_uniforms`` ([len(env_ids), 5] device f32: motor strength, Kp, Kd, x, y per env id) to replace the
         draws of the next reset."""
         inj, self.reset_uniforms = getattr(self, "reset_uniforms", None), None
         mode = self._root_mode()
-        for ids, c in (self._groups(env_ids) if len(env_ids) else []):
-            ids32 = ids.to(torch.int32).contiguous()
+        groups = self._groups(env_ids) if len(env_ids) else []
+        for ids, c in groups:
+            ids32 = _ids32 if (_ids32 is not None and len(groups) == 1) else ids.to(torch.int32).contiguous()
             flags = 0
             if inj is not None:
                 rows = inj if len(ids) == len(env_ids) else inj[torch.isin(env_ids, ids)]
@@ -632,7 +714,7 @@ class LeggedRobotEnv:
         tests replace it to inject the reference's draws)."""
         return torch.randint(0, high, like.shape, generator=self._level_gen, device=self.device, dtype=like.dtype)
 
-    def _update_terrain_curriculum(self, env_ids, cfg):
+    def _update_terrain_curriculum(self, env_ids, cfg, _ids32=None):
         """legged_robot.py:793-818: robots that walked past half a tile move a level up, those that covered less
         than half of their commanded distance move down (not both); past the last level a random level."""
         if not cfg.terrain.curriculum or not getattr(self, "init_done", False):
@@ -640,7 +722,7 @@ class LeggedRobotEnv:
         t = cfg.terrain
         if getattr(self, "_sim", None) is not None:  # one launch instead of ~25 indexed torch ops per reset
             rnd = self._rand_levels(env_ids, t.max_terrain_level).contiguous()  # same draw as the torch form below
-            ids32 = env_ids.to(torch.int32).contiguous()
+            ids32 = _ids32 if _ids32 is not None else env_ids.to(torch.int32).contiguous()
             to = t.terrain_origins
             _abi.check(self._L.lrl_sim_terrain_curriculum(
                 self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)), C.c_void_p(self.terrain_levels.data_ptr()),

@@ -197,7 +197,7 @@ class ActorCritic(nn.Module):
         mean = torch.empty(n, self.num_actions, device=dev)
         latent = torch.empty(n, net.latent, device=dev)
         ptr = lambda t: C.c_void_p(t.data_ptr())
-        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        stream = _abi.stream_of(dev)
         _abi.check(_abi.lib().lrl_ppo_act_student(C.byref(net), ptr(self._flat), ptr(obs), ptr(hist),
                                                   C.c_int32(hist.stride(0)), C.c_int32(n), ptr(mean), ptr(latent),
                                                   ptr(ws[1]), stream))
@@ -222,7 +222,7 @@ class ActorCritic(nn.Module):
         logp = torch.empty(n, device=dev)
         ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
         st = C.byref(store) if store is not None else None
-        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        stream = _abi.stream_of(dev)
         _abi.check(_abi.lib().lrl_ppo_act(C.byref(net), ptr(self._flat), ptr(obs), ptr(priv), ptr(hist), C.c_int32(n),
                                           ptr(eps), C.c_uint64(seed), C.c_uint64(counter), ptr(actions), ptr(mu),
                                           ptr(values), ptr(logp), st, C.c_int32(store_row), ptr(ws[1]), stream))

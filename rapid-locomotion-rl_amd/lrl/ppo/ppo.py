@@ -136,7 +136,7 @@ class PPO:
             raise AssertionError("Rollout buffer overflow")
         i = s.step
         p = lambda x: C.c_void_p(x.data_ptr()) if x is not None else None
-        stream = C.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+        stream = _abi.stream_of(rewards.device)
         _abi.check(_abi.lib().lrl_ppo_store_step(p(rewards), p(dones), p(bins), p(t.values if tout is not None else None),
                                                  p(tout), C.c_float(PPO_Args.gamma), C.c_int32(n), p(s.rewards[i]),
                                                  p(s.dones[i]), p(s.env_bins[i]), stream))
@@ -210,7 +210,7 @@ class PPO:
         world = _world()
         L = _abi.lib()
         ptr = lambda t: C.c_void_p(t.data_ptr())
-        stream = C.c_void_p(torch.cuda.current_stream(st["grads"].device).cuda_stream)
+        stream = _abi.stream_of(st["grads"].device)
         indices = torch.randperm(nmb * mb, requires_grad=False, device=self.device)
         trace = []
         flat = lambda t: t.flatten(0, 1)

@@ -103,7 +103,7 @@ class RolloutStorage:
             self._ws = torch.empty(4096, device=self.device)
         lv = last_values.contiguous().float()
         p = lambda t: C.c_void_p(t.data_ptr())
-        stream = C.c_void_p(torch.cuda.current_stream(self.rewards.device).cuda_stream)
+        stream = _abi.stream_of(self.rewards.device)
         if reduce_stats is None:
             _abi.check(_abi.lib().lrl_gae(p(self.rewards), p(self.dones), p(self.values), p(lv), C.c_int32(T),
                                           C.c_int32(N), C.c_float(gamma), C.c_float(lam), p(self.returns),

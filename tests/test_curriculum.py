@@ -54,3 +54,50 @@ def test_vectorised_update_equals_the_reference_loop():
             np.testing.assert_array_equal(c.weights, ref.weights)
             np.testing.assert_array_equal(c.episode_reward_lin, ref.episode_reward_lin)
             np.testing.assert_array_equal(c.episode_reward_ang, ref.episode_reward_ang)
+
+
+def test_native_curriculum_matches_numpy_form():
+    """lrl_curriculum_sample / lrl_curriculum_update_weights (csrc/lrl_curriculum.cpp: MT19937, numpy's pairwise sum,
+    choice's cdf + searchsorted, the uniform cell draws, the clipped neighbourhood adds) against the numpy form of
+    lrl/curriculum.py on the same generator state: identical bins, commands, weights and generator position over random
+    update / sample sequences (batch sizes 1 .. 4096, duplicate centres, grid edges, weights at the clip), with draws
+    made through ``rng`` in between (the native stream continues from them)."""
+    import ctypes as C
+    from lrl import _abi
+    from lrl.curriculum import RewardThresholdCurriculum
+    rng = np.random.default_rng(5)
+    L = _abi.lib()
+    for n in (1, 7, 8, 127, 128, 129, 1000, 5202, 6001):  # numpy's np.sum restated (pairwise blocks of 8 / 128)
+        a = rng.random(n) * rng.choice([1.0, 1e-3, 1e3], n)
+        assert L.lrl_np_sum_f64(a.ctypes.data_as(C.c_void_p), n) == np.sum(a)
+    for trial in range(6):
+        nat = RewardThresholdCurriculum(seed=100 + trial, x_vel=(-10, 10, 51), y_vel=(-0.6, 0.6, 2), yaw_vel=(-10, 10, 51))
+        ref = RewardThresholdCurriculum(seed=100 + trial, x_vel=(-10, 10, 51), y_vel=(-0.6, 0.6, 2), yaw_vel=(-10, 10, 51))
+        assert nat._native
+        ref._native = False  # the numpy form
+        for c in (nat, ref):
+            c.set_to(low=np.array([-1.0, -0.6, -1.0]), high=np.array([1.0, 0.6, 1.0]))
+        for step in range(8):
+            n = int(rng.choice([1, 3, 64, 500, 4096]))
+            cn, bn = nat.sample(n)
+            cr, br = ref.sample(n)
+            np.testing.assert_array_equal(bn, br)
+            np.testing.assert_array_equal(cn, cr)
+            lin = rng.random(n).astype(np.float32)
+            ang = rng.random(n).astype(np.float32)
+            bins = bn.copy()
+            if step % 3 == 1:
+                bins[: n // 2] = bins[0]
+                bins[-1:] = len(nat) - 1
+            nat.update(bins, lin, ang, 0.3, 0.2, local_range=[0.5, 0.1, 1.0][step % 3])
+            ref.update(bins, lin, ang, 0.3, 0.2, local_range=[0.5, 0.1, 1.0][step % 3])
+            np.testing.assert_array_equal(nat.weights, ref.weights)
+            if step == 4:  # a draw through the RandomState view: both streams continue from it
+                assert nat.rng.random_sample() == ref.rng.random_sample()
+            if step == 5:  # a deep copy continues the same stream on its own arrays (no shared native caches)
+                import copy
+                twin = copy.deepcopy(nat)
+                np.testing.assert_array_equal(twin.sample(9)[1], copy.deepcopy(nat).sample(9)[1])
+                assert twin.weights is not nat.weights
+        assert nat.rng.get_state()[2] == ref.rng.get_state()[2]
+        np.testing.assert_array_equal(nat.rng.get_state()[1], ref.rng.get_state()[1])
