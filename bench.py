@@ -25,6 +25,10 @@ ENVS_PER_GPU = 4096
 B_ENV = 1325            # algorithmic HBM bytes per env-step; history shift adds 4872
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TF = 157.3  # dense fp32 MFMA peak (v_mfma_f32_32x32x2_f32, MI355X_MICROARCH.md)
+# The update's fp32 products run on the bf16 MFMA with an exact 3-way operand split and six products per k-step
+# (csrc/lrl_gemm.hip gemm_x6_kernel, fp32-class error): their bound is the dense bf16 peak / 6 per fp32 FLOP
+MFMA_BF16_PEAK_TF = 2500.0
+X6_PEAK_TF = MFMA_BF16_PEAK_TF / 6
 
 
 def pmc_traffic(*kernels):
@@ -336,6 +340,9 @@ def main():
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": n_dev, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "dtype_note": ("f32 throughout (the reference's precision); the update's / act's products are fp32 products "
+                           "computed on the bf16 MFMA from an exact 3-way split of each fp32 operand (6 products, fp32 "
+                           "accumulation; error at the fp32 MFMA's level, DESIGN.md §3)"),
             "config": {"workload": WORKLOADS[args.workload](world),
                        "envs_per_gpu": ENVS_PER_GPU, "global_envs": world * ENVS_PER_GPU,
                        "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
@@ -356,16 +363,19 @@ def main():
                                  "per 16 envs, the slowest wave sets the launch), see DESIGN.md"},
             "roofline_update_gemm": {
                 "bound": "mfma", "kernel": f"{gemm_kernel} (dW2: 2 x 256x512, {mb_rows} rows)",
-                "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": MFMA_F32_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(gemm_tf / MFMA_F32_PEAK_TF, 4) if gemm_tf else None,
+                "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": round(X6_PEAK_TF, 1),
+                "unit": "TFLOP/s", "frac": round(gemm_tf / X6_PEAK_TF, 4) if gemm_tf else None,
+                "arithmetic": "fp32 operands split exactly into 3 bf16 parts, 6 bf16 MFMA products per k-step, fp32 "
+                              "accumulation (error at the fp32 level, tests/test_gemm_gpu.py); peak = dense bf16 MFMA "
+                              f"{MFMA_BF16_PEAK_TF:.0f} TF / 6 (the fp32 MFMA peak is {MFMA_F32_PEAK_TF} TF)",
                 "traffic": round(gemm_traffic) if gemm_traffic else None, "traffic_source": gemm_traffic_src,
                 "algorithmic_bytes": 4 * (2 * mb_rows * (256 + 512)),
                 "launch_ms": round(gemm_ms, 4), "launches": g_n.value,
                 "note": "the GEMM family is ~70% of the iteration's GPU time; this is its largest launch "
                         "(split-k partials written to the workspace count in traffic)"},
             "roofline_iteration": {
-                "bound": "mfma", "achieved": round(iter_tf, 2), "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(iter_tf / MFMA_F32_PEAK_TF, 4), "flop_per_iteration": iter_flop,
+                "bound": "mfma", "achieved": round(iter_tf, 2), "peak": round(X6_PEAK_TF, 1), "unit": "TFLOP/s",
+                "frac": round(iter_tf / X6_PEAK_TF, 4), "flop_per_iteration": iter_flop,
                 "note": "SURVEY.md §8(d): 3.92 MFLOP per row and epoch (update) + 0.94 MFLOP per rollout row; "
                         "the env step's work is not counted"},
             "reference_context": {"upstream_example_run_env_steps_per_s": 41176, "upstream_ppo_iters_per_s": 0.429,
