@@ -43,6 +43,19 @@ struct GemmTile {
   static_assert(TM >= 1 && TN >= 1, "tile shape");
 };
 
+// trace tag of a weight-gradient shape (M x N per group, groups): 1 = the update's largest product, the actor /
+// critic layer-2 gradient (256 x 512, 2 groups); 2 = their layer 3 (128 x 256, 2 groups); 3 = their layer 1
+// (512 x 60); 4 = the adaptation module's first layer (256 x 630 history); 5 = the env-factor encoder's first
+// layer (256 x 18); 6 = its second (128 x 256, 1 group); 0 = any other shape
+static int tn_shape_tag(int M, int N, int groups) {
+  if (M == 256 && N == 512) return 1;
+  if (M == 128 && N == 256) return groups > 1 ? 2 : 6;
+  if (M == 512 && N <= 64) return 3;
+  if (M == 256 && N >= 600) return 4;
+  if (M == 256 && N <= 64) return 5;
+  return 0;
+}
+
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
 
 // load 4 consecutive floats (all in range) with the widest access the operand's alignment allows
@@ -824,19 +837,6 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_glds_tn_kernel(GemmP p) {
     p.bias_part[((int64_t)sp * p.groups + g) * p.M + m0 + threadIdx.x] = bsum;
 }
 
-// trace tag of a weight-gradient shape (M x N per group, groups): 1 = the update's largest product, the actor /
-// critic layer-2 gradient (256 x 512, 2 groups); 2 = their layer 3 (128 x 256, 2 groups); 3 = their layer 1
-// (512 x 60); 4 = the adaptation module's first layer (256 x 630 history); 5 = the env-factor encoder's first
-// layer (256 x 18); 6 = its second (128 x 256, 1 group); 0 = any other shape
-static int tn_shape_tag(int M, int N, int groups) {
-  if (M == 256 && N == 512) return 1;
-  if (M == 128 && N == 256) return groups > 1 ? 2 : 6;
-  if (M == 512 && N <= 64) return 3;
-  if (M == 256 && N >= 600) return 4;
-  if (M == 256 && N <= 64) return 5;
-  return 0;
-}
-
 template <int BN, int SHAPE>
 static int launch_glds_tn_tag(const GemmP& p, int groups, hipStream_t st) {
   const size_t lds = (size_t)3 * 16 * (128 + BN) * sizeof(float) + (p.b_rows ? (size_t)p.kps * sizeof(int) : 0);
@@ -1018,7 +1018,9 @@ struct X6Op {
   }
 };
 
-template <int BM, int BN, int LAYOUT, int EPI, bool FAST, bool BGATHER>
+// TAG: trace tag only (the weight-gradient shape, tn_shape_tag): each of the update's large weight gradients gets its own
+// symbol so a kernel trace / PMC pass keys its launches apart; the code is the same for every value
+template <int BM, int BN, int LAYOUT, int EPI, bool FAST, bool BGATHER, int TAG = 0>
 __global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 waves / SIMD: 3 workgroups per CU (LDS 48 KB)
   constexpr bool AKC = (LAYOUT & 1) == 0, BKC = (LAYOUT & 2) == 0;
   constexpr int PA = BM * XBK, PB = BN * XBK, STG = 3 * (PA + PB);
@@ -1252,8 +1254,15 @@ static int launch_x6_tile(const GemmP& p, int layout, int epi, int groups, hipSt
     else if (epi == EPI_DELU) LRL_X6(GEMM_NN, EPI_DELU);
     else return LRL_E_INVALID;
   } else if (layout == GEMM_TN && epi == EPI_PARTIAL) {
-    if (bg) LRL_X6G(GEMM_TN, EPI_PARTIAL, true);
+    const int tag = (BM == 128 && BN == 128 && interior) ? tn_shape_tag(p.M, p.N, groups) : 0;
+#define LRL_X6T(G, T) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, GEMM_TN, EPI_PARTIAL, true, G, T>), grid, dim3(GTHREADS), 0, st, p)
+    if (tag == 1) LRL_X6T(false, 1);
+    else if (tag == 2) LRL_X6T(false, 2);
+    else if (tag == 4) { if (bg) LRL_X6T(true, 4); else LRL_X6T(false, 4); }
+    else if (tag == 6) LRL_X6T(false, 6);
+    else if (bg) LRL_X6G(GEMM_TN, EPI_PARTIAL, true);
     else LRL_X6G(GEMM_TN, EPI_PARTIAL, false);
+#undef LRL_X6T
   } else {
     return LRL_E_INVALID;
   }
@@ -1274,6 +1283,9 @@ static bool x6_enabled() {
 // returns 1 when the product was launched on the x6 kernel (0: not eligible, <0: error)
 static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
   if (!x6_enabled()) return 0;
+  // (LRL_X6_MIN: development override of the smallest output side x6 takes — 16 by default)
+  static const int min_side = getenv("LRL_X6_MIN") ? atoi(getenv("LRL_X6_MIN")) : 16;
+  if (p.N < min_side || (layout == GEMM_TN && p.M < min_side)) return 0;
   int rc;
   if (layout == GEMM_TN) {
     // (both operands r-contiguous: dword loads, any alignment)
