@@ -834,6 +834,35 @@ struct G {
   }
 };
 
+// The env-factor encoder's backward chain (five small products at the minibatch's rows, latency-bound) runs on a
+// second stream of the library's own, beside the actor / critic weight gradients of the same minibatch (they share no
+// buffer: the chain reads dlat / he1 / he2 / priv and the weights, writes dhe1 / dhe2 and its own partial slices).
+// One stream and two events per device, created on first use.  LRL_PPO_FORK=0 keeps everything on the caller's stream.
+struct Fork {
+  hipStream_t st = nullptr;
+  hipEvent_t go = nullptr, done = nullptr;
+};
+static Fork* fork_for_device() {
+  static const bool on = [] {
+    const char* e = getenv("LRL_PPO_FORK");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return nullptr;
+  static Fork forks[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  Fork& f = forks[dev];
+  if (!f.st) {
+    if (hipStreamCreateWithFlags(&f.st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&f.go, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess) {
+      f = Fork{};
+      return nullptr;
+    }
+  }
+  return &f;
+}
+
 static void launch_seg(const SegList& L0, hipStream_t st) {
   SegList L = L0;
   int total = 0;
@@ -1052,23 +1081,35 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
     part += ((hb * pl + 63) / 64) * 64;
   }
   // ---- backward ----
+  // the data-gradient chain first (dH2, dH1, the latent gradient), then the encoder's chain forks to the library's
+  // second stream while the actor / critic weight gradients run here; the split-k reduction joins both
   const int h0 = n.ac_h0, h1 = n.ac_h1, h2 = n.ac_h2;
-  g.tn(P.dh3, 2 * h2, P.h2, 2 * h1, nullptr, h2, h1, B, 2, h2, h1, part, grads + n.w3, grads + n.b3, L);
   g.nn(P.dh3, 2 * h2, w + n.w3, h1, P.dh2, 2 * h1, P.h2, 2 * h1, B, h1, h2, 2, h2, (int64_t)h2 * h1, h1, h1);
+  g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
+  // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
+  g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
+  Fork* fk = fork_for_device();
+  G ge{fk ? fk->st : st, g.part_end};
+  if (fk) {
+    if (hipEventRecord(fk->go, st) != hipSuccess || hipStreamWaitEvent(fk->st, fk->go, 0) != hipSuccess)
+      return lrl_set_error(LRL_E_HIP, "lrl_ppo_forward_backward: stream fork failed");
+  }
+  ge.tn(P.dlat, LATS, P.he2, n.enc_h1, nullptr, n.latent, n.enc_h1, B, 1, 0, 0, part, grads + n.e3w, grads + n.e3b, L);
+  ge.nn(P.dlat, LATS, w + n.e3w, n.enc_h1, P.dhe2, n.enc_h1, P.he2, n.enc_h1, B, n.enc_h1, n.latent);
+  ge.tn(P.dhe2, n.enc_h1, P.he1, n.enc_h0, nullptr, n.enc_h1, n.enc_h0, B, 1, 0, 0, part, grads + n.e2w, grads + n.e2b, L);
+  ge.nn(P.dhe2, n.enc_h1, w + n.e2w, n.enc_h0, P.dhe1, n.enc_h0, P.he1, n.enc_h0, B, n.enc_h0, n.enc_h1);
+  ge.tn(P.dhe1, n.enc_h0, bt->priv, n.num_priv, bt->rows, n.enc_h0, n.num_priv, B, 1, 0, 0, part, grads + n.e1w,
+        grads + n.e1b, L);
+  if (fk && hipEventRecord(fk->done, fk->st) != hipSuccess)
+    return lrl_set_error(LRL_E_HIP, "lrl_ppo_forward_backward: stream fork failed");
+  g.tn(P.dh3, 2 * h2, P.h2, 2 * h1, nullptr, h2, h1, B, 2, h2, h1, part, grads + n.w3, grads + n.b3, L);
   timer_begin(st);
   g.tn(P.dh2, 2 * h1, P.h1, 2 * h0, nullptr, h1, h0, B, 2, h1, h0, part, grads + n.w2, grads + n.b2, L);
   timer_end(st);
-  g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
   g.tn(P.dh1, 2 * h0, P.xa, XS, nullptr, 2 * h0, nx, B, 1, 0, 0, part, grads + n.w1, grads + n.b1, L);
-  // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
-  g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
-  g.tn(P.dlat, LATS, P.he2, n.enc_h1, nullptr, n.latent, n.enc_h1, B, 1, 0, 0, part, grads + n.e3w, grads + n.e3b, L);
-  g.nn(P.dlat, LATS, w + n.e3w, n.enc_h1, P.dhe2, n.enc_h1, P.he2, n.enc_h1, B, n.enc_h1, n.latent);
-  g.tn(P.dhe2, n.enc_h1, P.he1, n.enc_h0, nullptr, n.enc_h1, n.enc_h0, B, 1, 0, 0, part, grads + n.e2w, grads + n.e2b, L);
-  g.nn(P.dhe2, n.enc_h1, w + n.e2w, n.enc_h0, P.dhe1, n.enc_h0, P.he1, n.enc_h0, B, n.enc_h0, n.enc_h1);
-  g.tn(P.dhe1, n.enc_h0, bt->priv, n.num_priv, bt->rows, n.enc_h0, n.num_priv, B, 1, 0, 0, part, grads + n.e1w,
-       grads + n.e1b, L);
-  if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_forward_backward: backward GEMM launch failed");
+  if (fk && hipStreamWaitEvent(st, fk->done, 0) != hipSuccess)
+    return lrl_set_error(LRL_E_HIP, "lrl_ppo_forward_backward: stream join failed");
+  if (g.rc || ge.rc) return lrl_set_error(g.rc ? g.rc : ge.rc, "lrl_ppo_forward_backward: backward GEMM launch failed");
   launch_seg(L, st);
   return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_forward_backward: launch failed");
 }
