@@ -1301,7 +1301,10 @@ static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t s
     // thin kernel (B in registers) stays faster for <= 32-wide outputs over k = 512 / 1024
     if (p.K < 32) return 0;
     if (p.N <= 32 && p.K % 128 == 0 && (p.K / 128 == 4 || p.K / 128 == 8) && p.avec == 4 && p.M >= 256) return 0;
-    const int bn = p.N > 64 ? 128 : 64;
+    // (LRL_X6_SMALL_WG: development override — below this many 64 x 128 workgroups the product takes 64 x 64 tiles)
+    static const int small_wg = getenv("LRL_X6_SMALL_WG") ? atoi(getenv("LRL_X6_SMALL_WG")) : 1024;
+    int bn = p.N > 64 ? 128 : 64;
+    if (bn == 128 && (int64_t)((p.M + 63) / 64) * ((p.N + 127) / 128) * groups < small_wg) bn = 64;
     // 128-row tiles when they still give two workgroups per CU, 64 otherwise
     const int64_t wg128 = (int64_t)((p.M + 127) / 128) * ((p.N + bn - 1) / bn) * groups;
     const int bm = wg128 >= 512 ? 128 : 64;
