@@ -1380,7 +1380,11 @@ int gemm_pick_splits(int M, int N, int K, int groups) {
   // (LRL_SPLIT_WG / LRL_SPLIT_MAXF: development overrides of the workgroup target and the partial-size cap)
   static const int wg_target = getenv("LRL_SPLIT_WG") ? atoi(getenv("LRL_SPLIT_WG")) : 512;
   static const int64_t max_f = getenv("LRL_SPLIT_MAXF") ? atoll(getenv("LRL_SPLIT_MAXF")) : (12ll << 20);
-  while (tiles * splits < wg_target && splits < 256 && (K / (splits * 2)) >= 128 && out * splits * 2 <= max_f)
+  // small outputs (<= 64K elements: the encoder / adaptation layers' weight gradients) may split down to
+  // LRL_SPLIT_SMALL_ROWS rows per split: their partials are small and their few tiles need the parallelism
+  static const int small_rows = getenv("LRL_SPLIT_SMALL_ROWS") ? atoi(getenv("LRL_SPLIT_SMALL_ROWS")) : 128;
+  const int min_rows = out <= 65536 ? small_rows : 128;
+  while (tiles * splits < wg_target && splits < 256 && (K / (splits * 2)) >= min_rows && out * splits * 2 <= max_f)
     splits *= 2;
   return splits;
 }
