@@ -1,6 +1,8 @@
 // lrl_aux.hip — the non-step env kernels: reset_idx (device part), indexed state setters,
 // rigid-body-state refresh (forward kinematics), HistoryWrapper shift, DR initialisation.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 
@@ -271,9 +273,51 @@ __global__ void rows_mean_zero_kernel(float* __restrict__ tab, int64_t ld, const
     for (int i = threadIdx.x; i < n; i += 256) row[ids[i]] = 0.f;
 }
 
+// The upstream step's per-env code for the host (lrl/env.py step): bit 0 = reset now, bit 1 = due for command
+// resampling in the next step ((episode_length + 1) % interval == 0, episode length after this step's resets; every
+// env when interval == 1), as a float, then the two tracking command-sum rows the next curriculum update reads:
+// out = [code | sums[r0] | sums[r1]] (n floats each; the rows only when r0 >= 0).
+__global__ void step_code_kernel(KState S, int32_t interval, int32_t r0, int32_t r1, float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  uint32_t code = S.reset[e];
+  if (interval == 1 || (S.episode_length[e] + 1) % interval == 0) code |= 2u;
+  out[e] = (float)code;
+  if (r0 >= 0) {
+    out[S.n + e] = S.command_sums[(int64_t)r0 * S.stride + e];
+    out[2 * S.n + e] = S.command_sums[(int64_t)r1 * S.stride + e];
+  }
+}
+
+// _resample_commands' device writes (legged_robot.py:595-626 as lrl/env.py restates it): commands[ids, :3] = cmds,
+// command_sums[:, ids] = 0 (every row); then, when given, bins_out[:nb] = bins_in[:nb] (the env-bins tensor).
+__global__ void apply_commands_kernel(KState S, int32_t ncs, const int32_t* __restrict__ ids, int32_t n,
+                                      const float* __restrict__ cmds, const float* __restrict__ bins_in,
+                                      float* __restrict__ bins_out, int32_t nb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int e = ids[i];
+    for (int k = 0; k < 3; ++k) S.commands[(int64_t)k * S.stride + e] = cmds[i * 3 + k];
+    for (int r = 0; r < ncs; ++r) S.command_sums[(int64_t)r * S.stride + e] = 0.f;
+  }
+  if (bins_out && i < nb) bins_out[i] = bins_in[i];
+}
+
 }  // namespace lrl
 
 extern "C" {
+hipError_t lrl_launch_step_code(const KState* S, int32_t interval, int32_t r0, int32_t r1, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(lrl::step_code_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, *S, interval, r0, r1, out);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_apply_commands(const KState* S, int32_t ncs, const int32_t* ids, int32_t n, const float* cmds,
+                                     const float* bins_in, float* bins_out, int32_t nb, hipStream_t st) {
+  const int m = std::max(n, bins_out ? nb : 0);
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lrl::apply_commands_kernel, dim3((m + 255) / 256), dim3(256), 0, st, *S, ncs, ids, n, cmds,
+                     bins_in, bins_out, nb);
+  return hipGetLastError();
+}
 int32_t lrl_rows_mean_zero(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t n, float* means,
                            int32_t zero, void* stream) {
   if (!table || !means || rows < 0 || n < 0 || (n > 0 && !ids)) return 1;

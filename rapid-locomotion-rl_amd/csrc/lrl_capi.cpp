@@ -34,6 +34,9 @@ hipError_t lrl_env_kernel_setup(int lds_bytes);
 hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, float, float,
                             int32_t, int64_t, hipStream_t);
 hipError_t lrl_launch_set_root(const KState*, const float*, const int32_t*, int32_t, hipStream_t);
+hipError_t lrl_launch_step_code(const KState*, int32_t, int32_t, int32_t, float*, hipStream_t);
+hipError_t lrl_launch_apply_commands(const KState*, int32_t, const int32_t*, int32_t, const float*, const float*, float*,
+                                     int32_t, hipStream_t);
 hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t, int64_t*, const int64_t*,
                                          const int64_t*, const float*, int32_t, int32_t, float, float, int32_t,
                                          hipStream_t);
@@ -61,6 +64,7 @@ struct lrl_sim {
   float* d_foot_xyz = nullptr;
   void* terr = nullptr;  // terrain mesh buffers (lrl_sim_set_terrain)
   uint32_t* self_stats = nullptr;  // lrl_sim_self_contact_stats counters
+  float* d_code = nullptr;         // lrl_sim_step_code scratch [3][n]
   // lrl_sim_timing: HIP events around each env-kernel launch of lrl_sim_step (not the history-shift launch before it)
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -462,6 +466,7 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->d_foot_xyz);
   (void)hipFree(s->terr);
   (void)hipFree(s->self_stats);
+  (void)hipFree(s->d_code);
   for (auto& pr : s->ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -592,6 +597,27 @@ int32_t lrl_sim_terrain_curriculum(lrl_sim* s, const int32_t* ids, int32_t n, in
   if (n < 0 || rows <= 0 || cols <= 0) return fail(LRL_E_INVALID, "bad sizes");
   HIPCHECK(lrl_launch_terrain_curriculum(&s->S, ids, n, levels, types, rand_levels, terrain_origins, rows, cols,
                                          half_env_length, episode_length_s, max_level, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_step_code(lrl_sim* s, int32_t interval, int32_t row0, int32_t row1, float* host_out, void* stream) {
+  if (!s || !host_out || interval < 1) return fail(LRL_E_INVALID, "bad argument");
+  if ((row0 >= 0) != (row1 >= 0) || row0 >= s->hk.n_cs || row1 >= s->hk.n_cs)
+    return fail(LRL_E_INVALID, "command-sum rows out of range");
+  const int n = s->S.n;
+  if (!s->d_code) HIPCHECK(hipMalloc(&s->d_code, 3ull * n * sizeof(float)));
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHECK(lrl_launch_step_code(&s->S, interval, row0, row1, s->d_code, st));
+  HIPCHECK(hipMemcpyAsync(host_out, s->d_code, (row0 >= 0 ? 3ull : 1ull) * n * sizeof(float), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int32_t lrl_sim_apply_commands(lrl_sim* s, const int32_t* ids, int32_t n, const float* cmds, const float* bins_in,
+                               float* bins_out, int32_t nbins, void* stream) {
+  if (!s || n < 0 || (n > 0 && (!ids || !cmds)) || (bins_out && (!bins_in || nbins < 0 || nbins > s->S.n)))
+    return fail(LRL_E_INVALID, "bad argument");
+  HIPCHECK(lrl_launch_apply_commands(&s->S, s->hk.n_cs, ids, n, cmds, bins_in, bins_out, nbins, (hipStream_t)stream));
   return 0;
 }
 

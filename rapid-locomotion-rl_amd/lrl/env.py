@@ -421,9 +421,11 @@ class LeggedRobotEnv:
         dist.all_gather(bufs, buf)
         return np.concatenate([b[:c].cpu().numpy() for b, c in zip(bufs, cnts)]), sum(cnts[:rank])
 
-    def resample_commands(self, env_ids, _ids_host=None):
+    def resample_commands(self, env_ids, _ids_host=None, _ids32=None, _bins_to=None):
         """_resample_commands (legged_robot.py:595-626); disconnected in the fork (Q3), callable here.
-        ``_ids_host``: the same ids as a numpy array when the caller already has them on the host."""
+        ``_ids_host``: the same ids as a numpy array when the caller already has them on the host; ``_ids32``: as a
+        device int32 array; ``_bins_to``: a device float tensor that receives all envs' command bins (reset_idx's
+        env_bins) in the same launch."""
         if env_ids is not None and len(env_ids) == 0 and self._dist is None:  # (ranks join the collective update
             return  # with no envs of their own)
         if _ids_host is not None and len(_ids_host) == 0 and self._dist is None:
@@ -463,18 +465,22 @@ class LeggedRobotEnv:
         keep = (np.sqrt(c[:, 0] * c[:, 0] + c[:, 1] * c[:, 1]) > np.float32(0.2)).astype(np.float32)
         c[:, 0] *= keep
         c[:, 1] *= keep
-        if self._up is not None:  # one pinned upload of the commands (and of the ids when the caller had them on the host)
-            if ids is None:
-                ids, cd = self._up.put(np.asarray(ids_np, np.int64), c)
-            else:
-                cd, = self._up.put(c)
-        else:
-            ids = ids if ids is not None else torch.as_tensor(ids_np, device=self.device, dtype=torch.long)
-            cd = torch.from_numpy(c).to(self.device)
-        self.commands[ids, :3] = cd
-        self._command_sums[:, ids] = 0.0
-        if hs is not None and _ids_host is not None and hs[0] + 1 == self._command_sums._version:
-            self._sums_host = (self._command_sums._version, hs[1])  # the host copy was zeroed alike
+        # one pinned upload (int32 ids unless the caller has them on the device, the commands, the bins when asked for)
+        # and one launch: commands[ids, :3] = c, command_sums[:, ids] = 0, bins (lrl_sim_apply_commands)
+        arrays = ([] if _ids32 is not None else [np.asarray(ids_np, np.int32)]) + [c]
+        if _bins_to is not None:
+            arrays.append(self.env_command_bins.astype(np.float32))
+        up = self._up.put(*arrays)
+        ids32 = _ids32 if _ids32 is not None else up[0]
+        cd = up[0 if _ids32 is not None else 1]
+        bins = up[-1] if _bins_to is not None else None
+        _abi.check(self._L.lrl_sim_apply_commands(
+            self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids_np)), C.c_void_p(cd.data_ptr()),
+            C.c_void_p(bins.data_ptr() if bins is not None else 0),
+            C.c_void_p(_bins_to.data_ptr() if _bins_to is not None else 0),
+            C.c_int32(len(_bins_to) if _bins_to is not None else 0), self._stream()))
+        # (the kernel's writes do not move the tensors' version counters: the step's host copy of the tracking sums,
+        # zeroed above for these ids, stays valid)
 
     # -------------------------------------------------------------------------------- API
     def step(self, actions, _history=False):
@@ -511,14 +517,17 @@ class LeggedRobotEnv:
             # length after this step's resets: 0 for the reset envs), rows 1-2 = the tracking command sums the
             # curriculum update of the envs resampled next (resets now, due ones before the next kernel) reads
             eplen = self.episode_length_buf
-            nxt = ((eplen + 1) % interval == 0) if interval != 1 else torch.ones_like(self._reset_u8, dtype=torch.bool)
-            code = (self._reset_u8 | (nxt.to(torch.uint8) << 1)) if interval != 1 else (self._reset_u8 | 2)
+            # (lrl_sim_step_code: the code and the two tracking rows computed on the device and copied into a pinned
+            # host buffer in one call — the torch form was eight small ops and a pageable copy)
+            tr = self._track_rows if self._track_rows is not None else (-1, -1)
+            if getattr(self, "_code_host", None) is None:
+                self._code_host = torch.empty(3 * self.num_envs, dtype=torch.float32, pin_memory=True).numpy()
+            _abi.check(self._L.lrl_sim_step_code(self._sim, C.c_int32(interval), C.c_int32(tr[0]), C.c_int32(tr[1]),
+                                                 C.c_void_p(self._code_host.ctypes.data), self._stream()))
+            pack = self._code_host.reshape(3, self.num_envs)
+            code = pack[0].astype(np.uint8)
             if self._track_rows is not None:
-                pack = torch.cat([code.to(torch.float32).unsqueeze(0), self._command_sums[self._track_rows]]).cpu().numpy()
-                code = pack[0].astype(np.uint8)
                 self._sums_host = (self._command_sums._version, pack[1:3])
-            else:
-                code = code.cpu().numpy()
             if tm is not None:
                 tm.mark("launch_and_sync")
             rst = code & 1
@@ -617,8 +626,14 @@ class LeggedRobotEnv:
             self.update_command_curriculum(ev, self.eval_cfg)
         if tm is not None:
             tm.mark("r_terrain_cmdcurr")
+        bins_done = False
         if not self.legacy_fork:  # upstream reset_idx resamples the reset envs' commands
-            self.resample_commands(env_ids, _ids_host)
+            bins_to = None
+            if self.cfg.commands.command_curriculum:  # the env bins travel with the commands (one upload, one launch)
+                if self.env_command_bins_t.shape != (self.num_envs,):
+                    self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
+                bins_to, bins_done = self.env_command_bins_t, True
+            self.resample_commands(env_ids, _ids_host, _ids32=_ids32, _bins_to=bins_to)
         if tm is not None:
             tm.mark("r_resample")
         # episode logging before the per-env sums are zeroed (:261-276)
@@ -655,7 +670,9 @@ class LeggedRobotEnv:
         if self.cfg.terrain.curriculum:  # :278-280
             ep["terrain_level"] = torch.mean(self.terrain_levels[:self.num_train_envs].float())
         if self.cfg.commands.command_curriculum:  # (torch.tensor(env_command_bins, dtype=float), via the pinned slot)
-            if self._up is not None:
+            if bins_done:
+                pass  # written by resample_commands' launch
+            elif self._up is not None:
                 if self.env_command_bins_t.shape != (self.num_envs,):
                     self.env_command_bins_t = torch.zeros(self.num_envs, device=self.device)
                 self.env_command_bins_t.copy_(self._up.put(self.env_command_bins.astype(np.float32))[0])
