@@ -58,7 +58,9 @@ class PPO:
         self.adaptation_module_optimizer = torch.optim.Adam(self.actor_critic.parameters(),
                                                             lr=PPO_Args.adaptation_module_learning_rate)
         self.transition = RolloutStorage.Transition()
-        self.learning_rate = PPO_Args.learning_rate
+        self._lr = float(PPO_Args.learning_rate)
+        self.async_losses = False
+        self._lr_dev = None  # the native update's ctrl tensor while its learning rate is newer than self._lr
         self.fused = (torch.device(device).type == "cuda") if fused is None else fused
         rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.seed = seed + 1000003 * rank  # per-rank policy-noise stream (counter RNG keyed by local row)
@@ -200,7 +202,23 @@ class PPO:
             st["ws_batch"] = batch
         return st
 
-    def _update_native(self):
+    @property
+    def learning_rate(self):
+        """The adaptive learning rate (ppo.py:126-133).  The native update keeps it on the device between updates (no
+        host sync at the end of an update); reading it here fetches it."""
+        if self._lr_dev is not None:
+            self._lr = float(self._lr_dev[0].item())
+            self._lr_dev = None
+            for g in self.optimizer.param_groups:
+                g["lr"] = self._lr
+        return self._lr
+
+    @learning_rate.setter
+    def learning_rate(self, v):
+        self._lr = float(v)
+        self._lr_dev = None
+
+    def _update_native(self, sync=True):
         s = self.storage
         T, N = s.num_transitions_per_env, s.num_envs
         nmb = PPO_Args.num_mini_batches
@@ -226,7 +244,8 @@ class PPO:
         batch.batch = mb
         batch.hist_ld = bufs["hist"].stride(0)
         ctrl = st["ctrl"]
-        ctrl[0] = self.learning_rate
+        if self._lr_dev is not ctrl:  # the host value is newer (first update, or set since): upload it
+            ctrl[0] = self._lr
         ctrl[1:4] = 0.0
         params, grads, m, v, ws = self.actor_critic._flat, st["grads"], st["exp_avg"], st["exp_avg_sq"], st["ws"]
         main = grads[net.main_begin:net.kl_slot + 1]
@@ -298,19 +317,24 @@ class PPO:
             cur.wait_stream(sb)
             indices.record_stream(sb)
         num_updates = PPO_Args.num_learning_epochs * nmb
-        lr, vsum, ssum, asum = ctrl[:4].tolist()
         if self.record_lr:
             self.lr_trace = torch.stack(trace).tolist()
-        self.learning_rate = lr
-        for g in self.optimizer.param_groups:
-            g["lr"] = lr
+        self._lr_dev = ctrl  # the learning rate stays on the device (read lazily by .learning_rate)
         self.storage.clear()
-        return (vsum / num_updates, ssum / num_updates,
-                asum / (num_updates * PPO_Args.num_adaptation_module_substeps))
+        losses = ctrl[1:4] / torch.tensor([num_updates, num_updates,
+                                           num_updates * PPO_Args.num_adaptation_module_substeps],
+                                          dtype=ctrl.dtype, device=ctrl.device)
+        if not sync:  # the runner's path: device scalars, converted when its logger summarises
+            return tuple(losses.unbind(0))
+        vsum, ssum, asum = losses.tolist()
+        return vsum, ssum, asum
 
     def update(self):
+        """PPO.update (ppo.py:94-178): mean value / surrogate / adaptation losses.  With ``async_losses`` set (the Runner
+        sets it) they come back as device scalars, so the host does not wait for the update before enqueuing the next
+        rollout; host floats otherwise."""
         if self.fused:
-            return self._update_native()
+            return self._update_native(sync=not self.async_losses)
         mean_value_loss = torch.zeros((), device=self.device)
         mean_surrogate_loss = torch.zeros((), device=self.device)
         mean_adaptation_module_loss = torch.zeros((), device=self.device)

@@ -19,6 +19,11 @@ from .actor_critic import ActorCritic
 from .ppo import PPO
 
 
+# LRL_RUNNER_SYNC=1: the update's losses come back as host floats each iteration (a host sync per iteration; A/B of the
+# asynchronous default)
+_SYNC_UPDATE = os.environ.get("LRL_RUNNER_SYNC", "0") == "1"
+
+
 class RunnerArgs:
     algorithm_class_name = "PPO"
     num_steps_per_env = 24
@@ -44,8 +49,9 @@ class Logger:
         self._split = time.time()
 
     def store_metrics(self, **kw):
+        # (device scalars are kept as they are and converted when summarised: no host sync per iteration)
         for k, v in kw.items():
-            self.metrics[k].append(float(v) if not isinstance(v, float) else v)
+            self.metrics[k].append(v if isinstance(v, (float, torch.Tensor)) else float(v))
 
     def since(self, _="start"):
         return time.time() - self._t0
@@ -55,7 +61,7 @@ class Logger:
         return t
 
     def log_metrics_summary(self, key_values=None):
-        s = {k: sum(v) / len(v) for k, v in self.metrics.items() if v}
+        s = {k: float(sum(v) / len(v)) for k, v in self.metrics.items() if v}
         s.update(key_values or {})
         self.summaries.append(s)
         self.metrics.clear()
@@ -78,6 +84,7 @@ class Runner:
         ac = ActorCritic(self.env.num_obs, self.env.num_privileged_obs, self.env.num_obs_history,
                          self.env.num_actions).to(self.device)
         self.alg = PPO(ac, device=self.device, seed=seed)
+        self.alg.async_losses = not _SYNC_UPDATE  # losses logged as device scalars: no host sync per iteration
         self.num_steps_per_env = RunnerArgs.num_steps_per_env
         self.alg.init_storage(self.env.num_train_envs, self.num_steps_per_env, [self.env.num_obs],
                               [self.env.num_privileged_obs], [self.env.num_obs_history], [self.env.num_actions])
