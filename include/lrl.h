@@ -323,8 +323,11 @@ int32_t lrl_sim_terrain_curriculum(lrl_sim* sim, const int32_t* env_ids, int32_t
 /* The upstream step's host-side bookkeeping input in one call (lrl/env.py step, legacy_fork=False): per env
  * code = reset | (((episode_length + 1) % interval == 0 or interval == 1) << 1) as a float, followed — when
  * row0 / row1 >= 0 — by the two command-sum rows (the tracking sums the next curriculum update reads), copied into
- * host_out (pinned host memory, [1 or 3][num_envs] f32) on `stream`; returns after the stream reached the copy. */
-int32_t lrl_sim_step_code(lrl_sim* sim, int32_t interval, int32_t row0, int32_t row1, float* host_out, void* stream);
+ * host_out (pinned host memory, [1 or 3][num_envs] f32) on `stream`; when reset_ids_out (a device int32 array of
+ * num_envs) is given, the reset envs' ids in ascending order are written there too (their count is the number of
+ * codes with bit 0 set).  Returns after the stream reached the copy. */
+int32_t lrl_sim_step_code(lrl_sim* sim, int32_t interval, int32_t row0, int32_t row1, float* host_out,
+                          int32_t* reset_ids_out, void* stream);
 /* _resample_commands' device writes (legged_robot.py:595-626): commands[ids[i], 0:3] = cmds[i][0:3],
  * command_sums[:, ids] = 0; and, when bins_out is given, bins_out[0:nbins] = bins_in[0:nbins] (the float env-bins
  * tensor of the step's extras).  Device pointers; one launch on `stream`. */

@@ -289,6 +289,28 @@ __global__ void step_code_kernel(KState S, int32_t interval, int32_t r0, int32_t
   }
 }
 
+// The step's reset env ids in ascending order (np.flatnonzero of the reset flags), compacted on the device by one
+// 1024-thread workgroup: thread t counts the flags of its contiguous run, a block-wide exclusive scan gives its write
+// offset (deterministic: the order is the env order).
+__global__ __launch_bounds__(1024) void compact_resets_kernel(KState S, int32_t* __restrict__ ids_out) {
+  __shared__ int cnt[1024];
+  const int t = threadIdx.x, n = S.n;
+  const int per = (n + 1023) / 1024, b = t * per, e = min(n, b + per);
+  int c = 0;
+  for (int i = b; i < e; ++i) c += S.reset[i] != 0;
+  cnt[t] = c;
+  __syncthreads();
+  for (int w = 1; w < 1024; w <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = t >= w ? cnt[t - w] : 0;
+    __syncthreads();
+    cnt[t] += v;
+    __syncthreads();
+  }
+  int o = cnt[t] - c;
+  for (int i = b; i < e; ++i)
+    if (S.reset[i]) ids_out[o++] = i;
+}
+
 // _resample_commands' device writes (legged_robot.py:595-626 as lrl/env.py restates it): commands[ids, :3] = cmds,
 // command_sums[:, ids] = 0 (every row); then, when given, bins_out[:nb] = bins_in[:nb] (the env-bins tensor).
 __global__ void apply_commands_kernel(KState S, int32_t ncs, const int32_t* __restrict__ ids, int32_t n,
@@ -306,8 +328,10 @@ __global__ void apply_commands_kernel(KState S, int32_t ncs, const int32_t* __re
 }  // namespace lrl
 
 extern "C" {
-hipError_t lrl_launch_step_code(const KState* S, int32_t interval, int32_t r0, int32_t r1, float* out, hipStream_t st) {
+hipError_t lrl_launch_step_code(const KState* S, int32_t interval, int32_t r0, int32_t r1, float* out, int32_t* ids_out,
+                                hipStream_t st) {
   hipLaunchKernelGGL(lrl::step_code_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, *S, interval, r0, r1, out);
+  if (ids_out) hipLaunchKernelGGL(lrl::compact_resets_kernel, dim3(1), dim3(1024), 0, st, *S, ids_out);
   return hipGetLastError();
 }
 hipError_t lrl_launch_apply_commands(const KState* S, int32_t ncs, const int32_t* ids, int32_t n, const float* cmds,

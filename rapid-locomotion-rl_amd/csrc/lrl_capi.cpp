@@ -34,7 +34,7 @@ hipError_t lrl_env_kernel_setup(int lds_bytes);
 hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, float, float,
                             int32_t, int64_t, hipStream_t);
 hipError_t lrl_launch_set_root(const KState*, const float*, const int32_t*, int32_t, hipStream_t);
-hipError_t lrl_launch_step_code(const KState*, int32_t, int32_t, int32_t, float*, hipStream_t);
+hipError_t lrl_launch_step_code(const KState*, int32_t, int32_t, int32_t, float*, int32_t*, hipStream_t);
 hipError_t lrl_launch_apply_commands(const KState*, int32_t, const int32_t*, int32_t, const float*, const float*, float*,
                                      int32_t, hipStream_t);
 hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t, int64_t*, const int64_t*,
@@ -600,14 +600,15 @@ int32_t lrl_sim_terrain_curriculum(lrl_sim* s, const int32_t* ids, int32_t n, in
   return 0;
 }
 
-int32_t lrl_sim_step_code(lrl_sim* s, int32_t interval, int32_t row0, int32_t row1, float* host_out, void* stream) {
+int32_t lrl_sim_step_code(lrl_sim* s, int32_t interval, int32_t row0, int32_t row1, float* host_out,
+                          int32_t* reset_ids_out, void* stream) {
   if (!s || !host_out || interval < 1) return fail(LRL_E_INVALID, "bad argument");
   if ((row0 >= 0) != (row1 >= 0) || row0 >= s->hk.n_cs || row1 >= s->hk.n_cs)
     return fail(LRL_E_INVALID, "command-sum rows out of range");
   const int n = s->S.n;
   if (!s->d_code) HIPCHECK(hipMalloc(&s->d_code, 3ull * n * sizeof(float)));
   hipStream_t st = (hipStream_t)stream;
-  HIPCHECK(lrl_launch_step_code(&s->S, interval, row0, row1, s->d_code, st));
+  HIPCHECK(lrl_launch_step_code(&s->S, interval, row0, row1, s->d_code, reset_ids_out, st));
   HIPCHECK(hipMemcpyAsync(host_out, s->d_code, (row0 >= 0 ? 3ull : 1ull) * n * sizeof(float), hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
   return 0;

@@ -99,26 +99,37 @@ extern "C" int32_t lrl_curriculum_sample(uint32_t* mt_key, int32_t* mt_pos, cons
                                          int64_t* bins) {
   if (!mt_key || !mt_pos || !weights || !grid || !half || nbins <= 0 || n < 0 || (n > 0 && (!cmds || !bins)))
     return lrl_set_error(LRL_E_INVALID, "lrl_curriculum_sample: bad argument");
-  const double S = np_sum(weights, nbins);
-  thread_local std::vector<double> cdf;
-  cdf.resize((size_t)nbins);
-  double* c = cdf.data();
-  // RandomState.choice's checks on p: NaN, negative entries, and |kahan_sum(p) - 1| > sqrt(eps).  p = w / S with S
-  // numpy's own sum of w, so sum(p) is 1 to within nbins ulps (far inside the tolerance) unless S is 0 or not finite,
-  // which makes p NaN / inf: those are the cases the sum check can reject, and they are tested here directly.
-  bool nan = false, neg = false;
-  for (int i = 0; i < nbins; ++i) {
-    const double p = weights[i] / S;
-    c[i] = p;
-    nan |= p != p;
-    neg |= p < 0.0;
+  // the normalised cdf depends on the weights alone: reuse the last one while the weights are unchanged (the update
+  // before most resamples adds nothing: no bin of the batch passed its thresholds)
+  thread_local std::vector<double> cdf, wcopy;
+  double* c;
+  if ((int)wcopy.size() == nbins && memcmp(wcopy.data(), weights, (size_t)nbins * sizeof(double)) == 0) {
+    c = cdf.data();
+  } else {
+    wcopy.assign(weights, weights + nbins);
+    const double S = np_sum(weights, nbins);
+    cdf.resize((size_t)nbins);
+    c = cdf.data();
+    // RandomState.choice's checks on p: NaN, negative entries, and |kahan_sum(p) - 1| > sqrt(eps).  p = w / S with S
+    // numpy's own sum of w, so sum(p) is 1 to within nbins ulps (far inside the tolerance) unless S is 0 or not finite,
+    // which makes p NaN / inf: those are the cases the sum check can reject, and they are tested here directly.
+    bool nan = false, neg = false;
+    for (int i = 0; i < nbins; ++i) {
+      const double p = weights[i] / S;
+      c[i] = p;
+      nan |= p != p;
+      neg |= p < 0.0;
+    }
+    if (nan || neg || !(fabs(S) < INFINITY) || S == 0.0) {
+      wcopy.clear();  // (no cdf cached for these weights)
+      if (nan) return lrl_set_error(LRL_E_INVALID, "probabilities contain NaN");
+      if (neg) return lrl_set_error(LRL_E_INVALID, "probabilities are not non-negative");
+      return lrl_set_error(LRL_E_INVALID, "probabilities do not sum to 1");
+    }
+    for (int i = 1; i < nbins; ++i) c[i] = c[i - 1] + c[i];  // cumsum: sequential, as add.accumulate
+    const double last = c[nbins - 1];
+    for (int i = 0; i < nbins; ++i) c[i] /= last;
   }
-  if (nan) return lrl_set_error(LRL_E_INVALID, "probabilities contain NaN");
-  if (neg) return lrl_set_error(LRL_E_INVALID, "probabilities are not non-negative");
-  if (!(fabs(S) < INFINITY) || S == 0.0) return lrl_set_error(LRL_E_INVALID, "probabilities do not sum to 1");
-  for (int i = 1; i < nbins; ++i) c[i] = c[i - 1] + c[i];  // cumsum: sequential, as add.accumulate
-  const double last = c[nbins - 1];
-  for (int i = 0; i < nbins; ++i) c[i] /= last;
   MT mt{mt_key, *mt_pos};
   thread_local std::vector<double> u;
   u.resize((size_t)n);

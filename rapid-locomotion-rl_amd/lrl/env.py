@@ -431,11 +431,12 @@ class LeggedRobotEnv:
         if _ids_host is not None and len(_ids_host) == 0 and self._dist is None:
             return
         # env_ids None: the ids exist only on the host (_ids_host) and travel with the commands' upload
-        ids = None if env_ids is None else torch.as_tensor(env_ids, device=self.device, dtype=torch.long)
+        ids = None if (env_ids is None or _ids32 is not None) else torch.as_tensor(env_ids, device=self.device,
+                                                                                   dtype=torch.long)
         timesteps = int(self.cfg.commands.resampling_time / self.dt)
         ep_len = min(self.cfg.env.max_episode_length, timesteps)
         # both tracking sums in one device->host copy (float32 division on the device, as torch does)
-        ids_np = ids.cpu().numpy() if _ids_host is None else _ids_host
+        ids_np = (ids if ids is not None else _ids32).cpu().numpy() if _ids_host is None else _ids_host
         hs = self._sums_host
         if hs is not None and _ids_host is not None and hs[0] == self._command_sums._version:
             # the step's device->host copy (float32 sums / ep_len in float32, as torch divides on the device)
@@ -522,8 +523,11 @@ class LeggedRobotEnv:
             tr = self._track_rows if self._track_rows is not None else (-1, -1)
             if getattr(self, "_code_host", None) is None:
                 self._code_host = torch.empty(3 * self.num_envs, dtype=torch.float32, pin_memory=True).numpy()
+                self._rid32 = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+            # (the reset ids are compacted on the device in the same call: no host -> device upload of them)
             _abi.check(self._L.lrl_sim_step_code(self._sim, C.c_int32(interval), C.c_int32(tr[0]), C.c_int32(tr[1]),
-                                                 C.c_void_p(self._code_host.ctypes.data), self._stream()))
+                                                 C.c_void_p(self._code_host.ctypes.data),
+                                                 C.c_void_p(self._rid32.data_ptr()), self._stream()))
             pack = self._code_host.reshape(3, self.num_envs)
             code = pack[0].astype(np.uint8)
             if self._track_rows is not None:
@@ -534,10 +538,10 @@ class LeggedRobotEnv:
             ids_np = np.flatnonzero(rst)
             due_np = np.flatnonzero((code >> 1) & ((rst == 0) | (interval == 1)))
             if (len(ids_np) > 0) if self._dist is None else (self._dist_count(len(ids_np)) > 0):
-                ids, ids32 = self._up.put(ids_np.astype(np.int64), ids_np.astype(np.int32))  # one pinned upload
+                ids32 = self._rid32[:len(ids_np)]  # lrl_sim_step_code's compaction (ascending, as ids_np)
                 if tm is not None:
                     tm.mark("ids_h2d")
-                self.reset_idx(ids, ids_np, _ids32=ids32)
+                self.reset_idx(ids32, ids_np, _ids32=ids32)
                 _abi.check(self._L.lrl_sim_observe_idx(self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)),
                                                        C.c_uint32(flags), self._stream()))
             self._due_next = (eplen._version, due_np)
@@ -604,7 +608,9 @@ class LeggedRobotEnv:
         """legged_robot.py:227-290; train and eval envs (env id >= num_train_envs) go through their own cfg
         for the command curriculum (_call_train_eval, :456-469) and their own episode logging.  (_ids_host / _ids32:
         the same ids on the host and as a device int32 array, from step's upload.)"""
-        env_ids = torch.as_tensor(env_ids, device=self.device).long()
+        env_ids = torch.as_tensor(env_ids, device=self.device)
+        if env_ids.dtype not in (torch.int64, torch.int32):  # (int32 ids — the step's compaction — index as they are)
+            env_ids = env_ids.long()
         if len(env_ids) == 0 and self._dist is None:  # (ranks join the collective curriculum steps with no envs)
             return
         self._due_next = None  # episode lengths change: the next step re-derives its resampling set
