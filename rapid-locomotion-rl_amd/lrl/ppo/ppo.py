@@ -15,6 +15,7 @@ buffer) is all-reduced once per optimiser step and the advantage statistics once
 every rank takes identical steps.  ``fused=False`` keeps the torch-autograd restatement (CPU tests).
 """
 import ctypes as C
+import os
 
 import torch
 import torch.distributed as dist
@@ -24,6 +25,11 @@ import torch.nn.functional as F
 from .. import _abi
 from .actor_critic import ActorCritic
 from .rollout_storage import RolloutStorage
+
+
+# encoder-weight snapshots of the overlapped adaptation chain (see _update_native): how many minibatches the policy chain
+# may run ahead of it (LRL_ENC_SNAPSHOTS; 2 = double buffering)
+_SNAPSHOTS = max(2, int(os.environ.get("LRL_ENC_SNAPSHOTS", "4")))
 
 
 class PPO_Args:
@@ -255,7 +261,7 @@ class PPO:
         # and touches only the adaptation module's parameters, gradients and Adam moments, which phases 1 / 2 never
         # read or write.  So it runs on a second stream, overlapping phases 1 / 2 of the next minibatches (the GEMM
         # tails and small launches of one chain leave the CUs the other fills).  Its encoder target reads a snapshot
-        # of the encoder weights copied right after phase 2 of i (two buffers, alternating), so phase 2 of i + 1 may
+        # of the encoder weights copied right after phase 2 of i (a ring of _SNAPSHOTS buffers), so phase 2 of i + 1 may
         # overwrite the live ones without waiting for it; the copy for i + 2 waits until phase 3 of i has read its
         # buffer.  Each chain keeps its own launch order, so the result is bit-identical to the sequential order of
         # ppo.py:94-178.
@@ -266,14 +272,14 @@ class PPO:
                 sb = st["stream_b"] = torch.cuda.Stream(params.device)
             stream_b, ws_b = C.c_void_p(sb.cuda_stream), st["ws_b"]
             if "enc_snap" not in st:
-                st["enc_snap"] = [torch.zeros(net.total, device=params.device) for _ in range(2)]
+                st["enc_snap"] = [torch.zeros(net.total, device=params.device) for _ in range(_SNAPSHOTS)]
             e0, e1 = net.e1w, net.std_off  # the encoder's weights and biases: one contiguous range
         else:
             sb, stream_b, ws_b = cur, stream, ws
         # the adaptation chain's batch descriptor: the rows pointer of minibatch i must outlive the next C call
         batch_b = _abi.LrlPpoBatch()
         C.memmove(C.byref(batch_b), C.byref(batch), C.sizeof(batch))
-        read_done = [None, None]  # per snapshot buffer: phase 3 of the minibatch that last read it has run
+        read_done = [None] * _SNAPSHOTS  # per snapshot buffer: phase 3 of the minibatch that last read it has run
         k = 0
         for epoch in range(PPO_Args.num_learning_epochs):
             for i in range(nmb):
@@ -291,9 +297,9 @@ class PPO:
                     trace.append(ctrl[0].clone())
                 enc = None
                 if sb is not cur:
-                    snap = st["enc_snap"][k & 1]
-                    if read_done[k & 1] is not None:
-                        cur.wait_event(read_done[k & 1])
+                    snap = st["enc_snap"][k % _SNAPSHOTS]
+                    if read_done[k % _SNAPSHOTS] is not None:
+                        cur.wait_event(read_done[k % _SNAPSHOTS])
                     snap[e0:e1].copy_(params[e0:e1])
                     enc = ptr(snap)
                     sb.wait_stream(cur)
@@ -310,8 +316,8 @@ class PPO:
                                                          C.c_double(PPO_Args.adaptation_module_learning_rate),
                                                          C.c_float(scale), C.byref(hp), ptr(ctrl), stream_b))
                 if sb is not cur:
-                    read_done[k & 1] = torch.cuda.Event()
-                    read_done[k & 1].record(sb)
+                    read_done[k % _SNAPSHOTS] = torch.cuda.Event()
+                    read_done[k % _SNAPSHOTS].record(sb)
                 k += 1
         if sb is not cur:
             cur.wait_stream(sb)
