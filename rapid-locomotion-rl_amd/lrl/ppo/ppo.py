@@ -327,9 +327,14 @@ class PPO:
             self.lr_trace = torch.stack(trace).tolist()
         self._lr_dev = ctrl  # the learning rate stays on the device (read lazily by .learning_rate)
         self.storage.clear()
-        losses = ctrl[1:4] / torch.tensor([num_updates, num_updates,
-                                           num_updates * PPO_Args.num_adaptation_module_substeps],
-                                          dtype=ctrl.dtype, device=ctrl.device)
+        # the divisors are a cached device tensor: a torch.tensor(list, device=...) here is a pageable host -> device
+        # copy, which waits for the whole update to finish and so keeps the host from enqueuing the next rollout
+        den_key = (num_updates, PPO_Args.num_adaptation_module_substeps)
+        if st.get("loss_den_key") != den_key:
+            st["loss_den"] = torch.tensor([num_updates, num_updates, num_updates * den_key[1]], dtype=ctrl.dtype,
+                                          device=ctrl.device)
+            st["loss_den_key"] = den_key
+        losses = ctrl[1:4] / st["loss_den"]
         if not sync:  # the runner's path: device scalars, converted when its logger summarises
             return tuple(losses.unbind(0))
         vsum, ssum, asum = losses.tolist()
