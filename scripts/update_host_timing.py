@@ -30,6 +30,33 @@ runner = R.Runner(env, device="cuda:0", seed=1234)
 runner.learn(3, init_at_random_ep_len=True)
 torch.cuda.synchronize()
 alg = runner.alg
+env_obs = env.get_observations()
+
+
+def rollout():  # one rollout of the bench's loop (alg.act / env.step / process_env_step), nothing synchronised
+    global env_obs
+    with torch.inference_mode():
+        for _ in range(runner.num_steps_per_env):
+            a = alg.act(env_obs["obs"], env_obs["privileged_obs"], env_obs["obs_history"])
+            env_obs, rew, done, infos = env.step(a)
+            alg.process_env_step(rew, done, infos)
+        alg.compute_returns(env_obs["obs"], env_obs["privileged_obs"])
+
+
+# the update right after a rollout, once with a device sync between them and once without (the bench's order)
+for mode in ("after_rollout_synced", "after_rollout_queued"):
+    ts = []
+    for _ in range(reps):
+        rollout()
+        if mode == "after_rollout_synced":
+            torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        alg.update()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(round(e0.elapsed_time(e1), 3))
+    print(json.dumps({mode + "_update_gpu_ms": ts}))
 host, wall = [], []
 for _ in range(reps):
     s = alg.storage
