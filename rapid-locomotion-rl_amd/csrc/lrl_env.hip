@@ -193,6 +193,8 @@ struct Lds {
                    // K->leg[4], then per sphere (x, y, z, radius), then per sphere its link (int)
   int nsph;
   int lim_off;     // field offset of the joint-limit rows (LIM_* map below contact_pgs_q)
+  float* wl;       // terrain query work list (after the staged tables): [BLOCK] candidate masks, [BLOCK] offsets
+  __device__ __forceinline__ float* wlist() const { return wl; }
   __device__ __forceinline__ const KLeg& kleg(int l) const { return reinterpret_cast<const KLeg*>(ktab)[l]; }
   __device__ __forceinline__ float4 sph4(int s) const {
     return reinterpret_cast<const float4*>(ktab + 4 * KLEGF)[s];
@@ -1418,27 +1420,64 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #ifdef LRL_ENV_PROFILE
     const unsigned long long tq0 = clock64();
 #endif
-    for (uint64_t m = cand; __any((int)(m != 0ull));) {
-      if (m) {
+    // The workgroup's candidate (env slot, sphere) pairs are dealt over all its lanes, so the wave runs
+    // ceil(total / BLOCK) queries instead of the most any one lane recorded (4.6 per lane and step on average
+    // under random actions, a few times that for the busiest lane): each lane publishes its candidate mask and
+    // the exclusive prefix of the counts; item j goes to lane j % BLOCK, which finds the owner lane (the last
+    // one whose prefix is <= j) and the owner's sphere, queries it, and leaves the separation in the row's field
+    // 9 (and the world normal in 3..5 when in contact) of the owner's env slot.  The owners then activate their
+    // own contacts (the activation reads the owner's leg rates).  Same queries, same results.
+    {
+      const int lane = threadIdx.x;
+      const int cnt = __popcll(cand);
+      int inc = cnt;
+#pragma unroll
+      for (int d = 1; d < BLOCK; d <<= 1) {
+        const int v = __shfl_up(inc, d, BLOCK);
+        if (lane >= d) inc += v;
+      }
+      const int total = __shfl(inc, BLOCK - 1, BLOCK);
+      uint64_t* wl_mask = reinterpret_cast<uint64_t*>(M.wlist());
+      int* wl_off = reinterpret_cast<int*>(wl_mask + BLOCK);
+      wl_mask[lane] = cand;
+      wl_off[lane] = inc - cnt;
+      __syncthreads();
+      float4* tv = reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS);
+      for (int j = lane; j - lane < total; j += BLOCK) {
+        if (j < total) {
+          int L = 0;
+#pragma unroll
+          for (int step = BLOCK / 2; step; step >>= 1)
+            if (wl_off[L + step] <= j) L += step;
+          uint64_t mk = wl_mask[L];
+          for (int q = j - wl_off[L]; q > 0; --q) mk &= mk - 1ull;
+          const int s = __builtin_ctzll(mk);
+          float* row = M.base + (M.sph_off + s * NSF) * ENVS + (L >> 2);
+          const THit th = terrain_query(K, v3(row[6 * ENVS], row[7 * ENVS], row[8 * ENVS]), M.sph4(s).w,
+                                        P.contact_offset, tv, lane);
+#ifdef LRL_ENV_DEBUG
+          g_env_dbg[((size_t)(env_block() * ENVS + (L >> 2)) * 64 + s) * 8 + 1] = th.sep;
+#endif
+          row[9 * ENVS] = th.sep;
+          if (th.sep < P.contact_offset) {
+            row[3 * ENVS] = th.n.x;
+            row[4 * ENVS] = th.n.y;
+            row[5 * ENVS] = th.n.z;
+          }
+        }
+      }
+      __syncthreads();
+      for (uint64_t m = cand; m;) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        const THit th = terrain_query(K, v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8)), M.sph4(s).w, P.contact_offset,
-                                      reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS),
-                                      (int)threadIdx.x);
-#ifdef LRL_ENV_DEBUG
-        g_env_dbg[((size_t)(env_block() * ENVS + (int)(threadIdx.x >> 2)) * 64 + s) * 8 + 1] = th.sep;
-#endif
-        if (th.sep < P.contact_offset) {
-          M.sph(s, 3) = th.n.x;
-          M.sph(s, 4) = th.n.y;
-          M.sph(s, 5) = th.n.z;
-          activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), th.sep,
-                   mulT(R, th.n));
-        }
-#ifdef LRL_ENV_PROFILE
-        prof[15] += 1;
-#endif
+        const float sep = M.sph(s, 9);
+        if (sep < P.contact_offset)
+          activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), sep,
+                   mulT(R, v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5))));
       }
+#ifdef LRL_ENV_PROFILE
+      prof[15] += cnt;
+#endif
     }
 #ifdef LRL_ENV_PROFILE
     prof[14] += clock64() - tq0;  // terrain queries (part of kin+dyn+detect)
@@ -1857,9 +1896,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   // leg blocks first, then the contact rows, (terrain: the query's vertex block), then the model tables
   const int nsph = K->num_spheres;
   static_assert(LRL_NUM_DOF * LIMF * ENVS <= 64 * BLOCK, "joint-limit rows must fit the terrain vertex blocks");
-  const Lds M{lds, 4 * LEGF, es,
-              lds + (4 * LEGF + nsph * NSF) * ENVS + (TERR ? 64 * BLOCK : LRL_NUM_DOF * LIMF * ENVS), nsph,
-              4 * LEGF + nsph * NSF};
+  float* const ktab = lds + (4 * LEGF + nsph * NSF) * ENVS + (TERR ? 64 * BLOCK : LRL_NUM_DOF * LIMF * ENVS);
+  const Lds M{lds, 4 * LEGF, es, ktab, nsph, 4 * LEGF + nsph * NSF,
+              ktab + ((4 * KLEGF + 5 * nsph + 40 + K->self_npairs + 1) & ~1)};
   {
     const float* src = reinterpret_cast<const float*>(K->leg);
     for (int i = lane; i < 4 * KLEGF; i += BLOCK) M.ktab[i] = src[i];
