@@ -476,9 +476,13 @@ struct AdaptHeadArgs {
   int part_len;      // L*H + L + 1
 };
 
+// CH / CL: the hidden / latent widths as compile-time constants (the presets' 32 / 18: the dot-product loops unroll
+// and their LDS reads issue ahead of the FMA chain, same FMA order), 0 = read from the arguments
+template <int CH, int CL>
 __global__ __launch_bounds__(HEAD_THREADS) void adapt_head_kernel(AdaptHeadArgs a) {
   // every global load (HD2 tile, weights, the encoder targets) issued up front; the prediction dots spread over
   // (row, output) pairs; per-row squared errors summed in output order (as a sequential loop would)
+  const int H = CH ? CH : a.H, L = CL ? CL : a.L;
   __shared__ float HS[HEAD_ROWS][MAX_LAT + 1];
   __shared__ float DP[HEAD_ROWS][MAX_LAT + 1];
   __shared__ float WS[MAX_LAT][MAX_LAT + 1];
@@ -487,23 +491,23 @@ __global__ __launch_bounds__(HEAD_THREADS) void adapt_head_kernel(AdaptHeadArgs 
   const int t = threadIdx.x;
   const int r0 = blockIdx.x * HEAD_ROWS;
   const int nrows = min(HEAD_ROWS, a.B - r0);
-  for (int i = t; i < HEAD_ROWS * a.H; i += HEAD_THREADS) {
-    const int r = i / a.H, c = i - r * a.H;
+  for (int i = t; i < HEAD_ROWS * H; i += HEAD_THREADS) {
+    const int r = i / H, c = i - r * H;
     HS[r][c] = r < nrows ? a.hd2[(int64_t)(r0 + r) * a.ldh + c] : 0.f;
   }
-  for (int i = t; i < a.L * a.H; i += HEAD_THREADS) WS[i / a.H][i % a.H] = a.w[i];
-  for (int i = t; i < HEAD_ROWS * a.L; i += HEAD_THREADS) {
-    const int r = i / a.L, j = i - r * a.L;
+  for (int i = t; i < L * H; i += HEAD_THREADS) WS[i / H][i % H] = a.w[i];
+  for (int i = t; i < HEAD_ROWS * L; i += HEAD_THREADS) {
+    const int r = i / L, j = i - r * L;
     TG[r][j] = r < nrows ? a.tgt[(int64_t)(r0 + r) * a.ldt + j] : 0.f;
   }
   __syncthreads();
-  const float scale = 2.f / ((float)a.B * (float)a.L);
-  for (int i = t; i < HEAD_ROWS * a.L; i += HEAD_THREADS) {
-    const int r = i / a.L, j = i - r * a.L;
+  const float scale = 2.f / ((float)a.B * (float)L);
+  for (int i = t; i < HEAD_ROWS * L; i += HEAD_THREADS) {
+    const int r = i / L, j = i - r * L;
     float d = 0.f;
     if (r < nrows) {
       float s = 0.f;
-      for (int k = 0; k < a.H; ++k) s = fmaf(HS[r][k], WS[j][k], s);
+      for (int k = 0; k < H; ++k) s = fmaf(HS[r][k], WS[j][k], s);
       const float pred = s + a.b[j];
       d = pred - TG[r][j];
     }
@@ -513,33 +517,35 @@ __global__ __launch_bounds__(HEAD_THREADS) void adapt_head_kernel(AdaptHeadArgs 
   __syncthreads();
   if (t < HEAD_ROWS) {
     float e = 0.f;
-    for (int j = 0; j < a.L; ++j) e += TG[t][j];
+    for (int j = 0; j < L; ++j) e += TG[t][j];
     ERR[t] = e;
   }
   __syncthreads();
   float* P = a.part + (int64_t)blockIdx.x * a.part_len;
   // dHD2 (thread = (row, k) pairs)
-  for (int i = t; i < nrows * a.H; i += HEAD_THREADS) {
-    const int r = i / a.H, k = i - r * a.H;
+  for (int i = t; i < nrows * H; i += HEAD_THREADS) {
+    const int r = i / H, k = i - r * H;
     float s = 0.f;
-    for (int j = 0; j < a.L; ++j) s = fmaf(DP[r][j], WS[j][k], s);
+    for (int j = 0; j < L; ++j) s = fmaf(DP[r][j], WS[j][k], s);
     a.dhd2[(int64_t)(r0 + r) * a.ldh + k] = s * delu(HS[r][k]);
   }
-  // dW_D3 partial (thread = (j, k))
-  for (int i = t; i < a.L * a.H; i += HEAD_THREADS) {
-    const int j = i / a.H, k = i - j * a.H;
+  // dW_D3 partial (thread = (j, k)); the specialised form runs over every row of the tile (rows past nrows hold
+  // DP = 0 and ERR = 0, so they add exact zeros) so that the row loops unroll
+  const int nr = CH ? HEAD_ROWS : nrows;
+  for (int i = t; i < L * H; i += HEAD_THREADS) {
+    const int j = i / H, k = i - j * H;
     float s = 0.f;
-    for (int r = 0; r < nrows; ++r) s = fmaf(DP[r][j], HS[r][k], s);
+    for (int r = 0; r < nr; ++r) s = fmaf(DP[r][j], HS[r][k], s);
     P[i] = s;
   }
-  if (t < a.L) {
+  if (t < L) {
     float s = 0.f;
-    for (int r = 0; r < nrows; ++r) s += DP[r][t];
-    P[a.L * a.H + t] = s;
+    for (int r = 0; r < nr; ++r) s += DP[r][t];
+    P[L * H + t] = s;
   } else if (t == 64) {
     float s = 0.f;
-    for (int r = 0; r < nrows; ++r) s += ERR[r];
-    P[a.L * a.H + a.L] = s;
+    for (int r = 0; r < nr; ++r) s += ERR[r];
+    P[L * H + L] = s;
   }
 }
 
@@ -1178,7 +1184,10 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
   AdaptHeadArgs aa{};
   aa.hd2 = P.hd2; aa.ldh = HD2S; aa.tgt = P.tgt; aa.ldt = LATS; aa.dhd2 = P.dhd2; aa.w = w + n.d3w; aa.b = w + n.d3b;
   aa.B = B; aa.H = n.ad_h1; aa.L = n.latent; aa.part = part; aa.part_len = n.latent * n.ad_h1 + n.latent + 1;
-  hipLaunchKernelGGL(adapt_head_kernel, dim3(hb), dim3(HEAD_THREADS), 0, st, aa);
+  if (aa.H == 32 && aa.L == 18)
+    hipLaunchKernelGGL((adapt_head_kernel<32, 18>), dim3(hb), dim3(HEAD_THREADS), 0, st, aa);
+  else
+    hipLaunchKernelGGL((adapt_head_kernel<0, 0>), dim3(hb), dim3(HEAD_THREADS), 0, st, aa);
   {
     const int64_t pl = aa.part_len;
     L.s[L.n++] = Seg{part, grads + n.d3w, (int64_t)n.latent * n.ad_h1, pl, hb, 1.f};
