@@ -43,12 +43,34 @@ __device__ __forceinline__ float delu(float h) { return h > 0.f ? 1.f : h + 1.f;
 
 // ---------------------------------------------------------------------------------------------------
 // gather obs rows into the actor/critic input X = [obs | latent | 0-pad] ([B][64])
+// thread = (group of PREP_R rows, column): the group's row indices, then its values, are loaded before any store, so
+// a thread has PREP_R gathers in flight and the grid is resident in one round (one thread per element left most of
+// a minibatch's workgroups waiting behind two dependent load latencies)
+constexpr int PREP_R = 4;
 __global__ void ppo_prep_kernel(const float* __restrict__ obs, const int64_t* __restrict__ rows, int B, int no,
                                 int xs, float* __restrict__ X) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)B * xs) return;
-  const int b = (int)(i / xs), c = (int)(i - (int64_t)b * xs);
-  X[i] = c < no ? obs[(rows ? rows[b] : (int64_t)b) * no + c] : 0.f;
+  const int64_t ng = ((int64_t)B + PREP_R - 1) / PREP_R;
+  if (i >= ng * xs) return;
+  const int g = (int)(i / xs), c = (int)(i - (int64_t)g * xs);
+  int64_t src[PREP_R];
+  float v[PREP_R];
+#pragma unroll
+  for (int u = 0; u < PREP_R; ++u) {
+    const int b = g * PREP_R + u;
+    src[u] = b < B ? (rows ? rows[b] : (int64_t)b) : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < PREP_R; ++u) v[u] = (c < no && src[u] >= 0) ? obs[src[u] * no + c] : 0.f;
+#pragma unroll
+  for (int u = 0; u < PREP_R; ++u) {
+    const int b = g * PREP_R + u;
+    if (b < B) X[(int64_t)b * xs + c] = v[u];
+  }
+}
+
+inline unsigned prep_blocks(int64_t rows, int xs) {
+  return (unsigned)((((rows + PREP_R - 1) / PREP_R) * xs + 255) / 256);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -934,7 +956,7 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(n, XS)), dim3(256), 0, st, obs,
                      (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
   g.nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1, nt.enc_h0, true);
@@ -1000,7 +1022,7 @@ extern "C" int32_t lrl_ppo_act_student(const lrl_ppo_net* net, const float* para
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)n * XS + 255) / 256)), dim3(256), 0, st, obs,
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(n, XS)), dim3(256), 0, st, obs,
                      (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   if (hld >= hpad && hld % 4 == 0 && ((uintptr_t)hist & 15) == 0 && hpad != nt.num_hist) {
     const int64_t cnt = (int64_t)nt.ad_h0 * hpad;
@@ -1045,7 +1067,7 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   const float* w = params;
   const int nx = n.num_obs + n.latent, XS = xs_of(n);
   // ---- forward ----
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3((unsigned)(((int64_t)B * XS + 255) / 256)), dim3(256), 0, st, bt->obs,
+  hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(B, XS)), dim3(256), 0, st, bt->obs,
                      bt->rows, B, n.num_obs, XS, P.xa);
   g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
   g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
