@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define LRL_ABI_VERSION 2
+#define LRL_ABI_VERSION 3
 
 #define LRL_OK 0
 #define LRL_E_INVALID (-1)  /* bad argument / unsupported configuration */
@@ -340,6 +340,21 @@ int32_t lrl_sim_set_root_state_indexed(lrl_sim* sim, const float* root /*[N,13] 
 int32_t lrl_sim_set_dof_state_indexed(lrl_sim* sim, const float* dof_pos, const float* dof_vel,
                                       const int32_t* env_ids, int32_t n, void* stream);
 int32_t lrl_sim_refresh_rigid_body_state(lrl_sim* sim, void* stream);
+/* VelocityTrackingEasyEnv.step's numpy extras (velocity_tracking_easy_env.py:48-62) as a device snapshot of the
+ * current state, enqueued on `stream`: out = device f32 [LRL_EXTRAS_ROWS][num_envs], rows at the LRL_EXTRAS_* offsets
+ * (contact states as 1 / 0 for contact force z > 1 on each foot, foot positions as the rigid-body state's feet). */
+#define LRL_EXTRAS_JOINT_POS 0
+#define LRL_EXTRAS_JOINT_VEL 12
+#define LRL_EXTRAS_JOINT_POS_TARGET 24
+#define LRL_EXTRAS_BODY_LIN_VEL 36
+#define LRL_EXTRAS_BODY_ANG_VEL 39
+#define LRL_EXTRAS_COMMANDS 42
+#define LRL_EXTRAS_CONTACT_STATES 46
+#define LRL_EXTRAS_FOOT_POSITIONS 50
+#define LRL_EXTRAS_BODY_POS 62
+#define LRL_EXTRAS_TORQUES 65
+#define LRL_EXTRAS_ROWS 77
+int32_t lrl_sim_extras_snapshot(lrl_sim* sim, float* out, void* stream);
 /* Terrain mesh for params->terrain_mesh == 1 (gym.add_triangle_mesh / add_heightfield, legged_robot.py:
  * 1122-1160): `vertices` host [rows*cols][3] in the terrain frame (the Terrain class's trimesh vertices, or
  * the unmoved grid for a heightfield), placed at (-border_size, -border_size, 0) like tm_params.transform;
@@ -422,7 +437,8 @@ typedef struct lrl_ppo_ctrl {
 /* Rollout step of PPO.act (ppo.py:62-74): latent = enc(priv); mu = actor([obs, latent]);
  * a = mu + std * eps; value = critic([obs, latent]); logp = sum log N(a; mu, std) — the same fp32-MFMA
  * GEMM chain as the update's forward, then one head kernel.  eps [n, num_actions] is given (injected)
- * or drawn from the counter RNG (seed, counter, env row) when eps == NULL.  If `store` != NULL the
+ * or drawn from the counter RNG (seed, counter, global env id = row_offset + row) when eps == NULL — with
+ * row_offset the rank's env_offset, a sharded rollout draws what one process holding every env would.  If `store` != NULL the
  * transition (obs, priv, hist, actions, values, logp, mu, sigma) is written to row `store_row` of the
  * [T, n, ...] storage arrays (RolloutStorage.add_transitions, rollout_storage.py:57-71). */
 typedef struct lrl_rollout_store {
@@ -433,7 +449,8 @@ typedef struct lrl_rollout_store {
 
 int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n);
 int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, const float* obs, const float* priv,
-                    const float* hist, int32_t n, const float* eps, uint64_t seed, uint64_t counter, float* actions,
+                    const float* hist, int32_t n, const float* eps, uint64_t seed, uint64_t counter, int64_t row_offset,
+                    float* actions,
                     float* mu, float* values, float* logp, const lrl_rollout_store* store, int32_t store_row,
                     void* workspace, void* stream);
 

@@ -155,60 +155,74 @@ __device__ inline void cr3(const float* a, const float* b, float* o) {
   o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// Base pose of env e: rotation R (row-major, from the xyzw quaternion), origin p, origin velocity vo (COM velocity
+// - w x (R c)) and angular velocity W
+__device__ inline void base_pose(const KState& S, int e, float* R, float* p, float* vo, float* W) {
+  const int N = S.stride;
+  float q[4], V[3];
+  for (int k = 0; k < 4; ++k) q[k] = S.root[(3 + k) * N + e];
+  for (int k = 0; k < 3; ++k) { p[k] = S.root[k * N + e]; V[k] = S.root[(7 + k) * N + e]; W[k] = S.root[(10 + k) * N + e]; }
+  float x = q[0], y = q[1], z = q[2], w = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
+  R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+  R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+  float c[3] = {S.com[e], S.com[N + e], S.com[2 * N + e]}, Rc[3], wc[3];
+  mv3(R, c, Rc);
+  cr3(W, Rc, wc);
+  for (int k = 0; k < 3; ++k) vo[k] = V[k] - wc[k];
+}
+
+// Forward kinematics of body (leg, link) of env e (leg < 0: the base; link 3: the foot frame at foot_xyz[leg]):
+// rotation Rb, origin ob, origin velocity vb, angular velocity wb
+__device__ inline void body_fk(const KParams* __restrict__ K, const KState& S, int e, int leg, int link,
+                               const float* __restrict__ foot_xyz, const float* R, const float* p, const float* vo,
+                               const float* W, float* Rb, float* ob, float* vb, float* wb) {
+  const int N = S.stride;
+  for (int k = 0; k < 9; ++k) Rb[k] = R[k];
+  for (int k = 0; k < 3; ++k) { ob[k] = p[k]; vb[k] = vo[k]; wb[k] = W[k]; }
+  if (leg < 0) return;
+  const KLeg& L = K->leg[leg];
+  int nj = link > 2 ? 3 : link + 1;
+  for (int j = 0; j < nj; ++j) {
+    float off[3], tmp[9], Rj[9], ax[3], axw[3];
+    mv3(Rb, L.xyz[j], off);
+    for (int k = 0; k < 3; ++k) ob[k] += off[k];
+    // velocity of the new origin: v += w x off
+    float wo[3];
+    cr3(wb, off, wo);
+    for (int k = 0; k < 3; ++k) vb[k] += wo[k];
+    mm3(Rb, L.rfix[j], tmp);
+    float th = S.dof_pos[(3 * leg + j) * N + e], sn, cs;
+    sincosf(th, &sn, &cs);
+    float t1 = 1.f - cs;
+    for (int k = 0; k < 3; ++k) ax[k] = L.axis[j][k];
+    float Ra[9] = {t1 * ax[0] * ax[0] + cs, t1 * ax[0] * ax[1] - sn * ax[2], t1 * ax[0] * ax[2] + sn * ax[1],
+                   t1 * ax[0] * ax[1] + sn * ax[2], t1 * ax[1] * ax[1] + cs, t1 * ax[1] * ax[2] - sn * ax[0],
+                   t1 * ax[0] * ax[2] - sn * ax[1], t1 * ax[1] * ax[2] + sn * ax[0], t1 * ax[2] * ax[2] + cs};
+    mm3(tmp, Ra, Rj);
+    for (int k = 0; k < 9; ++k) Rb[k] = Rj[k];
+    mv3(Rb, ax, axw);
+    float qd = S.dof_vel[(3 * leg + j) * N + e];
+    for (int k = 0; k < 3; ++k) wb[k] += qd * axw[k];
+  }
+  if (link == 3) {
+    float off[3], wo[3];
+    mv3(Rb, &foot_xyz[3 * leg], off);
+    cr3(wb, off, wo);
+    for (int k = 0; k < 3; ++k) { ob[k] += off[k]; vb[k] += wo[k]; }
+  }
+}
+
 __global__ void rigid_body_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ body_leg,
                                   const int32_t* __restrict__ body_link, const float* __restrict__ foot_xyz) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
   const int N = S.stride;
-  float q[4], p[3], V[3], W[3];
-  for (int k = 0; k < 4; ++k) q[k] = S.root[(3 + k) * N + e];
-  for (int k = 0; k < 3; ++k) { p[k] = S.root[k * N + e]; V[k] = S.root[(7 + k) * N + e]; W[k] = S.root[(10 + k) * N + e]; }
-  float x = q[0], y = q[1], z = q[2], w = q[3];
-  float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w), 2 * (x * y + z * w),
-                1 - 2 * (x * x + z * z), 2 * (y * z - x * w), 2 * (x * z - y * w), 2 * (y * z + x * w),
-                1 - 2 * (x * x + y * y)};
-  // base origin velocity = COM velocity - w x (R c)
-  float c[3] = {S.com[e], S.com[N + e], S.com[2 * N + e]}, Rc[3], wc[3], vo[3];
-  mv3(R, c, Rc);
-  cr3(W, Rc, wc);
-  for (int k = 0; k < 3; ++k) vo[k] = V[k] - wc[k];
+  float R[9], p[3], vo[3], W[3];
+  base_pose(S, e, R, p, vo, W);
   for (int b = 0; b < K->num_bodies; ++b) {
-    int leg = body_leg[b], link = body_link[b];
     float Rb[9], ob[3], vb[3], wb[3];
-    for (int k = 0; k < 9; ++k) Rb[k] = R[k];
-    for (int k = 0; k < 3; ++k) { ob[k] = p[k]; vb[k] = vo[k]; wb[k] = W[k]; }
-    if (leg >= 0) {
-      const KLeg& L = K->leg[leg];
-      int nj = link > 2 ? 3 : link + 1;
-      for (int j = 0; j < nj; ++j) {
-        float off[3], tmp[9], Rj[9], ax[3], axw[3];
-        mv3(Rb, L.xyz[j], off);
-        for (int k = 0; k < 3; ++k) ob[k] += off[k];
-        // velocity of the new origin: v += w x off
-        float wo[3];
-        cr3(wb, off, wo);
-        for (int k = 0; k < 3; ++k) vb[k] += wo[k];
-        mm3(Rb, L.rfix[j], tmp);
-        float th = S.dof_pos[(3 * leg + j) * N + e], sn, cs;
-        sincosf(th, &sn, &cs);
-        float t1 = 1.f - cs;
-        for (int k = 0; k < 3; ++k) ax[k] = L.axis[j][k];
-        float Ra[9] = {t1 * ax[0] * ax[0] + cs, t1 * ax[0] * ax[1] - sn * ax[2], t1 * ax[0] * ax[2] + sn * ax[1],
-                       t1 * ax[0] * ax[1] + sn * ax[2], t1 * ax[1] * ax[1] + cs, t1 * ax[1] * ax[2] - sn * ax[0],
-                       t1 * ax[0] * ax[2] - sn * ax[1], t1 * ax[1] * ax[2] + sn * ax[0], t1 * ax[2] * ax[2] + cs};
-        mm3(tmp, Ra, Rj);
-        for (int k = 0; k < 9; ++k) Rb[k] = Rj[k];
-        mv3(Rb, ax, axw);
-        float qd = S.dof_vel[(3 * leg + j) * N + e];
-        for (int k = 0; k < 3; ++k) wb[k] += qd * axw[k];
-      }
-      if (link == 3) {
-        float off[3], wo[3];
-        mv3(Rb, &foot_xyz[3 * leg], off);
-        cr3(wb, off, wo);
-        for (int k = 0; k < 3; ++k) { ob[k] += off[k]; vb[k] += wo[k]; }
-      }
-    }
+    body_fk(K, S, e, body_leg[b], body_link[b], foot_xyz, R, p, vo, W, Rb, ob, vb, wb);
     float qb[4];
     mat_to_quat(Rb, qb);
     float* out = S.rb_state + (size_t)b * 13 * N;
@@ -216,6 +230,38 @@ __global__ void rigid_body_kernel(const KParams* __restrict__ K, KState S, const
     for (int k = 0; k < 4; ++k) out[(3 + k) * N + e] = qb[k];
     for (int k = 0; k < 3; ++k) { out[(7 + k) * N + e] = vb[k]; out[(10 + k) * N + e] = wb[k]; }
   }
+}
+
+// VelocityTrackingEasyEnv.step's per-step numpy extras (velocity_tracking_easy_env.py:48-62) as one device snapshot,
+// rows of n floats (lrl.h LRL_EXTRAS_*): dof_pos, dof_vel, joint_pos_target (12 each), base_lin_vel, base_ang_vel (3),
+// commands (4), contact states of the feet (contact force z > 1: 1 / 0), foot positions (4 x 3, the rigid-body state's
+// feet), root position (3), torques (12).  Coalesced: thread e reads row r of every SoA field at word e.
+__global__ void extras_snapshot_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ body_leg,
+                                       const int32_t* __restrict__ body_link, const float* __restrict__ foot_xyz,
+                                       float* __restrict__ out) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  const int N = S.stride, n = S.n;
+  const lrl_env_params& P = K->p;
+  int r = 0;
+  auto put = [&](float v) { out[(int64_t)(r++) * n + e] = v; };
+  for (int k = 0; k < 12; ++k) put(S.dof_pos[k * N + e]);
+  for (int k = 0; k < 12; ++k) put(S.dof_vel[k * N + e]);
+  for (int k = 0; k < 12; ++k) put(S.joint_pos_target[k * N + e]);
+  for (int k = 0; k < 3; ++k) put(S.base_lin_vel[k * N + e]);
+  for (int k = 0; k < 3; ++k) put(S.base_ang_vel[k * N + e]);
+  for (int k = 0; k < 4; ++k) put(S.commands[k * N + e]);
+  for (int f = 0; f < LRL_NUM_LEGS; ++f)
+    put(f < P.num_feet && S.contact[(P.feet[f] * 3 + 2) * N + e] > 1.f ? 1.f : 0.f);
+  float R[9], p[3], vo[3], W[3];
+  base_pose(S, e, R, p, vo, W);
+  for (int f = 0; f < LRL_NUM_LEGS; ++f) {
+    float Rb[9], ob[3] = {0.f, 0.f, 0.f}, vb[3], wb[3];
+    if (f < P.num_feet) body_fk(K, S, e, body_leg[P.feet[f]], body_link[P.feet[f]], foot_xyz, R, p, vo, W, Rb, ob, vb, wb);
+    for (int k = 0; k < 3; ++k) put(ob[k]);
+  }
+  for (int k = 0; k < 3; ++k) put(p[k]);
+  for (int k = 0; k < 12; ++k) put(S.torques[k * N + e]);
 }
 
 // HistoryWrapper.get_observations shift: hist = cat(hist[:, NO:], obs)  (history_wrapper.py:26-30)
@@ -381,6 +427,12 @@ hipError_t lrl_launch_rigid_body(const KParams* K, const KState* S, const int32_
                                  const float* foot_xyz, hipStream_t st) {
   hipLaunchKernelGGL(lrl::rigid_body_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, K, *S, body_leg, body_link,
                      foot_xyz);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_extras_snapshot(const KParams* K, const KState* S, const int32_t* body_leg, const int32_t* body_link,
+                                      const float* foot_xyz, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(lrl::extras_snapshot_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, K, *S, body_leg,
+                     body_link, foot_xyz, out);
   return hipGetLastError();
 }
 hipError_t lrl_launch_shift_history(const KState* S, int NO, int H, int append, hipStream_t st) {

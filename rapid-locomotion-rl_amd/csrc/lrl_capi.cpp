@@ -43,6 +43,8 @@ hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t,
 hipError_t lrl_launch_set_dof(const KState*, const float*, const float*, const int32_t*, int32_t, hipStream_t);
 hipError_t lrl_launch_rigid_body(const KParams*, const KState*, const int32_t*, const int32_t*, const float*,
                                  hipStream_t);
+hipError_t lrl_launch_extras_snapshot(const KParams*, const KState*, const int32_t*, const int32_t*, const float*, float*,
+                                      hipStream_t);
 hipError_t lrl_launch_shift_history(const KState*, int, int, int, hipStream_t);
 hipError_t lrl_launch_randomize(const KState*, const float*, const float*, const float*, const float*, uint32_t,
                                 hipStream_t);
@@ -639,6 +641,13 @@ int32_t lrl_sim_set_dof_state_indexed(lrl_sim* s, const float* pos, const float*
                                       void* stream) {
   if (!s || !pos || !vel || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
   HIPCHECK(lrl_launch_set_dof(&s->S, pos, vel, ids, n, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_extras_snapshot(lrl_sim* s, float* out, void* stream) {
+  if (!s || !out) return fail(LRL_E_INVALID, "lrl_sim_extras_snapshot: null argument");
+  HIPCHECK(lrl_launch_extras_snapshot(s->dk, &s->S, s->d_body_leg, s->d_body_link, s->d_foot_xyz, out,
+                                      (hipStream_t)stream));
   return 0;
 }
 

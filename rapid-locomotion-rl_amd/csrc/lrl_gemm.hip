@@ -968,11 +968,16 @@ struct X6Op {
 #pragma unroll
       for (int e = 0; e < KR; ++e) {
         const int k = k0 + kb + e;
-        const int kr = KGATHER ? (int)krows[k] : k;
-        if (fast) {
-          v[e] = P[kr * ldi + roff];
+        // gathered rows index the whole rollout buffer (T * N rows): 64-bit offsets; identity rows are bounded by
+        // try_x6's K * ld < 2^31 check, so 32-bit math is exact there
+        if constexpr (KGATHER) {
+          const int64_t o = krows[k] * ld + roff;
+          if (fast) v[e] = P[o];
+          else v[e] = (rok && k < k_lim) ? P[o] : 0.f;
+        } else if (fast) {
+          v[e] = P[k * ldi + roff];
         } else {
-          v[e] = (rok && k < k_lim) ? P[kr * ldi + roff] : 0.f;
+          v[e] = (rok && k < k_lim) ? P[k * ldi + roff] : 0.f;
         }
       }
     }
@@ -1286,6 +1291,12 @@ static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t s
   // (LRL_X6_MIN: development override of the smallest output side x6 takes — 16 by default)
   static const int min_side = getenv("LRL_X6_MIN") ? atoi(getenv("LRL_X6_MIN")) : 16;
   if (p.N < min_side || (layout == GEMM_TN && p.M < min_side)) return 0;
+  // r-contiguous operands (A of TN, B of NN / TN) and the epilogue use 32-bit element offsets from the group base
+  // (k * ld + row, row * ldc + col): keep every identity-indexed offset below 2^31 (gathered rows are 64-bit)
+  const int64_t lim = int64_t(1) << 31;
+  if ((layout & 1) && (int64_t)p.K * p.lda >= lim) return 0;
+  if ((layout & 2) && p.b_rows == nullptr && (int64_t)p.K * p.ldb >= lim) return 0;
+  if ((int64_t)p.M * p.ldc >= lim || (epi == EPI_DELU && (int64_t)p.M * p.ld_aux >= lim)) return 0;
   int rc;
   if (layout == GEMM_TN) {
     // (both operands r-contiguous: dword loads, any alignment)

@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "../../include/lrl.h"
@@ -339,6 +340,7 @@ struct ActHeadArgs {
   const float *obs, *priv, *hist, *eps;
   int n, na, no, np;
   uint64_t seed, counter;
+  int64_t row_offset;  // global id of row 0 (the rank's env_offset): the noise key, so draws do not depend on sharding
   float *actions, *mu, *values, *logp;
   lrl_rollout_store store;
   int store_row, do_store;
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
     if (a.eps) {
       e = a.eps[(int64_t)g * na + j];
     } else {  // Box-Muller on the counter RNG (stream POLICY): pairs of actions share one Philox draw
-      lrl_u32x4 u = lrl_philox((uint32_t)g, (uint32_t)a.counter, (LRL_RNG_POLICY << 16) ^ (uint32_t)(a.counter >> 32),
+      lrl_u32x4 u = lrl_philox((uint32_t)(a.row_offset + g), (uint32_t)a.counter, (LRL_RNG_POLICY << 16) ^ (uint32_t)(a.counter >> 32),
                                (uint32_t)(j >> 1), a.seed);
       const float u1 = fmaxf(lrl_u01(u.v[0]), 1e-7f), u2 = lrl_u01(u.v[1]);
       const float rad = sqrtf(-2.f * logf(u1)), th = 6.283185307179586f * u2;
@@ -870,23 +872,41 @@ struct Fork {
   hipStream_t st = nullptr;
   hipEvent_t go = nullptr, done = nullptr;
 };
-static Fork* fork_for_device() {
+// The fork lives on the device of the caller's stream (hipStreamGetDevice; the null stream means the current device),
+// and each device's fork is created once under a mutex, so concurrent first calls do not race.  Host threads sharing a
+// device share its fork: the stream is in order, so a later `done` record still covers an earlier caller's chain (at
+// worst a caller waits for more work than its own).
+static Fork* fork_for_device(hipStream_t caller) {
   static const bool on = [] {
     const char* e = getenv("LRL_PPO_FORK");
     return !(e && e[0] == '0');
   }();
   if (!on) return nullptr;
   static Fork forks[64];
+  static std::mutex mu;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (caller) {
+    hipDevice_t d = 0;
+    if (hipStreamGetDevice(caller, &d) != hipSuccess) return nullptr;
+    dev = (int)d;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return nullptr;
+  }
+  if (dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
   Fork& f = forks[dev];
   if (!f.st) {
-    if (hipStreamCreateWithFlags(&f.st, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&f.go, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess) {
-      f = Fork{};
-      return nullptr;
-    }
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    const bool sw = cur != dev;  // stream and events are created on the caller's device
+    if (sw && hipSetDevice(dev) != hipSuccess) return nullptr;
+    Fork nf;
+    const bool ok = hipStreamCreateWithFlags(&nf.st, hipStreamNonBlocking) == hipSuccess &&
+                    hipEventCreateWithFlags(&nf.go, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&nf.done, hipEventDisableTiming) == hipSuccess;
+    if (sw) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
+    f = nf;
   }
   return &f;
 }
@@ -942,7 +962,7 @@ extern "C" int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n
 
 extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, const float* obs, const float* priv,
                                const float* hist, int32_t n, const float* eps, uint64_t seed, uint64_t counter,
-                               float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
+                               int64_t row_offset, float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
                                int32_t store_row, void* workspace, void* stream) {
   if (int rc = check_net(net)) return rc;
   if (!params || !obs || !priv || !actions || !workspace || n <= 0)
@@ -971,6 +991,7 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   ah.h3 = P.h3; ah.w4a = w + nt.w4a; ah.b4a = w + nt.b4a; ah.w4c = w + nt.w4c; ah.b4c = w + nt.b4c;
   ah.stdv = w + nt.std_off; ah.obs = obs; ah.priv = priv; ah.hist = hist; ah.eps = eps;
   ah.n = n; ah.na = nt.num_actions; ah.no = nt.num_obs; ah.np = nt.num_priv; ah.seed = seed; ah.counter = counter;
+  ah.row_offset = row_offset;
   ah.actions = actions; ah.mu = mu; ah.values = values; ah.logp = logp;
   if (store) ah.store = *store;
   ah.store_row = store_row; ah.do_store = store ? 1 : 0;
@@ -1116,7 +1137,7 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
   // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
   g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
-  Fork* fk = fork_for_device();
+  Fork* fk = fork_for_device(st);
   G ge{fk ? fk->st : st, g.part_end};
   if (fk) {
     if (hipEventRecord(fk->go, st) != hipSuccess || hipStreamWaitEvent(fk->st, fk->go, 0) != hipSuccess)

@@ -174,7 +174,7 @@ def lib():
                      "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms", "lrl_sim_inject_push_uniforms", "lrl_sim_timing",
                      "lrl_sim_self_contact_stats", "lrl_ppo_store_step", "lrl_curriculum_sample",
                      "lrl_curriculum_update_weights", "lrl_rows_mean_zero", "lrl_sim_step_code",
-                     "lrl_sim_apply_commands"]:
+                     "lrl_sim_apply_commands", "lrl_sim_extras_snapshot"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_np_sum_f64.restype = C.c_double
         L.lrl_np_sum_f64.argtypes = [C.c_void_p, C.c_int64]

@@ -33,8 +33,11 @@ MINI_GYM_ROOT_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class _LazyExtras(dict):
-    """``extras`` dict whose per-step numpy copies (velocity_tracking_easy_env.py:48-62) are only
-    materialised when a caller reads them — the reference pays 11 device->host syncs per step."""
+    """``extras`` dict whose per-step numpy entries (velocity_tracking_easy_env.py:48-62) are step-time snapshots: step
+    enqueues one device copy of the fields they read (lrl_sim_extras_snapshot, into a buffer of that step's own), and an
+    entry becomes a numpy array only when read (the reference pays 11 device->host syncs per step).  As in the
+    reference, ``extras`` is one dict updated by every step, so reading a key after the next step gives the next
+    step's values; an array read, or a ``copy()`` / ``dict(...)`` / ``items()`` taken, holds the step it came from."""
 
     def __init__(self, env):
         super().__init__()
@@ -45,19 +48,61 @@ class _LazyExtras(dict):
         self._lazy[key] = fn
         dict.pop(self, key, None)
 
-    def __getitem__(self, key):
-        if key in self._lazy and not dict.__contains__(self, key):
-            return self._lazy[key]()
+    def _get(self, key):
+        fn = self._lazy.pop(key, None)
+        if fn is not None:  # materialise once: later reads return the same array
+            dict.__setitem__(self, key, fn())
         return dict.__getitem__(self, key)
+
+    def __getitem__(self, key):
+        return self._get(key)
+
+    def __setitem__(self, key, value):
+        self._lazy.pop(key, None)
+        dict.__setitem__(self, key, value)
+
+    def __delitem__(self, key):
+        if self._lazy.pop(key, None) is None:
+            dict.__delitem__(self, key)
 
     def __contains__(self, key):
         return dict.__contains__(self, key) or key in self._lazy
 
+    def __iter__(self):
+        return iter(self.keys())
+
+    def __len__(self):
+        return dict.__len__(self) + len(self._lazy)
+
     def get(self, key, default=None):
-        return self[key] if key in self else default
+        return self._get(key) if key in self else default
+
+    def pop(self, key, *default):
+        if key in self:
+            v = self._get(key)
+            dict.pop(self, key)
+            return v
+        if default:
+            return default[0]
+        raise KeyError(key)
 
     def keys(self):
         return list(dict.keys(self)) + [k for k in self._lazy if not dict.__contains__(self, k)]
+
+    def items(self):
+        return [(k, self._get(k)) for k in self.keys()]
+
+    def values(self):
+        return [self._get(k) for k in self.keys()]
+
+    def copy(self):
+        return dict(self.items())
+
+    def update(self, other=(), **kw):
+        for k, v in (other.items() if hasattr(other, "items") else other):
+            self[k] = v
+        for k, v in kw.items():
+            self[k] = v
 
 
 class _Upload:
@@ -99,7 +144,7 @@ class _Upload:
 class LeggedRobotEnv:
     def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
                  eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=0,
-                 solver_iterations=None, legacy_fork=True):
+                 solver_iterations=None, legacy_fork=True, num_envs_global=None):
         if cfg is None:
             from .config import Cfg as cfg
         if num_envs is not None:
@@ -137,6 +182,20 @@ class LeggedRobotEnv:
         self.num_privileged_obs = cfg.env.num_privileged_obs
         self.num_actions = cfg.env.num_actions
         self.seed = int(seed)
+        # data-parallel sharding: this sim holds global envs [env_offset, env_offset + num_envs) of
+        # num_envs_global.  Every per-env draw is keyed by the global id and the env origins are the global grid's, so
+        # a rank's envs evolve exactly as the same envs of one process holding all of them.  Default: equal shards over
+        # the initialised process group (the bench's layout), else env_offset + num_envs.
+        self.env_offset = int(env_offset)
+        if num_envs_global is None:
+            import torch.distributed as tdist
+            world = tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
+            num_envs_global = max(self.num_envs * world, self.env_offset + self.num_envs) if self.env_offset or \
+                world > 1 else self.num_envs
+        if num_envs_global < self.env_offset + self.num_envs:
+            raise ValueError(f"num_envs_global {num_envs_global} < env_offset + num_envs "
+                             f"{self.env_offset + self.num_envs}")
+        self.num_envs_global = int(num_envs_global)
 
         # ---- asset + terrain + derived params (legged_robot.py:1162-1319, 1417-1429) ----
         asset_file = cfg.asset.file.format(MINI_GYM_ROOT_DIR=MINI_GYM_ROOT_DIR)
@@ -367,20 +426,26 @@ class LeggedRobotEnv:
                     raise IndexError(f"initial terrain levels [{min_l}, {max_l}] outside the {t.num_rows} terrain rows "
                                      "(Cfg.terrain.max_init_terrain_level)")
                 k = len(ids)
-                self.terrain_levels[ids] = torch.randint(min_l, max_l + 1, (k,), generator=g).to(self.device)
-                self.terrain_types[ids] = torch.div(torch.arange(k), (k / t.num_cols),
-                                                    rounding_mode="floor").long().to(self.device)
+                # the train group of a shard draws over the global train envs and keeps its slice (the eval group is
+                # per process)
+                lo, kg = (self.env_offset, self.num_envs_global - (self.num_envs - self.num_train_envs)) \
+                    if c is self.cfg else (0, k)
+                lv = torch.randint(min_l, max_l + 1, (kg,), generator=g)[lo:lo + k]
+                ty = torch.div(torch.arange(kg), (kg / t.num_cols), rounding_mode="floor").long()[lo:lo + k]
+                self.terrain_levels[ids] = lv.to(self.device)
+                self.terrain_types[ids] = ty.to(self.device)
                 t.max_terrain_level = t.num_rows
                 t.terrain_origins = torch.from_numpy(t.env_origins).to(self.device).float()
                 self.env_origins[ids] = t.terrain_origins[self.terrain_levels[ids], self.terrain_types[ids]]
             self._level_gen = torch.Generator(device=self.device).manual_seed(self.seed + 1)
-        else:
-            num_cols = np.floor(np.sqrt(n))
-            num_rows = np.ceil(n / num_cols)
+        else:  # the global grid of all ranks' envs, this shard's slice
+            ng, lo = self.num_envs_global, self.env_offset
+            num_cols = np.floor(np.sqrt(ng))
+            num_rows = np.ceil(ng / num_cols)
             xx, yy = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
             sp = cfg.env.env_spacing
-            self.env_origins[:, 0] = (sp * xx.flatten()[:n]).to(self.device)
-            self.env_origins[:, 1] = (sp * yy.flatten()[:n]).to(self.device)
+            self.env_origins[:, 0] = (sp * xx.flatten()[lo:lo + n]).to(self.device)
+            self.env_origins[:, 1] = (sp * yy.flatten()[lo:lo + n]).to(self.device)
             self.env_origins[:, 2] = 0.0
 
     # -------------------------------------------------------------------------------- commands
@@ -549,21 +614,34 @@ class LeggedRobotEnv:
                 tm.mark("reset_idx_observe")
         ex = self.extras
         ex["privileged_obs"] = self.privileged_obs_buf
-        ex.set_lazy("joint_pos", lambda: self.dof_pos.cpu().numpy())
-        ex.set_lazy("joint_vel", lambda: self.dof_vel.cpu().numpy())
-        ex.set_lazy("joint_pos_target", lambda: self.joint_pos_target.cpu().numpy())
         ex["joint_vel_target"] = torch.zeros(12)
-        ex.set_lazy("body_linear_vel", lambda: self.base_lin_vel.cpu().numpy())
-        ex.set_lazy("body_angular_vel", lambda: self.base_ang_vel.cpu().numpy())
-        ex.set_lazy("body_linear_vel_cmd", lambda: self.commands.cpu().numpy()[:, 0:2])
-        ex.set_lazy("body_angular_vel_cmd", lambda: self.commands.cpu().numpy()[:, 2:])
-        ex.set_lazy("contact_states", lambda: (self.contact_forces[:, self.feet_indices, 2] > 1.0).cpu().numpy().copy())
-        ex.set_lazy("foot_positions", lambda: self._foot_positions().cpu().numpy().copy())
-        ex.set_lazy("body_pos", lambda: self.root_states[:, 0:3].cpu().numpy())
-        ex.set_lazy("torques", lambda: self.torques.cpu().numpy())
+        self._register_extras(ex)
         if tm is not None:
             tm.mark("extras")
         return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
+
+    # rows of lrl_sim_extras_snapshot (include/lrl.h LRL_EXTRAS_*): key -> (first row, rows)
+    _EXTRAS_ROWS = 77
+    _EXTRAS = {"joint_pos": (0, 12), "joint_vel": (12, 12), "joint_pos_target": (24, 12), "body_linear_vel": (36, 3),
+               "body_angular_vel": (39, 3), "body_linear_vel_cmd": (42, 2), "body_angular_vel_cmd": (44, 2),
+               "contact_states": (46, 4), "foot_positions": (50, 12), "body_pos": (62, 3), "torques": (65, 12)}
+
+    def _register_extras(self, ex):
+        """The step's numpy extras as lazy reads of one device snapshot taken now (see _LazyExtras)."""
+        n = self.num_envs
+        snap = torch.empty(self._EXTRAS_ROWS, n, device=self.device)
+        _abi.check(self._L.lrl_sim_extras_snapshot(self._sim, C.c_void_p(snap.data_ptr()), self._stream()))
+        nf = len(self.feet_indices)
+
+        def read(key):
+            r0, k = self._EXTRAS[key]
+            if key == "contact_states":
+                return (snap[r0:r0 + nf].t() > 0.5).cpu().numpy().copy()
+            if key == "foot_positions":
+                return snap[r0:r0 + 3 * nf].t().reshape(n, nf, 3).cpu().numpy().copy()
+            return snap[r0:r0 + k].t().cpu().numpy().copy()
+        for key in self._EXTRAS:
+            ex.set_lazy(key, lambda key=key: read(key))
 
     def kernel_timing(self, start):
         """Env-kernel launch time, the one definition bench.py and the scripts use: HIP events around each
@@ -734,8 +812,9 @@ class LeggedRobotEnv:
 
     def _rand_levels(self, like, high):
         """torch.randint_like(levels, high) of _update_terrain_curriculum (seeded device generator here;
-        tests replace it to inject the reference's draws)."""
-        return torch.randint(0, high, like.shape, generator=self._level_gen, device=self.device, dtype=like.dtype)
+        tests replace it to inject the reference's draws).  Always int64, the dtype of terrain_levels: ``like`` may be
+        the step's int32 reset ids, and the curriculum kernel reads the draws as int64."""
+        return torch.randint(0, high, like.shape, generator=self._level_gen, device=self.device, dtype=torch.int64)
 
     def _update_terrain_curriculum(self, env_ids, cfg, _ids32=None):
         """legged_robot.py:793-818: robots that walked past half a tile move a level up, those that covered less
@@ -745,6 +824,9 @@ class LeggedRobotEnv:
         t = cfg.terrain
         if getattr(self, "_sim", None) is not None:  # one launch instead of ~25 indexed torch ops per reset
             rnd = self._rand_levels(env_ids, t.max_terrain_level).contiguous()  # same draw as the torch form below
+            if rnd.dtype != torch.int64 or rnd.device != self.device or rnd.numel() < len(env_ids):
+                raise TypeError(f"terrain level draws must be int64 on {self.device} with one per env id, got "
+                                f"{rnd.dtype} on {rnd.device} [{rnd.numel()}] for {len(env_ids)} ids")
             ids32 = _ids32 if _ids32 is not None else env_ids.to(torch.int32).contiguous()
             to = t.terrain_origins
             _abi.check(self._L.lrl_sim_terrain_curriculum(

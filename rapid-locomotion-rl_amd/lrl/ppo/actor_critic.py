@@ -203,9 +203,11 @@ class ActorCritic(nn.Module):
                                                   ptr(ws[1]), stream))
         return mean, latent
 
-    def act_fused(self, obs, priv, hist=None, eps=None, seed=0, counter=0, store=None, store_row=0):
+    def act_fused(self, obs, priv, hist=None, eps=None, seed=0, counter=0, store=None, store_row=0, row_offset=0):
         """PPO.act teacher path on the flat parameters (lrl_ppo_act: fp32-MFMA GEMM chain + one head
-        kernel that samples, scores and writes the storage row).  Returns (actions, mu, values [N,1], logp [N])."""
+        kernel that samples, scores and writes the storage row).  Returns (actions, mu, values [N,1], logp [N]).
+        The policy noise is keyed by (seed, counter, row_offset + row): row_offset is the global id of row 0 (the
+        rank's env_offset), so a sharded rollout samples what one process holding every env would."""
         n = obs.shape[0]
         dev = obs.device
         assert obs.is_contiguous() and priv.is_contiguous() and obs.dtype == torch.float32
@@ -224,6 +226,7 @@ class ActorCritic(nn.Module):
         st = C.byref(store) if store is not None else None
         stream = _abi.stream_of(dev)
         _abi.check(_abi.lib().lrl_ppo_act(C.byref(net), ptr(self._flat), ptr(obs), ptr(priv), ptr(hist), C.c_int32(n),
-                                          ptr(eps), C.c_uint64(seed), C.c_uint64(counter), ptr(actions), ptr(mu),
+                                          ptr(eps), C.c_uint64(seed), C.c_uint64(counter), C.c_int64(row_offset),
+                                          ptr(actions), ptr(mu),
                                           ptr(values), ptr(logp), st, C.c_int32(store_row), ptr(ws[1]), stream))
         return actions, mu, values, logp

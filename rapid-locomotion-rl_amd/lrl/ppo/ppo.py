@@ -68,8 +68,10 @@ class PPO:
         self.async_losses = False
         self._lr_dev = None  # the native update's ctrl tensor while its learning rate is newer than self._lr
         self.fused = (torch.device(device).type == "cuda") if fused is None else fused
-        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
-        self.seed = seed + 1000003 * rank  # per-rank policy-noise stream (counter RNG keyed by local row)
+        # policy noise: counter RNG keyed by (seed, act counter, global env id); row_offset = the global id of storage row
+        # 0 (the rank's env_offset, set by the Runner), so the draws do not depend on how envs are sharded over ranks
+        self.seed = seed
+        self.row_offset = 0
         self._act_counter = 0
         self._store = None
         self.grad_allreduce = _world() > 1
@@ -97,7 +99,8 @@ class PPO:
             self._act_counter += 1
             a, mu, v, lp = self.actor_critic.act_fused(
                 obs.contiguous(), privileged_obs.contiguous(), obs_history.contiguous(), eps=eps, seed=self.seed,
-                counter=self._act_counter, store=self._store, store_row=self.storage.step)
+                counter=self._act_counter, store=self._store, store_row=self.storage.step,
+                row_offset=self.row_offset)
             t = self.transition
             t.actions, t.values, t.actions_log_prob, t.action_mean = a, v, lp, mu
             t.action_sigma = self.actor_critic.std.detach().expand_as(mu)
@@ -155,7 +158,7 @@ class PPO:
         if self.fused:
             _, _, last_values, _ = self.actor_critic.act_fused(last_critic_obs.contiguous(),
                                                                last_critic_privileged_obs.contiguous(),
-                                                               seed=self.seed, counter=0)
+                                                               seed=self.seed, counter=0, row_offset=self.row_offset)
         else:
             last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
         reduce = None

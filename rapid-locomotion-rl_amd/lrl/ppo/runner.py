@@ -84,6 +84,7 @@ class Runner:
         ac = ActorCritic(self.env.num_obs, self.env.num_privileged_obs, self.env.num_obs_history,
                          self.env.num_actions).to(self.device)
         self.alg = PPO(ac, device=self.device, seed=seed)
+        self.alg.row_offset = int(getattr(env, "env_offset", 0))  # policy noise keyed by global env id (sharded ranks)
         self.alg.async_losses = not _SYNC_UPDATE  # losses logged as device scalars: no host sync per iteration
         self.num_steps_per_env = RunnerArgs.num_steps_per_env
         self.alg.init_storage(self.env.num_train_envs, self.num_steps_per_env, [self.env.num_obs],

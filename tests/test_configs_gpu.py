@@ -8,11 +8,11 @@
   4096 envs from the same states against the oracle, observations included.
 * configs[2]: 4096 Go1 envs on the default 10 x 20 curriculum trimesh (legged_robot_config.py:52-57, border 50 m):
   one step of mesh physics against the oracle, and the height scan of the GPU's final poses bit-exact.
-* configs[3] / [4]: two ranks (gloo, sharing this GPU) at the per-rank shape — 4096 Mini Cheetah envs per rank,
-  and 4096 Go1 envs per rank with the adaptation update — run one full PPO iteration (env + act + GAE + update):
-  the replicas end bit-identical (parameters, both Adam moments, learning-rate trace), and the all-reduced first
-  gradient equals the mean of the single-rank gradients, each recomputed by a world-1 process on that rank's
-  rollout.
+* configs[3] / [4]: gloo ranks sharing this GPU at the per-rank shape — 2 and 8 ranks of 4096 Mini Cheetah envs
+  (8 x 4096 = configs[3]'s 32,768), 2 ranks of 4096 Go1 envs with the adaptation update — run one full PPO iteration
+  (env + act + GAE + update): the replicas end bit-identical (parameters, both Adam moments, learning-rate trace), and
+  the all-reduced first gradient equals the mean of the single-rank gradients, each recomputed by a world-1 process
+  on that rank's rollout.  And the rollout does not depend on the GPU count: 2 x 2048 envs = 1 x 4096, bit for bit.
 * configs[0]: scripts/test.py's run_env(16, 1000) stays finite and most robots stay up (the preset's COM / payload
   randomisation can tip a robot that only holds its default pose).
 """
@@ -284,29 +284,35 @@ def _port():
     return p
 
 
-def _iteration(robot, rank, world, tmp):
-    """One Runner.learn iteration of ``robot`` at 4096 envs for global rank ``rank`` (env_offset rank x 4096), the
+def _iteration(robot, rank, world, tmp, n=N_BENCH, rollout_only=False):
+    """One Runner.learn iteration of ``robot`` at ``n`` envs for global rank ``rank`` (env_offset rank x n), the
     bench's setup.  The rollout the update sees (storage + the CUDA generator state its randperm draws from) and
-    the initial parameters are written to ``tmp`` for the single-rank recomputation."""
+    the initial parameters are written to ``tmp`` for the single-rank recomputation.  ``rollout_only``: the update is
+    skipped, and the rollout storage plus the env's final state come back instead."""
     from lrl import config as lcfg
     from lrl.env import LeggedRobotEnv
     from lrl.history import HistoryWrapper
     from lrl.ppo import runner as R
     cfg = lcfg.make_cfg()
     (lcfg.config_mini_cheetah if robot == "mc" else lcfg.config_go1)(cfg)
-    cfg.env.num_envs = N_BENCH
+    cfg.env.num_envs = n
     R.RunnerArgs.save_interval = 0
-    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=1234, env_offset=rank * N_BENCH))
+    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=1234, env_offset=rank * n))
     torch.manual_seed(0)  # same initial weights on every rank (as DDP broadcasts them)
     runner = R.Runner(env, device="cuda:0", seed=1234)
     alg = runner.alg
     alg.record_lr = True
     init = alg.actor_critic._flat.detach().clone()
     orig_update = alg.update
+    roll = {}
 
     def update():
         s = alg.storage
         snap = {k: getattr(s, k).detach().cpu().clone() for k in STORE_KEYS}
+        if rollout_only:
+            roll.update({k: v.numpy().copy() for k, v in snap.items()})
+            s.clear()
+            return 0.0, 0.0, 0.0
         snap["cuda_rng"] = torch.cuda.get_rng_state()
         snap["init"] = init.cpu()
         snap["lr"] = alg.learning_rate
@@ -329,6 +335,13 @@ def _iteration(robot, rank, world, tmp):
     finally:
         dist.all_reduce = orig
     torch.cuda.synchronize()
+    if rollout_only:
+        e = env.env
+        roll.update(root=_np(e.root_states).copy(), dof_pos=_np(e.dof_pos).copy(), dof_vel=_np(e.dof_vel).copy(),
+                    contact=_np(e.contact_forces).copy(), hist=_np(e.obs_history_buf).copy(),
+                    origins=_np(e.env_origins).copy())
+        env.env.close()
+        return roll
     nat = alg._native
     out = dict(params=alg.actor_critic._flat.detach().cpu().numpy().copy(),
                m=nat["exp_avg"].cpu().numpy().copy(), v=nat["exp_avg_sq"].cpu().numpy().copy(),
@@ -342,14 +355,16 @@ STORE_KEYS = ["observations", "privileged_observations", "observation_histories"
               "actions_log_prob", "advantages", "mu", "sigma", "rewards", "dones"]
 
 
-def _rank_worker(rank, world, port, robot, tmp, out):
+def _rank_worker(rank, world, port, robot, tmp, out, n=N_BENCH, rollout_only=False):
     sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    out[rank] = _iteration(robot, rank, world, tmp)
-    dist.destroy_process_group()
+    out[rank] = _iteration(robot, rank, world, tmp, n, rollout_only)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def _single_rank_first_grad(path):
@@ -388,29 +403,57 @@ def _single_rank_first_grad(path):
     return cap[0]
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("robot", ["mc", "go1"])
-def test_two_rank_full_iteration_at_bench_shape(robot):
-    """configs[3] (Mini Cheetah, 4096 envs per rank) and configs[4] (Go1, 4096 envs per rank, teacher PPO +
-    adaptation update) at world 2: one full PPO iteration per rank."""
-    world = 2
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("robot,world", [("mc", 2), ("go1", 2), ("mc", 8)])
+def test_multi_rank_full_iteration_at_bench_shape(robot, world):
+    """configs[3] (Mini Cheetah, 4096 envs per rank: world 8 is its 32,768-env shape) and configs[4] (Go1, 4096 envs
+    per rank, teacher PPO + adaptation update) as gloo ranks sharing this GPU: one full PPO iteration per rank.  The
+    replicas end bit-identical (parameters, both Adam moments, learning-rate trace) and the all-reduced first gradient
+    is the mean of the ranks' gradients, each recomputed by a world-1 update on that rank's saved rollout."""
     mgr = mp.Manager()
     out = mgr.dict()
     with tempfile.TemporaryDirectory() as tmp:
         mp.spawn(_rank_worker, args=(world, _port(), robot, tmp, out), nprocs=world, join=True)
-        a, b = out[0], out[1]
+        res = [out[r] for r in range(world)]
+        a = res[0]
         assert np.isfinite(a["params"]).all()
-        assert a["rew"] != b["rew"]  # the ranks stepped different envs (env_offset) with different policy noise
-        np.testing.assert_array_equal(a["params"], b["params"])
-        np.testing.assert_array_equal(a["m"], b["m"])
-        np.testing.assert_array_equal(a["v"], b["v"])
-        assert a["lr"] == b["lr"] and len(a["lr"]) == 20
-        np.testing.assert_array_equal(a["post"], b["post"])
+        assert len({r["rew"] for r in res}) == world  # the ranks stepped different envs (env_offset)
+        for b in res[1:]:
+            np.testing.assert_array_equal(a["params"], b["params"])
+            np.testing.assert_array_equal(a["m"], b["m"])
+            np.testing.assert_array_equal(a["v"], b["v"])
+            assert a["lr"] == b["lr"] and len(a["lr"]) == 20
+            np.testing.assert_array_equal(a["post"], b["post"])
         single = [_single_rank_first_grad(os.path.join(tmp, f"rollout_{robot}_{r}.pt")) for r in range(world)]
     for r in range(world):
-        np.testing.assert_allclose(out[r]["pre"], single[r], rtol=1e-6, atol=1e-9)
-    np.testing.assert_allclose(a["post"] / world, (single[0] + single[1]) / world, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(res[r]["pre"], single[r], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(a["post"] / world, sum(single) / world, rtol=1e-6, atol=1e-8)
     assert np.abs(single[0] - single[1]).max() > 1e-4
+
+
+@pytest.mark.timeout(600)
+def test_rollout_does_not_depend_on_the_gpu_count():
+    """every draw is keyed by the global env id (env: env_offset; policy noise: PPO.row_offset) and the
+    env origins are the global layout's, so 2 ranks x 2048 Mini Cheetah envs roll out exactly what 1 x 4096 does: a
+    24-step Runner rollout's storage (observations, histories, actions, values, log-probs, means, rewards, dones,
+    returns) and the final env state are bit-identical per global env; the advantages, normalised with all-reduced
+    statistics (another summation order), agree to fp32 rounding."""
+    mgr = mp.Manager()
+    one, two = mgr.dict(), mgr.dict()
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_rank_worker, args=(1, 0, "mc", tmp, one, N_BENCH, True), nprocs=1, join=True)
+        mp.spawn(_rank_worker, args=(2, _port(), "mc", tmp, two, N_BENCH // 2, True), nprocs=2, join=True)
+    ref = one[0]
+    h = N_BENCH // 2
+    for k in STORE_KEYS + ["root", "dof_pos", "dof_vel", "contact", "hist", "origins"]:
+        whole = ref[k]
+        ax = 1 if k in STORE_KEYS else 0  # storage is [T, N, ...]
+        parts = np.concatenate([two[0][k], two[1][k]], axis=ax)
+        if k == "advantages":
+            np.testing.assert_allclose(parts, whole, rtol=0, atol=2e-6 * max(1.0, np.abs(whole).max()), err_msg=k)
+            continue
+        np.testing.assert_array_equal(parts, whole, err_msg=k)
+    assert np.abs(ref["actions"][:, :h] - ref["actions"][:, h:]).max() > 0.1  # the halves are different envs
 
 
 # ------------------------------------------------------------------------------------------ configs[0]

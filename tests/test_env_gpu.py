@@ -468,3 +468,46 @@ def test_train_eval_split():
     assert runner.alg.storage.num_envs == n_tr
     assert "eval/episode" in henv.env.extras
     henv.env.close()
+
+
+def test_extras_are_step_time_snapshots():
+    """VelocityTrackingEasyEnv.step's numpy extras (velocity_tracking_easy_env.py:48-62): what a caller took from
+    ``info`` — an array read, or the dict copied — holds the step it came from after later steps; ``info`` itself is
+    one dict updated by every step (as the reference's ``self.extras.update``), so a read after the next step gives
+    that step's values.  Values against the live tensors at the step they snapshot."""
+    from lrl.env import LeggedRobotEnv
+    cfg = lcfg.make_cfg()
+    lcfg.config_mini_cheetah(cfg)
+    n = 64
+    env = LeggedRobotEnv("cuda:0", cfg=cfg, num_envs=n)
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+
+    def live():
+        torch.cuda.synchronize()
+        f = env.feet_indices
+        return {"joint_pos": _np(env.dof_pos), "joint_vel": _np(env.dof_vel), "joint_pos_target": _np(env.joint_pos_target),
+                "body_linear_vel": _np(env.base_lin_vel), "body_angular_vel": _np(env.base_ang_vel),
+                "body_linear_vel_cmd": _np(env.commands)[:, 0:2], "body_angular_vel_cmd": _np(env.commands)[:, 2:],
+                "contact_states": _np(env.contact_forces[:, f, 2] > 1.0), "foot_positions": _np(env._foot_positions()),
+                "body_pos": _np(env.root_states[:, 0:3]), "torques": _np(env.torques)}
+    env.commands[:, :3] = torch.rand(n, 3, generator=g, device="cuda:0")
+    _, _, _, info = env.step(torch.randn(n, 12, generator=g, device="cuda:0") * 0.5)
+    want0 = live()
+    held = dict(info)          # the dict copied at step t
+    jp = info["joint_pos"]     # an array read at step t
+    items = info.copy()
+    env.commands[:, :3] = torch.rand(n, 3, generator=g, device="cuda:0")
+    env.step(torch.randn(n, 12, generator=g, device="cuda:0") * 0.5)
+    env.step(torch.randn(n, 12, generator=g, device="cuda:0") * 0.5)
+    want2 = live()
+    assert np.abs(want2["joint_pos"] - want0["joint_pos"]).max() > 1e-3  # the state moved
+    for k, v in want0.items():
+        tol = 1e-6 if k == "foot_positions" else 0.0  # (the same FK in another kernel: contraction may differ)
+        assert held[k].shape == v.shape and items[k].shape == v.shape, k
+        np.testing.assert_allclose(held[k], v, rtol=0, atol=tol, err_msg=k)
+        np.testing.assert_allclose(items[k], v, rtol=0, atol=tol, err_msg=k)
+        np.testing.assert_allclose(info[k], want2[k], rtol=0, atol=tol, err_msg=k)  # the live dict: latest step
+    np.testing.assert_array_equal(jp, want0["joint_pos"])
+    assert set(info.keys()) >= set(want0) | {"privileged_obs", "joint_vel_target"} and len(info) == len(info.keys())
+    env.close()

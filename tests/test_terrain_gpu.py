@@ -275,6 +275,35 @@ def test_native_terrain_curriculum_matches_torch_form_on_random_inputs():
     env.close()
 
 
+def test_terrain_curriculum_wraps_through_step_resets():
+    """Resets driven by step() (upstream path: time-outs, int32 reset ids from lrl_sim_step_code) on the curriculum
+    mesh with every env on the top level and walked past half a tile: each level wraps to the generator's own draw
+    (the real _rand_levels, int64 whatever the ids' dtype), so new levels fall in [0, max) and the origins follow."""
+    from lrl.env import LeggedRobotEnv
+    n, rows, cols = 256, 5, 4
+    cfg = _rough_cfg(n, 3.0, **{"terrain.num_rows": rows, "terrain.num_cols": cols})
+    env = LeggedRobotEnv("cuda:0", cfg=cfg, seed=4, legacy_fork=False)
+    env.reset()
+    zero = torch.zeros(n, 12, device="cuda:0")
+    env.step(zero)
+    t = cfg.terrain
+    env.terrain_levels[:] = t.max_terrain_level - 1
+    env.root_states[:, 0] = env.env_origins[:, 0] + t.env_length  # walked more than env_length / 2: move up
+    env.episode_length_buf[:] = cfg.env.max_episode_length  # every env times out in the next step
+    env._due_next = None
+    env.step(zero)
+    torch.cuda.synchronize()
+    lv = env.terrain_levels
+    assert lv.dtype == torch.int64
+    assert bool(((lv >= 0) & (lv < t.max_terrain_level)).all()), _np(lv)[:32]
+    assert len(torch.unique(lv)) > 1  # random levels, not one fused value
+    org = t.terrain_origins[lv, env.terrain_types]
+    assert torch.equal(env.env_origins, org)
+    m = float(env.extras["train/episode"]["terrain_level"])
+    assert 0.0 <= m < t.max_terrain_level, m
+    env.close()
+
+
 def test_perceptive_policy_trains_on_rough_terrain():
     """The base config's perceptive layout (observe_vel + 17 x 11 height scan = 235 observations, history
     15 x 235) end to end: upstream resets on the curriculum trimesh, one Runner.learn iteration through the
