@@ -30,6 +30,7 @@ from .terrain import Terrain, convert_heightfield_to_trimesh
 # Cfg.asset.file is formatted with the package root, as mini_gym does; only its file name selects the robot's
 # committed model table (lrl/robots/<name>.json) — no URDF is read at run time
 MINI_GYM_ROOT_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_SNAPSHOT_EXTRAS = os.environ.get("LRL_EXTRAS_SNAPSHOT", "1") != "0"
 
 
 class _LazyExtras(dict):
@@ -627,8 +628,20 @@ class LeggedRobotEnv:
                "contact_states": (46, 4), "foot_positions": (50, 12), "body_pos": (62, 3), "torques": (65, 12)}
 
     def _register_extras(self, ex):
-        """The step's numpy extras as lazy reads of one device snapshot taken now (see _LazyExtras)."""
+        """The step's numpy extras as lazy reads of one device snapshot taken now (see _LazyExtras).
+        (LRL_EXTRAS_SNAPSHOT=0, a development switch for A/B timing: lazy reads of the live tensors instead.)"""
         n = self.num_envs
+        if not _SNAPSHOT_EXTRAS:
+            live = {"joint_pos": lambda: self.dof_pos, "joint_vel": lambda: self.dof_vel,
+                    "joint_pos_target": lambda: self.joint_pos_target, "body_linear_vel": lambda: self.base_lin_vel,
+                    "body_angular_vel": lambda: self.base_ang_vel, "body_linear_vel_cmd": lambda: self.commands[:, 0:2],
+                    "body_angular_vel_cmd": lambda: self.commands[:, 2:],
+                    "contact_states": lambda: self.contact_forces[:, self.feet_indices, 2] > 1.0,
+                    "foot_positions": self._foot_positions, "body_pos": lambda: self.root_states[:, 0:3],
+                    "torques": lambda: self.torques}
+            for key, fn in live.items():
+                ex.set_lazy(key, lambda fn=fn: fn().cpu().numpy().copy())
+            return
         snap = torch.empty(self._EXTRAS_ROWS, n, device=self.device)
         _abi.check(self._L.lrl_sim_extras_snapshot(self._sim, C.c_void_p(snap.data_ptr()), self._stream()))
         nf = len(self.feet_indices)

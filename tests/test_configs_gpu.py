@@ -29,7 +29,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from helpers import (MAX_EXCLUDED, SEP_EPS_1, VEL_EPS, make, make_rough, oracle_sensitivity, perturb_state,
-                     within_tolerance)
+                     record_errors, within_tolerance)
 from lrl import _abi
 from oracle import oracle
 
@@ -201,6 +201,7 @@ def test_bench_grid_physics_step_matches_oracle(robot):
     got = {k: _np(getattr(env, a)) for k, a in dict(root="root_states", dof_pos="dof_pos", dof_vel="dof_vel",
                                                       contact="contact_forces", obs="obs_buf").items()}
     excl = (m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS) | oracle_sensitivity(st, sp)
+    record_errors(f"configs {robot} n={n} physics step", got, st, excl, sp)
     ok = within_tolerance(got, st) | excl
     print(f"{robot} n={n}: {excl.sum()} envs excluded, {(~ok).sum()} outside tolerance")
     for e in np.flatnonzero(~ok)[:4]:
@@ -261,6 +262,7 @@ def test_configs2_full_curriculum_trimesh_step_matches_oracle():
                                                       contact="contact_forces", h="measured_heights").items()}
     assert (np.abs(st["contact"]).sum((1, 2)) > 0).mean() > 0.4  # the poses do touch the terrain
     excl = (m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS) | oracle_sensitivity(st, sp)
+    record_errors(f"configs[2] n={n} trimesh step", got, st, excl, sp)
     ok = within_tolerance(got, st) | excl
     print(f"configs[2] n={n}: {excl.sum()} envs excluded, {(~ok).sum()} outside tolerance")
     for e in np.flatnonzero(~ok)[:4]:

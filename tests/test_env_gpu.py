@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (MAX_EXCLUDED, POST_PHYSICS, SEP_EPS_1, VEL_EPS, golden, make, oracle_sensitivity,
+from helpers import (MAX_EXCLUDED, POST_PHYSICS, SEP_EPS_1, VEL_EPS, golden, make, oracle_sensitivity, record_errors,
                      perturb_state, physics_mismatch)
 from lrl import _abi
 from lrl import config as lcfg
@@ -233,6 +233,8 @@ def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True,
         assert np.isfinite(got["root"]).all() and np.isfinite(got["dof_vel"]).all()
         sens = oracle_sensitivity(st, st_p)
         bad, excl = physics_mismatch(got, st, m, sens, sep_eps=SEP_EPS_1)
+        record_errors(f"{robot} n={n} step {s + 1}/{steps} limits={limits} self={selfc} extra={sorted(over)}", got, st,
+                      excl, st_p)
         worst = max(worst, excl.mean())
         print(f"{robot} n={n} step {s + 1}/{steps} limits={limits} self={selfc}: {excl.sum()} of {n} envs excluded "
               f"(discontinuity margin {((m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS)).sum()}, oracle-sensitive "

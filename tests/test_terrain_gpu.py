@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from helpers import (MAX_EXCLUDED, SEP_EPS_1, VEL_EPS, golden, make_rough, oracle_sensitivity, perturb_state,
-                     physics_mismatch)
+                     physics_mismatch, record_errors)
 from lrl import _abi
 from lrl import config as lcfg
 from oracle import oracle
@@ -157,6 +157,7 @@ def test_rough_terrain_physics_matches_oracle(steps):
         # normal rule (step edges / corners) within SEP_EPS_1 — which are counted and capped
         touched = max(touched, (np.abs(st["contact"]).sum((1, 2)) > 0).mean())
         bad, excl = physics_mismatch(got, st, margins, sens, sep_eps=SEP_EPS_1)
+        record_errors(f"terrain n={n} step {s + 1}/{steps}", got, st, excl, st_p)
         print(f"terrain n={n} step {s + 1}/{steps}: {excl.sum()} envs excluded (discontinuity margin "
               f"{((margins[:, 0] < SEP_EPS_1) | (margins[:, 1] < VEL_EPS)).sum()}, oracle-sensitive {sens.sum()}), "
               f"{bad.sum()} outside tolerance")
