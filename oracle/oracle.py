@@ -229,3 +229,9 @@ def reset_idx_device(params, state, ids, u, root_mode, xy_lo=0.0, xy_span=0.0, x
     state["episode_length"][ids] = 0
     state["reset"][ids] = 1
     return state
+
+
+def set_solver_tgs(on):
+    """lrl_oracle.c:lrlo_set_solver_tgs — the PGS-vs-TGS study's solver switch (scripts/tgs_vs_pgs.py); 0 (the model
+    the kernel runs) everywhere else."""
+    lib().lrlo_set_solver_tgs(C.c_int(1 if on else 0))

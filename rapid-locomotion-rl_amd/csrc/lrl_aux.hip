@@ -431,7 +431,7 @@ hipError_t lrl_launch_rigid_body(const KParams* K, const KState* S, const int32_
 }
 hipError_t lrl_launch_extras_snapshot(const KParams* K, const KState* S, const int32_t* body_leg, const int32_t* body_link,
                                       const float* foot_xyz, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(lrl::extras_snapshot_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, K, *S, body_leg,
+  hipLaunchKernelGGL(lrl::extras_snapshot_kernel, dim3((S->n + 63) / 64), dim3(64), 0, st, K, *S, body_leg,
                      body_link, foot_xyz, out);
   return hipGetLastError();
 }

@@ -486,6 +486,249 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Fused rollout act (PPO.act, ppo.py:62-74 -> actor_critic.py:137-147,170-173, + RolloutStorage.add_transitions,
+// rollout_storage.py:57-71): one workgroup carries FA_R = 16 env rows through the whole chain — encoder, actor / critic
+// bodies, heads, sampling, log-prob and the storage row — with every activation in LDS, so a rollout step's act is one
+// launch (the unfused chain is eight, each on its ~6-10 us load -> MFMA -> store floor at 4,096 rows).  The products
+// run on the fp32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation): a wave owns a run of 16-column
+// output tiles; per 16-k chunk lane (i, q) = (lane & 15, lane >> 4) reads A[i][k0 + 4q .. +3] from LDS (one b128) and,
+// per tile, the 4 weights W[n][k0 + 4q .. +3] of its output column n straight from L2 (the next chunk's loads are in
+// flight while this chunk's MFMAs run); step s of the chunk multiplies k = k0 + 4q + s.  16 rows per workgroup puts
+// 4,096 envs on 256 workgroups, one per CU (115 KB of LDS).
+constexpr int FA_R = 16, FA_THREADS = 256;
+constexpr int FA_D = 6;       // weight chunks (16 k each) in flight per wave: the L2 round trip over the MFMA work
+constexpr int FA_XP = 260;    // X / he1 / h3 pitch (widths <= 256) + 4: conflict-free b128 row reads
+constexpr int FA_BIGP = 1028; // h1 pitch (2 x ac_h0 <= 1024)
+constexpr int FA_MIDP = 516;  // h2 pitch (2 x ac_h1 <= 512); priv / he2 use narrower pitches in the same region
+constexpr int FA_LDS_FLOATS = FA_R * (FA_XP + FA_BIGP + FA_MIDP);
+
+typedef float fa_f32x4 __attribute__((ext_vector_type(4)));
+
+struct FaLayer {
+  const float* A;   // LDS input rows
+  int pa, ga, K;    // pitch, column offset of group g's input (g * ga), k extent (multiple of 16, zero-padded)
+  const float* W;   // weights of group 0: [Nw rows][ldw], group g at W + g * gw
+  int ldw, Kw, Nw;  // row pitch, valid k (< Kw), valid rows (< Nw)
+  int64_t gw;
+  const float* b;   // bias of group 0 (group g at b + g * Nw)
+  float* C;         // LDS output: group g's column n at C[row * pc + coff + g * Ng + n]
+  int pc, coff, Ng, groups;
+  int elu, vec;     // ELU after the bias; vec: 16-B aligned weight rows with Kw % 4 == 0 (float4 loads)
+};
+
+template <int NB>
+__device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
+  const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
+  const int tpg = L.Ng >> 4, g = t0 / tpg;  // a run never crosses a group (fa_layer)
+  const float* A = L.A + i * L.pa + g * L.ga + 4 * q;
+  const float* W = L.W + g * L.gw;
+  int nr[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) nr[j] = (t0 + j - g * tpg) * 16 + i;
+  fa_f32x4 acc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) acc[j] = fa_f32x4{0.f, 0.f, 0.f, 0.f};
+  auto load_b = [&](float4 (&bv)[NB], int k0) {
+    const int k = k0 + 4 * q;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int n = nr[j];
+      const float* src = W + (int64_t)n * L.ldw + k;
+      if (L.vec && n < L.Nw && k < L.Kw) {
+        bv[j] = *reinterpret_cast<const float4*>(src);
+      } else {
+        const bool rn = n < L.Nw;
+        bv[j].x = rn && k < L.Kw ? src[0] : 0.f;
+        bv[j].y = rn && k + 1 < L.Kw ? src[1] : 0.f;
+        bv[j].z = rn && k + 2 < L.Kw ? src[2] : 0.f;
+        bv[j].w = rn && k + 3 < L.Kw ? src[3] : 0.f;
+      }
+    }
+  };
+  // FA_D chunks of weights in flight (a ring of register sets, indexed at compile time by unrolling FA_D chunks)
+  const int nck = L.K >> 4;
+  float4 ring[FA_D][NB];
+#pragma unroll
+  for (int d = 0; d < FA_D; ++d)
+    if (d < nck) load_b(ring[d], 16 * d);
+  for (int c0 = 0; c0 < nck; c0 += FA_D) {
+#pragma unroll
+    for (int d = 0; d < FA_D; ++d) {
+      const int c = c0 + d;
+      if (c < nck) {
+        const float4 a = *reinterpret_cast<const float4*>(A + 16 * c);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, ring[d][j].x, acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, ring[d][j].y, acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, ring[d][j].z, acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, ring[d][j].w, acc[j], 0, 0, 0);
+        if (c + FA_D < nck) load_b(ring[d], 16 * (c + FA_D));
+      }
+    }
+  }
+  // C/D: column i of the tile, rows 4q .. 4q + 3 in the four registers
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int n = nr[j];
+    if (n < L.Nw) {
+      const float bias = L.b[g * L.Nw + n];
+      float* c = L.C + (4 * q) * L.pc + L.coff + g * L.Ng + n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[j][r] + bias;
+        if (L.elu) v = v > 0.f ? v : expm1f(v);
+        c[r * L.pc] = v;
+      }
+    }
+  }
+}
+
+// one layer: the T = groups * Ng / 16 column tiles split into equal runs over the 4 waves (T < 4: one tile per wave)
+__device__ __forceinline__ void fa_layer(const FaLayer& L) {
+  const int w = threadIdx.x >> 6, T = L.groups * (L.Ng >> 4);
+  const int tpw = T >= 4 ? T / 4 : 1;
+  if (w * tpw >= T) return;
+  const int t0 = w * tpw;
+  switch (tpw) {
+    case 1: fa_tiles<1>(L, t0); break;
+    case 2: fa_tiles<2>(L, t0); break;
+    case 4: fa_tiles<4>(L, t0); break;
+    case 8: fa_tiles<8>(L, t0); break;
+    case 16: fa_tiles<8>(L, t0); fa_tiles<8>(L, t0 + 8); break;
+    default:
+      for (int t = t0; t < t0 + tpw; ++t) fa_tiles<1>(L, t);
+  }
+}
+
+struct FusedActArgs {
+  const float* w;
+  lrl_ppo_net net;
+  const float *obs, *priv, *hist, *eps;
+  int n, xs;
+  uint32_t vec;  // bit l: float4 weight loads allowed for layer l (FA_L_*)
+  uint64_t seed, counter;
+  int64_t row_offset;
+  float *actions, *mu, *values, *logp;
+  lrl_rollout_store store;
+  int store_row, do_store;
+};
+
+__global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float fa_lds[];
+  float* X = fa_lds;                     // [16][FA_XP]: obs | latent | 0
+  float* BIG = X + FA_R * FA_XP;         // he1 [16][FA_XP], h1 [16][FA_BIGP], h3 [16][FA_XP]
+  float* MID = BIG + FA_R * FA_BIGP;     // priv [16][36], he2 [16][enc_h1 + 4], h2 [16][FA_MIDP]
+  const lrl_ppo_net& nt = a.net;
+  const int t = threadIdx.x, r0 = blockIdx.x * FA_R, nrows = min(FA_R, a.n - r0);
+  const int no = nt.num_obs, np = nt.num_priv, PP = 36, EP2 = nt.enc_h1 + 4;
+  // stage obs (zero padding and rows past n) and priv (k padded to 32)
+  for (int e = t; e < FA_R * a.xs; e += FA_THREADS) {
+    const int r = e / a.xs, c = e - r * a.xs;
+    X[r * FA_XP + c] = (r < nrows && c < no) ? a.obs[(int64_t)(r0 + r) * no + c] : 0.f;
+  }
+  for (int e = t; e < FA_R * 32; e += FA_THREADS) {
+    const int r = e >> 5, c = e & 31;
+    MID[r * PP + c] = (r < nrows && c < np) ? a.priv[(int64_t)(r0 + r) * np + c] : 0.f;
+  }
+  __syncthreads();
+  const float* w = a.w;
+  FaLayer L;
+  // env_factor_encoder: priv -> enc_h0 (ELU) -> enc_h1 (ELU) -> latent, the latent into X[:, no:]
+  L = FaLayer{MID, PP, 0, 32, w + nt.e1w, np, np, nt.enc_h0, 0, w + nt.e1b, BIG, FA_XP, 0, nt.enc_h0, 1, 1, 0};
+  fa_layer(L);
+  __syncthreads();
+  L = FaLayer{BIG, FA_XP, 0, nt.enc_h0, w + nt.e2w, nt.enc_h0, nt.enc_h0, nt.enc_h1, 0, w + nt.e2b, MID, EP2, 0,
+              nt.enc_h1, 1, 1, (int)(a.vec >> 1) & 1};
+  fa_layer(L);
+  __syncthreads();
+  L = FaLayer{MID, EP2, 0, nt.enc_h1, w + nt.e3w, nt.enc_h1, nt.enc_h1, nt.latent, 0, w + nt.e3b, X, FA_XP, no,
+              (nt.latent + 15) / 16 * 16, 1, 0, (int)(a.vec >> 2) & 1};
+  fa_layer(L);
+  __syncthreads();
+  // actor / critic bodies, both at once: [obs | latent] -> 2 x ac_h0 -> 2 x ac_h1 -> 2 x ac_h2 (ELU)
+  const int nx = no + nt.latent;
+  L = FaLayer{X, FA_XP, 0, a.xs, w + nt.w1, nx, nx, 2 * nt.ac_h0, 0, w + nt.b1, BIG, FA_BIGP, 0, 2 * nt.ac_h0, 1, 1,
+              (int)(a.vec >> 3) & 1};
+  fa_layer(L);
+  __syncthreads();
+  L = FaLayer{BIG, FA_BIGP, nt.ac_h0, nt.ac_h0, w + nt.w2, nt.ac_h0, nt.ac_h0, nt.ac_h1, (int64_t)nt.ac_h1 * nt.ac_h0,
+              w + nt.b2, MID, FA_MIDP, 0, nt.ac_h1, 2, 1, (int)(a.vec >> 4) & 1};
+  fa_layer(L);
+  __syncthreads();
+  L = FaLayer{MID, FA_MIDP, nt.ac_h1, nt.ac_h1, w + nt.w3, nt.ac_h1, nt.ac_h1, nt.ac_h2, (int64_t)nt.ac_h2 * nt.ac_h1,
+              w + nt.b3, BIG, FA_XP, 0, nt.ac_h2, 2, 1, (int)(a.vec >> 5) & 1};
+  fa_layer(L);
+  __syncthreads();
+  // heads: thread (r, j) j < na: mu; (r, na): value — sequential fmaf over k, as act_head_kernel's mu
+  constexpr int NA = HEAD_NA;
+  float* MU = X;  // the obs tile is dead: [16][NA + 1] mu, then log-prob terms; value in column NA
+  if (t < FA_R * (NA + 1)) {
+    const int r = t / (NA + 1), j = t - r * (NA + 1);
+    const float* h = BIG + r * FA_XP + (j < NA ? 0 : HEAD_W);
+    const float* wr = j < NA ? w + nt.w4a + j * HEAD_W : w + nt.w4c;
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < HEAD_W; ++k) s = fmaf(h[k], wr[k], s);
+    s += j < NA ? w[nt.b4a + j] : w[nt.b4c];
+    MU[r * 16 + j] = s;
+  }
+  __syncthreads();
+  const int64_t so = (int64_t)a.store_row * a.n;
+  if (t < FA_R * NA) {
+    const int r = t / NA, j = t - r * NA, g = r0 + r;
+    if (r < nrows) {
+      float e;
+      if (a.eps) {
+        e = a.eps[(int64_t)g * NA + j];
+      } else {  // Box-Muller on the counter RNG (stream POLICY), keyed by the global env id (as act_head_kernel)
+        lrl_u32x4 u = lrl_philox((uint32_t)(a.row_offset + g), (uint32_t)a.counter,
+                                 (LRL_RNG_POLICY << 16) ^ (uint32_t)(a.counter >> 32), (uint32_t)(j >> 1), a.seed);
+        const float u1 = fmaxf(lrl_u01(u.v[0]), 1e-7f), u2 = lrl_u01(u.v[1]);
+        const float rad = sqrtf(-2.f * logf(u1)), th = 6.283185307179586f * u2;
+        e = (j & 1) ? rad * sinf(th) : rad * cosf(th);
+      }
+      const float m = MU[r * 16 + j], sd = w[nt.std_off + j];
+      const float act = m + sd * e;
+      const float d = act - m;
+      MU[r * 16 + j] = -(d * d) / (2.f * (sd * sd)) - logf(sd) - LOG_SQRT_2PI;
+      a.actions[(int64_t)g * NA + j] = act;
+      if (a.mu) a.mu[(int64_t)g * NA + j] = m;
+      if (a.do_store) {
+        const int64_t o = (so + g) * NA + j;
+        a.store.actions[o] = act;
+        a.store.mu[o] = m;
+        a.store.sigma[o] = sd;
+      }
+    }
+  }
+  __syncthreads();
+  if (t < nrows) {
+    const int g = r0 + t;
+    float lp = 0.f;
+    for (int j = 0; j < NA; ++j) lp += MU[t * 16 + j];
+    const float v = MU[t * 16 + NA];
+    if (a.values) a.values[g] = v;
+    if (a.logp) a.logp[g] = lp;
+    if (a.do_store) {
+      a.store.values[so + g] = v;
+      a.store.logp[so + g] = lp;
+    }
+  }
+  if (a.do_store) {  // obs / priv / history rows of this tile into storage row `store_row`
+    const int64_t b = so + r0;
+    copy_rows(a.obs + (int64_t)r0 * no, no, a.store.obs + b * no, no, nrows, no, t);
+    copy_rows(a.priv + (int64_t)r0 * np, np, a.store.priv + b * np, np, nrows, np, t);
+    if (a.hist && a.store.hist) {
+      const int hd = a.store.hist_dim, ld = a.store.hist_ld > hd ? a.store.hist_ld : hd;
+      copy_rows(a.hist + (int64_t)r0 * hd, hd, a.store.hist + b * ld, ld, nrows, hd, t);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Adaptation head: pred = HD2 W_D3^T + b, MSE against the encoder target (F.mse_loss, mean over B*L),
 // dHD2 = dpred W_D3 * elu'(HD2); partials dW_D3 [L][H], db_D3 [L], sum of squared errors.
 struct AdaptHeadArgs {
@@ -955,6 +1198,24 @@ static ActPlan make_act_plan(const lrl_ppo_net& n, int rows, char* base) {
   return p;
 }
 
+// The fused act's envelope (LDS pitches, tile runs that never cross a group); LRL_ACT_FUSED=1 selects it over the GEMM chain
+// (A/B timing and the tests that compare the two)
+static bool fused_act_fits(const lrl_ppo_net& n) {
+  const char* e = getenv("LRL_ACT_FUSED");  // (read per call: a test switches it inside one process)
+  if (!(e && e[0] == '1')) return false;  // off by default until it measures faster than the chain
+  auto run_ok = [](int groups, int Ng) {  // fa_layer: equal runs per wave inside one group
+    if (Ng % 16) return false;
+    const int T = groups * (Ng / 16), tpg = Ng / 16;
+    const int tpw = T >= 4 ? T / 4 : 1;
+    if (T >= 4 && T % 4) return false;
+    return tpg % std::min(tpw, 8) == 0;
+  };
+  return n.num_priv <= 32 && n.enc_h0 <= 256 && n.enc_h1 + 4 <= FA_MIDP && n.latent <= 32 && xs_of(n) <= 256 &&
+         2 * n.ac_h0 <= 1024 && 2 * n.ac_h1 <= 512 && 2 * n.ac_h2 <= 256 && n.enc_h0 % 16 == 0 && n.enc_h1 % 16 == 0 &&
+         n.ac_h0 % 16 == 0 && n.ac_h1 % 16 == 0 && run_ok(1, n.enc_h0) && run_ok(1, n.enc_h1) &&
+         run_ok(1, (n.latent + 15) / 16 * 16) && run_ok(1, 2 * n.ac_h0) && run_ok(2, n.ac_h1) && run_ok(2, n.ac_h2);
+}
+
 extern "C" int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n) {
   if (check_net(net) || n <= 0) return -1;
   return make_act_plan(*net, n, nullptr).bytes;
@@ -972,6 +1233,26 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
     return lrl_set_error(LRL_E_INVALID, "lrl_ppo_act: incomplete rollout store");
   const lrl_ppo_net& nt = *net;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (fused_act_fits(nt)) {  // one launch: act_fused_kernel
+    static const bool ok = [] { return hipFuncSetAttribute(reinterpret_cast<const void*>(act_fused_kernel),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           FA_LDS_FLOATS * sizeof(float)) == hipSuccess; }();
+    if (!ok) return lrl_set_error(LRL_E_HIP, "lrl_ppo_act: fused kernel LDS attribute");
+    FusedActArgs fa{};
+    fa.w = params; fa.net = nt; fa.obs = obs; fa.priv = priv; fa.hist = hist; fa.eps = eps;
+    fa.n = n; fa.xs = xs_of(nt);
+    auto al = [&](int64_t off, int ld) { return ((reinterpret_cast<uintptr_t>(params + off) & 15) == 0 && ld % 4 == 0); };
+    const int nx = nt.num_obs + nt.latent;
+    fa.vec = (al(nt.e2w, nt.enc_h0) ? 2u : 0u) | (al(nt.e3w, nt.enc_h1) ? 4u : 0u) | (al(nt.w1, nx) ? 8u : 0u) |
+             (al(nt.w2, nt.ac_h0) ? 16u : 0u) | (al(nt.w3, nt.ac_h1) ? 32u : 0u);
+    fa.seed = seed; fa.counter = counter; fa.row_offset = row_offset;
+    fa.actions = actions; fa.mu = mu; fa.values = values; fa.logp = logp;
+    if (store) fa.store = *store;
+    fa.store_row = store_row; fa.do_store = store ? 1 : 0;
+    hipLaunchKernelGGL(act_fused_kernel, dim3((n + FA_R - 1) / FA_R), dim3(FA_THREADS), FA_LDS_FLOATS * sizeof(float),
+                       st, fa);
+    return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act: launch failed");
+  }
   ActPlan P = make_act_plan(nt, n, static_cast<char*>(workspace));
   G g{st, nullptr};
   const float* w = params;

@@ -282,7 +282,12 @@ class PPO:
         # the adaptation chain's batch descriptor: the rows pointer of minibatch i must outlive the next C call
         batch_b = _abi.LrlPpoBatch()
         C.memmove(C.byref(batch_b), C.byref(batch), C.sizeof(batch))
-        read_done = [None] * _SNAPSHOTS  # per snapshot buffer: phase 3 of the minibatch that last read it has run
+        # per snapshot buffer: phase 3 of the minibatch that last read it has run.  The events live as long as the native
+        # state (re-recorded each update): an event destroyed while a wait on it is still queued on the GPU is a hazard
+        # this code does not take (round-4 audit of the round-3 core dump)
+        if sb is not cur and "read_done_ev" not in st:
+            st["read_done_ev"] = [torch.cuda.Event() for _ in range(_SNAPSHOTS)]
+        read_done = [None] * _SNAPSHOTS
         k = 0
         for epoch in range(PPO_Args.num_learning_epochs):
             for i in range(nmb):
@@ -319,8 +324,9 @@ class PPO:
                                                          C.c_double(PPO_Args.adaptation_module_learning_rate),
                                                          C.c_float(scale), C.byref(hp), ptr(ctrl), stream_b))
                 if sb is not cur:
-                    read_done[k % _SNAPSHOTS] = torch.cuda.Event()
-                    read_done[k % _SNAPSHOTS].record(sb)
+                    ev = st["read_done_ev"][k % _SNAPSHOTS]
+                    ev.record(sb)
+                    read_done[k % _SNAPSHOTS] = ev
                 k += 1
         if sb is not cur:
             cur.wait_stream(sb)

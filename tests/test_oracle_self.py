@@ -6,12 +6,16 @@ mini_cheetah_config.py:44, go1_config.py:44, passed to create_actor at legged_ro
 * with self-collision on, legs driven into each other and into the base stop there (the Baumgarte-recovered overlap
   stays small); with it off, the same drive interpenetrates.
 The GPU parity of the kernel against these rows is tests/test_env_gpu.py::test_self_collision_matches_oracle."""
+import os
+
 import numpy as np
 import pytest
 
 from helpers import make
 from lrl import _abi
 from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _dyn(M, s):
@@ -74,3 +78,26 @@ def test_oracle_self_collision_separates_and_holds(robot):
         worst[on] = sep[pen].min()
     assert worst[0] < -0.005, worst  # still interpenetrated without the rows
     assert worst[1] > -1e-3, worst  # pushed apart (Baumgarte) with them, within 0.1 s
+
+
+def test_oracle_tgs_variant_matches_pgs_on_standing():
+    """The PGS-vs-TGS study's solver switch (lrl_oracle.c lrlo_set_solver_tgs, scripts/tgs_vs_pgs.py): from the same
+    standing state both solvers hold the robot (base height within 3 mm of each other after 0.5 s, foot forces carrying
+    the weight), and the switch off restores the kernel's model exactly."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("tgs_vs_pgs", os.path.join(ROOT, "scripts", "tgs_vs_pgs.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    cfg, P, M = mod.setup()
+    res = []
+    for tgs in (0, 1, 0):
+        oracle.set_solver_tgs(tgs)
+        st = mod.state(P, M)
+        h, fz, vx, up = mod.run(P, M, st, 25)
+        res.append((h, fz, st["dof_pos"].copy()))
+    oracle.set_solver_tgs(0)
+    (h0, f0, q0), (h1, f1, q1), (h2, f2, q2) = res
+    assert np.abs(h0 - h1).max() < 3e-3 and abs(f1[-5:].mean() - 1.0) < 0.1 and abs(f0[-5:].mean() - 1.0) < 0.1
+    assert np.abs(h0 - h1).max() > 0  # the variant is a different solver
+    np.testing.assert_array_equal(h0, h2)
+    np.testing.assert_array_equal(q0, q2)

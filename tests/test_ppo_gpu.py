@@ -69,6 +69,43 @@ def test_fused_policy_act_matches_torch(n, no):
     torch.testing.assert_close(lp, lp_ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("n,no", [(4096, 42), (37, 42), (300, 235)])
+def test_one_launch_act_matches_gemm_chain(n, no, monkeypatch):
+    """The one-launch act (act_fused_kernel: fp32 MFMA, activations in LDS) against the GEMM-chain act
+    (LRL_ACT_FUSED=0: x6 products + act_head_kernel) on the same inputs, noise drawn by the counter RNG: actions, means,
+    values, log-probs to fp32 rounding; the storage row (obs / priv / history copies, sigma) exactly."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.rollout_storage import RolloutStorage
+    ac = ActorCritic(no, 18, 15 * no, 12).cuda()
+    init_params(ac)
+    with torch.no_grad():
+        ac.std.copy_(torch.linspace(0.5, 1.5, 12))
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    obs = torch.randn(n, no, device="cuda:0", generator=g)
+    priv = torch.randn(n, 18, device="cuda:0", generator=g)
+    hist = torch.randn(n, 15 * no, device="cuda:0", generator=g)
+    outs = []
+    for fused in ("1", "0"):  # (LRL_ACT_FUSED=1 selects the one-launch act)
+        monkeypatch.setenv("LRL_ACT_FUSED", fused)
+        st = RolloutStorage(n, 3, [no], [18], [15 * no], [12], "cuda:0")
+        res = ac.act_fused(obs, priv, hist, seed=11, counter=3, store=st.store_desc(), store_row=1, row_offset=64)
+        torch.cuda.synchronize()
+        outs.append([r.clone() for r in res] + [st.observations[1].clone(), st.privileged_observations[1].clone(),
+                                                st.observation_histories[1].clone(), st.actions[1].clone(),
+                                                st.sigma[1].clone(), st.mu[1].clone(), st.values[1].clone(),
+                                                st.actions_log_prob[1].clone()])
+    (a, mu, v, lp, so, sp, sh, sa, ss, sm, sv, sl), (a0, mu0, v0, lp0, so0, sp0, sh0, sa0, ss0, sm0, sv0, sl0) = outs
+    torch.testing.assert_close(mu, mu0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(a, a0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(v, v0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(lp, lp0, rtol=2e-5, atol=2e-4)
+    assert torch.equal(a - mu, a0 - mu0) or torch.allclose(a - mu, a0 - mu0, rtol=0, atol=1e-6)  # the same noise
+    for x, y in ((so, so0), (sp, sp0), (sh, sh0), (ss, ss0)):
+        assert torch.equal(x, y)
+    assert torch.equal(sa, a) and torch.equal(sm, mu) and torch.equal(sv.flatten(), v.flatten())
+    assert torch.equal(sl.flatten(), lp.flatten())
+
+
 def test_fused_policy_sampling_statistics():
     """Counter-RNG Box-Muller sampling: actions - mu ~ N(0, std^2)."""
     from lrl.ppo.actor_critic import ActorCritic
