@@ -355,6 +355,55 @@ int32_t lrl_sim_refresh_rigid_body_state(lrl_sim* sim, void* stream);
 #define LRL_EXTRAS_TORQUES 65
 #define LRL_EXTRAS_ROWS 77
 int32_t lrl_sim_extras_snapshot(lrl_sim* sim, float* out, void* stream);
+
+/* ---- the upstream step without a host round trip (lrl/env.py, legacy_fork=False, one process): id lists and their
+ * counts stay on the device; `nmax` bounds a device count `dcount` (launch size).
+ * lrl_sim_env_lists: mode 0 = the envs whose reset flag is set (reset_idx's ids after check_termination / time-outs),
+ * mode 1 = the envs due for command resampling before this step's kernel ((episode_length + 1) % interval == 0, every
+ * env when interval == 1: _post_physics_step_callback, legged_robot.py:578-581), ascending as np.flatnonzero. */
+int32_t lrl_sim_env_lists(lrl_sim* sim, int32_t mode, int32_t interval, int32_t* ids_out, int32_t* count_out,
+                          void* stream);
+/* _update_terrain_curriculum (legged_robot.py:793-818) of the listed envs; the wrap-around level is a uniform draw of
+ * the counter RNG (global env id, step counter).  lrl_sim_terrain_curriculum with rand_levels == NULL draws the same. */
+int32_t lrl_sim_terrain_curriculum_dev(lrl_sim* sim, const int32_t* ids, int32_t nmax, const int32_t* dcount,
+                                       int64_t* levels, const int64_t* types, const float* terrain_origins,
+                                       int32_t rows, int32_t cols, float half_env_length, float episode_length_s,
+                                       int32_t max_level, void* stream);
+/* reset_idx's device part (as lrl_sim_reset_idx_ex, counter-RNG draws) and the observation refresh (as
+ * lrl_sim_observe_idx) of the listed envs */
+int32_t lrl_sim_reset_idx_dev(lrl_sim* sim, const int32_t* ids, int32_t nmax, const int32_t* dcount, int32_t root_mode,
+                              float xy_lo, float xy_span, float x_off, float y_off, void* stream);
+int32_t lrl_sim_observe_idx_dev(lrl_sim* sim, const int32_t* ids, int32_t nmax, const int32_t* dcount, uint32_t flags,
+                                void* stream);
+/* reset_idx's episode logging (torch.mean of each row over the ids, then zeroed) with a device count; an empty batch
+ * leaves `means` as they were (the reference's extras keep the last reset batch's dict) */
+int32_t lrl_rows_mean_zero_dev(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t nmax,
+                               const int32_t* dcount, float* means, int32_t zero, void* stream);
+/* The grid-adaptive command curriculum on the device (RewardThresholdCurriculum, curriculum.py:16-124): its state in
+ * caller-owned device buffers, bit-exact with the host forms (numpy RandomState MT19937, pairwise sums). */
+typedef struct lrl_dev_curriculum {
+  double* weights;                 /* [nbins] sampling weights */
+  double* cdf;                     /* [nbins] normalised cdf cache */
+  int32_t* state;                  /* [4]: cdf valid, MT position, error (1 NaN, 2 negative, 3 bad sum), spare */
+  uint32_t* mt_key;                /* [624] MT19937 key (numpy RandomState.get_state()[1]) */
+  double *ep_rew_lin, *ep_rew_ang; /* [nbins] episode_reward_lin / _ang */
+  int64_t* env_bins;               /* [num_envs] env_command_bins */
+  float* env_bins_f;               /* [num_envs] the float env bins reset_idx exposes as extras['env_bins'] */
+  double* command_area;            /* [1] np.sum(weights) / nbins at the last resample with log_area */
+  const double* axes;              /* [nx + ny + nz] the grid axes (np.linspace of each key range) */
+  double half[3];                  /* bin_sizes / 2 */
+  int32_t nx, ny, nz;
+  uint32_t* words;                 /* scratch [8 * num_envs] */
+  double* draws;                   /* scratch [4 * num_envs] */
+} lrl_dev_curriculum;
+/* _resample_commands (legged_robot.py:595-626) of the listed envs: update(old bins, tracking sums / ep_len vs the
+ * thresholds, local_range) when `update`, sample(count), then commands[ids, :3] (|xy| > 0.2 mask), command_sums[:, ids]
+ * = 0 and the env bins — one workgroup, no host wait.  log_area: also command_area = np.sum(weights) / nbins after
+ * the update (reset_idx's log, legged_robot.py:272). */
+int32_t lrl_sim_curriculum_resample_dev(lrl_sim* sim, const lrl_dev_curriculum* cur, const int32_t* ids, int32_t nmax,
+                                        const int32_t* dcount, int32_t ep_len, int32_t row_lin, int32_t row_ang,
+                                        double lin_threshold, double ang_threshold, double local_range, int32_t update,
+                                        int32_t log_area, void* stream);
 /* Terrain mesh for params->terrain_mesh == 1 (gym.add_triangle_mesh / add_heightfield, legged_robot.py:
  * 1122-1160): `vertices` host [rows*cols][3] in the terrain frame (the Terrain class's trimesh vertices, or
  * the unmoved grid for a heightfield), placed at (-border_size, -border_size, 0) like tm_params.transform;

@@ -17,7 +17,8 @@
 #define LRL_HD static inline
 #endif
 
-enum { LRL_RNG_OBS_NOISE = 1, LRL_RNG_DR = 2, LRL_RNG_INIT = 3, LRL_RNG_POLICY = 4, LRL_RNG_RESET = 5, LRL_RNG_PUSH = 6 };
+enum { LRL_RNG_OBS_NOISE = 1, LRL_RNG_DR = 2, LRL_RNG_INIT = 3, LRL_RNG_POLICY = 4, LRL_RNG_RESET = 5, LRL_RNG_PUSH = 6,
+       LRL_RNG_TERRAIN = 7 };
 
 typedef struct { uint32_t v[4]; } lrl_u32x4;
 

@@ -23,11 +23,14 @@ namespace lrl {
 // xy draw xy_span * u + xy_lo and the (x_off, y_off) init offsets.  Uniform draws: (motor strength, Kp, Kd, x, y)
 // from Philox keyed by (global env, reset counter), or row t of S.inj_reset (the reference's torch.rand draws,
 // one row per env id in id order).  Float32 arithmetic in the reference's operation order, uncontracted.
+// (dn: the id count on the device, the host's n is then the launch bound — the upstream step's asynchronous path;
+// dctr: the reset counter, bumped on the device by bump_counter_kernel when the batch is not empty)
 __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
-                             int32_t root_mode, float xy_lo, float xy_span, float x_off, float y_off, int32_t inject,
-                             int64_t counter) {
+                             const int32_t* __restrict__ dn, int32_t root_mode, float xy_lo, float xy_span, float x_off,
+                             float y_off, int32_t inject, const int64_t* __restrict__ dctr) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= (dn ? min(*dn, n) : n)) return;
+  const int64_t counter = *dctr;
   const lrl_env_params& P = K->p;
   const int N = S.stride;
   int e = ids[t];
@@ -82,12 +85,16 @@ __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int3
 
 // _update_terrain_curriculum (legged_robot.py:793-818), one thread per reset env.  Float32 ops in torch's order
 // without contraction (torch.norm of a 2-vector: x0*x0 + x1*x1, then sqrt; the command term (|c| * T) * 0.5).
-__global__ void terrain_curriculum_kernel(KState S, const int32_t* __restrict__ ids, int32_t n, int64_t* levels,
+// rnd: injected wrap-around draws (one per id, the tests' reference draws); null: a uniform level in [0, max_level) from
+// the counter RNG keyed by (global env, step counter) — torch.randint_like's role (the reference's draws come from the
+// global torch generator, not reproducible across process layouts either)
+__global__ void terrain_curriculum_kernel(KState S, const int32_t* __restrict__ ids, int32_t n,
+                                          const int32_t* __restrict__ dn, int64_t* levels,
                                           const int64_t* __restrict__ types, const int64_t* __restrict__ rnd,
                                           const float* __restrict__ torig, int32_t rows, int32_t cols, float half,
-                                          float ep_len_s, int32_t max_level) {
+                                          float ep_len_s, int32_t max_level, int64_t step_counter) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= (dn ? min(*dn, n) : n)) return;
   const int e = ids[t];
   if (e < 0 || e >= S.n) return;
   const int N = S.stride;
@@ -98,7 +105,17 @@ __global__ void terrain_curriculum_kernel(KState S, const int32_t* __restrict__ 
   const bool up = dist > half;
   const bool down = dist < (cn * ep_len_s) * 0.5f && !up;
   int64_t lv = levels[e] + (up ? 1 : 0) - (down ? 1 : 0);
-  lv = lv >= max_level ? rnd[t] : (lv < 0 ? 0 : lv);
+  if (lv >= max_level) {
+    if (rnd) {
+      lv = rnd[t];
+    } else {
+      const lrl_u32x4 r = lrl_philox((uint32_t)(S.env_offset + e), (uint32_t)step_counter,
+                                     (LRL_RNG_TERRAIN << 16) ^ (uint32_t)(step_counter >> 32), 0, S.seed);
+      lv = (int64_t)(((uint64_t)r.v[0] * (uint64_t)max_level) >> 32);
+    }
+  } else if (lv < 0) {
+    lv = 0;
+  }
   levels[e] = lv;
   const int64_t li = lv < 0 ? 0 : (lv >= rows ? rows - 1 : lv);
   const int64_t ty = types[e] < 0 ? 0 : (types[e] >= cols ? cols - 1 : types[e]);
@@ -302,9 +319,15 @@ __global__ void randomize_kernel(KState S, float f0, float f1, float r0, float r
 // those envs zeroed) for every row of a [rows][ld] table in one launch: workgroup r sums row r over the ids in a
 // fixed order (strided per-thread partials, then an LDS tree), writes the mean, and after a barrier zeroes the
 // entries it read.
+// (dn: the id count on the device, n its bound; an empty batch then leaves the previous means in place, as the
+// reference's extras keep the last reset batch's episode dict)
 __global__ void rows_mean_zero_kernel(float* __restrict__ tab, int64_t ld, const int32_t* __restrict__ ids, int32_t n,
-                                      float* __restrict__ means, int32_t zero) {
+                                      const int32_t* __restrict__ dn, float* __restrict__ means, int32_t zero) {
   __shared__ float red[256];
+  if (dn) {
+    n = min(*dn, n);
+    if (n == 0) return;
+  }
   float* row = tab + (int64_t)blockIdx.x * ld;
   float s = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) s += row[ids[i]];
@@ -338,12 +361,19 @@ __global__ void step_code_kernel(KState S, int32_t interval, int32_t r0, int32_t
 // The step's reset env ids in ascending order (np.flatnonzero of the reset flags), compacted on the device by one
 // 1024-thread workgroup: thread t counts the flags of its contiguous run, a block-wide exclusive scan gives its write
 // offset (deterministic: the order is the env order).
-__global__ __launch_bounds__(1024) void compact_resets_kernel(KState S, int32_t* __restrict__ ids_out) {
+// MODE 0: the reset flags; MODE 1: the envs due for command resampling before this step's kernel ((episode_length + 1)
+// % interval == 0, every env when interval == 1: _post_physics_step_callback's set).  count_out (optional): the count.
+template <int MODE>
+__global__ __launch_bounds__(1024) void compact_kernel(KState S, int32_t interval, int32_t* __restrict__ ids_out,
+                                                       int32_t* __restrict__ count_out) {
   __shared__ int cnt[1024];
   const int t = threadIdx.x, n = S.n;
   const int per = (n + 1023) / 1024, b = t * per, e = min(n, b + per);
+  auto flag = [&](int i) {
+    return MODE == 0 ? S.reset[i] != 0 : (interval == 1 || (S.episode_length[i] + 1) % interval == 0);
+  };
   int c = 0;
-  for (int i = b; i < e; ++i) c += S.reset[i] != 0;
+  for (int i = b; i < e; ++i) c += flag(i);
   cnt[t] = c;
   __syncthreads();
   for (int w = 1; w < 1024; w <<= 1) {  // inclusive Hillis-Steele scan
@@ -354,7 +384,13 @@ __global__ __launch_bounds__(1024) void compact_resets_kernel(KState S, int32_t*
   }
   int o = cnt[t] - c;
   for (int i = b; i < e; ++i)
-    if (S.reset[i]) ids_out[o++] = i;
+    if (flag(i)) ids_out[o++] = i;
+  if (count_out && t == 1023) count_out[0] = cnt[1023];
+}
+
+// the reset counter of a non-empty batch (the host's count n, or the device count dn)
+__global__ void bump_counter_kernel(int64_t* ctr, const int32_t* __restrict__ dn, int32_t n) {
+  if (threadIdx.x == 0 && (dn ? min(*dn, n) : n) > 0) ctr[0] += 1;
 }
 
 // _resample_commands' device writes (legged_robot.py:595-626 as lrl/env.py restates it): commands[ids, :3] = cmds,
@@ -376,8 +412,18 @@ __global__ void apply_commands_kernel(KState S, int32_t ncs, const int32_t* __re
 extern "C" {
 hipError_t lrl_launch_step_code(const KState* S, int32_t interval, int32_t r0, int32_t r1, float* out, int32_t* ids_out,
                                 hipStream_t st) {
-  hipLaunchKernelGGL(lrl::step_code_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, *S, interval, r0, r1, out);
-  if (ids_out) hipLaunchKernelGGL(lrl::compact_resets_kernel, dim3(1), dim3(1024), 0, st, *S, ids_out);
+  if (out)
+    hipLaunchKernelGGL(lrl::step_code_kernel, dim3((S->n + 255) / 256), dim3(256), 0, st, *S, interval, r0, r1, out);
+  if (ids_out)
+    hipLaunchKernelGGL(lrl::compact_kernel<0>, dim3(1), dim3(1024), 0, st, *S, interval, ids_out, (int32_t*)nullptr);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_env_lists(const KState* S, int32_t mode, int32_t interval, int32_t* ids_out, int32_t* count_out,
+                                hipStream_t st) {
+  if (mode == 0)
+    hipLaunchKernelGGL(lrl::compact_kernel<0>, dim3(1), dim3(1024), 0, st, *S, interval, ids_out, count_out);
+  else
+    hipLaunchKernelGGL(lrl::compact_kernel<1>, dim3(1), dim3(1024), 0, st, *S, interval, ids_out, count_out);
   return hipGetLastError();
 }
 hipError_t lrl_launch_apply_commands(const KState* S, int32_t ncs, const int32_t* ids, int32_t n, const float* cmds,
@@ -393,23 +439,33 @@ int32_t lrl_rows_mean_zero(float* table, int64_t ld, int32_t rows, const int32_t
   if (!table || !means || rows < 0 || n < 0 || (n > 0 && !ids)) return 1;
   if (rows == 0) return 0;
   hipLaunchKernelGGL(lrl::rows_mean_zero_kernel, dim3(rows), dim3(256), 0, static_cast<hipStream_t>(stream), table,
-                     ld, ids, n, means, zero);
+                     ld, ids, n, (const int32_t*)nullptr, means, zero);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
-hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* ids, int32_t n, int32_t root_mode,
-                            float xy_lo, float xy_span, float x_off, float y_off, int32_t inject, int64_t counter,
-                            hipStream_t st) {
+int32_t lrl_rows_mean_zero_dev(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t nmax,
+                               const int32_t* dcount, float* means, int32_t zero, void* stream) {
+  if (!table || !means || rows < 0 || nmax < 0 || !dcount || (nmax > 0 && !ids)) return 1;
+  if (rows == 0 || nmax == 0) return 0;
+  hipLaunchKernelGGL(lrl::rows_mean_zero_kernel, dim3(rows), dim3(256), 0, static_cast<hipStream_t>(stream), table,
+                     ld, ids, nmax, dcount, means, zero);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* ids, int32_t n, const int32_t* dn,
+                            int32_t root_mode, float xy_lo, float xy_span, float x_off, float y_off, int32_t inject,
+                            int64_t* dctr, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, root_mode, xy_lo,
-                     xy_span, x_off, y_off, inject, counter);
+  hipLaunchKernelGGL(lrl::bump_counter_kernel, dim3(1), dim3(64), 0, st, dctr, dn, n);
+  hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, dn, root_mode, xy_lo,
+                     xy_span, x_off, y_off, inject, (const int64_t*)dctr);
   return hipGetLastError();
 }
-hipError_t lrl_launch_terrain_curriculum(const KState* S, const int32_t* ids, int32_t n, int64_t* levels,
-                                         const int64_t* types, const int64_t* rnd, const float* torig, int32_t rows,
-                                         int32_t cols, float half, float ep_len_s, int32_t max_level, hipStream_t st) {
+hipError_t lrl_launch_terrain_curriculum(const KState* S, const int32_t* ids, int32_t n, const int32_t* dn,
+                                         int64_t* levels, const int64_t* types, const int64_t* rnd, const float* torig,
+                                         int32_t rows, int32_t cols, float half, float ep_len_s, int32_t max_level,
+                                         int64_t step_counter, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lrl::terrain_curriculum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, *S, ids, n, levels,
-                     types, rnd, torig, rows, cols, half, ep_len_s, max_level);
+  hipLaunchKernelGGL(lrl::terrain_curriculum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, *S, ids, n, dn, levels,
+                     types, rnd, torig, rows, cols, half, ep_len_s, max_level, step_counter);
   return hipGetLastError();
 }
 hipError_t lrl_launch_set_root(const KState* S, const float* src, const int32_t* ids, int32_t n, hipStream_t st) {

@@ -29,16 +29,21 @@ extern "C" int lrl_set_error(int code, const char* msg) { return fail(code, "%s"
 
 extern "C" {
 hipError_t lrl_launch_env_step(const KParams*, const KState*, int, const float*, uint32_t, int64_t, int, hipStream_t);
-hipError_t lrl_launch_observe(const KParams*, const KState*, const int32_t*, int32_t, uint32_t, int64_t, hipStream_t);
+hipError_t lrl_launch_observe(const KParams*, const KState*, const int32_t*, int32_t, const int32_t*, uint32_t, int64_t,
+                              hipStream_t);
 hipError_t lrl_env_kernel_setup(int lds_bytes);
-hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, int32_t, float, float, float, float,
-                            int32_t, int64_t, hipStream_t);
+hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, const int32_t*, int32_t, float, float,
+                            float, float, int32_t, int64_t*, hipStream_t);
+hipError_t lrl_launch_env_lists(const KState*, int32_t, int32_t, int32_t*, int32_t*, hipStream_t);
+hipError_t lrl_launch_curriculum_dev(const lrl_dev_curriculum*, const KState*, int32_t, const int32_t*, int32_t,
+                                     const int32_t*, int32_t, int32_t, int32_t, double, double, double, int32_t,
+                                     int32_t, hipStream_t);
 hipError_t lrl_launch_set_root(const KState*, const float*, const int32_t*, int32_t, hipStream_t);
 hipError_t lrl_launch_step_code(const KState*, int32_t, int32_t, int32_t, float*, int32_t*, hipStream_t);
 hipError_t lrl_launch_apply_commands(const KState*, int32_t, const int32_t*, int32_t, const float*, const float*, float*,
                                      int32_t, hipStream_t);
-hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t, int64_t*, const int64_t*,
-                                         const int64_t*, const float*, int32_t, int32_t, float, float, int32_t,
+hipError_t lrl_launch_terrain_curriculum(const KState*, const int32_t*, int32_t, const int32_t*, int64_t*, const int64_t*,
+                                         const int64_t*, const float*, int32_t, int32_t, float, float, int32_t, int64_t,
                                          hipStream_t);
 hipError_t lrl_launch_set_dof(const KState*, const float*, const float*, const int32_t*, int32_t, hipStream_t);
 hipError_t lrl_launch_rigid_body(const KParams*, const KState*, const int32_t*, const int32_t*, const float*,
@@ -59,7 +64,7 @@ struct lrl_sim {
   size_t arena_bytes = 0;
   int lds_bytes = 0;
   int64_t step_counter = 0;
-  int64_t reset_counter = 0;
+  int64_t* d_reset_ctr = nullptr;  // reset_idx's counter-RNG counter, on the device (bumped per non-empty batch)
   lrl_tensor t[LRL_T_NUM];
   int32_t* d_body_leg = nullptr;
   int32_t* d_body_link = nullptr;
@@ -295,6 +300,8 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   size_t off = 0;
   for (auto& f : fields) { *f.p = (char*)arena + off; off += (f.bytes + 255) / 256 * 256; }
   HIPCHECK(hipMemset(arena, 0, total));
+  HIPCHECK(hipMalloc(&s->d_reset_ctr, sizeof(int64_t)));
+  HIPCHECK(hipMemset(s->d_reset_ctr, 0, sizeof(int64_t)));
   // initial values: identity quaternion, unit DR factors, default friction 1
   std::vector<float> ones(N, 1.f);
   HIPCHECK(hipMemcpy(S.root + 6ull * N, ones.data(), N * 4, hipMemcpyHostToDevice));
@@ -470,6 +477,7 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->terr);
   (void)hipFree(s->self_stats);
   (void)hipFree(s->d_code);
+  (void)hipFree(s->d_reset_ctr);
   for (auto& pr : s->ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -585,9 +593,41 @@ int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t 
   if (root_mode < 0 || root_mode > 2) return fail(LRL_E_INVALID, "root_mode %d", root_mode);
   const bool inject = (flags & LRL_STEP_INJECT_UNIFORM) != 0;
   if (inject && n > 0 && !s->S.inj_reset) return fail(LRL_E_INVALID, "injected reset uniforms not set");
-  s->reset_counter += 1;
-  HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, root_mode, xy_lo, xy_span, x_off, y_off, inject ? 1 : 0,
-                            s->reset_counter, (hipStream_t)stream));
+  HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, nullptr, root_mode, xy_lo, xy_span, x_off, y_off, inject ? 1 : 0,
+                            s->d_reset_ctr, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_reset_idx_dev(lrl_sim* s, const int32_t* ids, int32_t nmax, const int32_t* dcount, int32_t root_mode,
+                              float xy_lo, float xy_span, float x_off, float y_off, void* stream) {
+  if (!s || !dcount || nmax < 0 || (nmax > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  if (root_mode < 0 || root_mode > 2) return fail(LRL_E_INVALID, "root_mode %d", root_mode);
+  HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, nmax, dcount, root_mode, xy_lo, xy_span, x_off, y_off, 0,
+                            s->d_reset_ctr, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_curriculum_resample_dev(lrl_sim* s, const lrl_dev_curriculum* c, const int32_t* ids, int32_t nmax,
+                                        const int32_t* dcount, int32_t ep_len, int32_t row_lin, int32_t row_ang,
+                                        double lin_thr, double ang_thr, double local_range, int32_t update,
+                                        int32_t log_area, void* stream) {
+  if (!s || !c || !dcount || nmax < 0 || (nmax > 0 && !ids) || ep_len <= 0 || nmax > s->S.n)
+    return fail(LRL_E_INVALID, "lrl_sim_curriculum_resample_dev: bad argument");
+  if (!c->weights || !c->cdf || !c->state || !c->mt_key || !c->ep_rew_lin || !c->ep_rew_ang || !c->env_bins ||
+      !c->env_bins_f || !c->command_area || !c->axes || !c->words || !c->draws || c->nx <= 0 || c->ny <= 0 || c->nz <= 0)
+    return fail(LRL_E_INVALID, "lrl_sim_curriculum_resample_dev: incomplete curriculum");
+  if (row_lin < 0 || row_ang < 0 || row_lin >= s->hk.n_cs || row_ang >= s->hk.n_cs)
+    return fail(LRL_E_INVALID, "lrl_sim_curriculum_resample_dev: command-sum rows out of range");
+  if (nmax == 0) return 0;
+  HIPCHECK(lrl_launch_curriculum_dev(c, &s->S, s->hk.n_cs, ids, nmax, dcount, ep_len, row_lin, row_ang, lin_thr, ang_thr,
+                                     local_range, update, log_area, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_env_lists(lrl_sim* s, int32_t mode, int32_t interval, int32_t* ids_out, int32_t* count_out,
+                          void* stream) {
+  if (!s || !ids_out || !count_out || (mode != 0 && mode != 1) || interval < 1) return fail(LRL_E_INVALID, "bad argument");
+  HIPCHECK(lrl_launch_env_lists(&s->S, mode, interval, ids_out, count_out, (hipStream_t)stream));
   return 0;
 }
 
@@ -595,11 +635,25 @@ int32_t lrl_sim_terrain_curriculum(lrl_sim* s, const int32_t* ids, int32_t n, in
                                    const int64_t* rand_levels, const float* terrain_origins, int32_t rows,
                                    int32_t cols, float half_env_length, float episode_length_s, int32_t max_level,
                                    void* stream) {
-  if (!s || (n > 0 && (!ids || !levels || !types || !rand_levels || !terrain_origins)))
+  if (!s || (n > 0 && (!ids || !levels || !types || !terrain_origins)))  // (rand_levels null: counter-RNG draws)
     return fail(LRL_E_INVALID, "null argument");
   if (n < 0 || rows <= 0 || cols <= 0) return fail(LRL_E_INVALID, "bad sizes");
-  HIPCHECK(lrl_launch_terrain_curriculum(&s->S, ids, n, levels, types, rand_levels, terrain_origins, rows, cols,
-                                         half_env_length, episode_length_s, max_level, (hipStream_t)stream));
+  HIPCHECK(lrl_launch_terrain_curriculum(&s->S, ids, n, nullptr, levels, types, rand_levels, terrain_origins, rows, cols,
+                                         half_env_length, episode_length_s, max_level, s->step_counter,
+                                         (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_terrain_curriculum_dev(lrl_sim* s, const int32_t* ids, int32_t nmax, const int32_t* dcount,
+                                       int64_t* levels, const int64_t* types, const float* terrain_origins,
+                                       int32_t rows, int32_t cols, float half_env_length, float episode_length_s,
+                                       int32_t max_level, void* stream) {
+  if (!s || !dcount || nmax < 0 || (nmax > 0 && (!ids || !levels || !types || !terrain_origins)))
+    return fail(LRL_E_INVALID, "null argument");
+  if (rows <= 0 || cols <= 0) return fail(LRL_E_INVALID, "bad sizes");
+  HIPCHECK(lrl_launch_terrain_curriculum(&s->S, ids, nmax, dcount, levels, types, nullptr, terrain_origins, rows, cols,
+                                         half_env_length, episode_length_s, max_level, s->step_counter,
+                                         (hipStream_t)stream));
   return 0;
 }
 
@@ -627,7 +681,14 @@ int32_t lrl_sim_apply_commands(lrl_sim* s, const int32_t* ids, int32_t n, const 
 
 int32_t lrl_sim_observe_idx(lrl_sim* s, const int32_t* ids, int32_t n, uint32_t flags, void* stream) {
   if (!s || (n > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
-  HIPCHECK(lrl_launch_observe(s->dk, &s->S, ids, n, flags, s->step_counter, (hipStream_t)stream));
+  HIPCHECK(lrl_launch_observe(s->dk, &s->S, ids, n, nullptr, flags, s->step_counter, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_sim_observe_idx_dev(lrl_sim* s, const int32_t* ids, int32_t nmax, const int32_t* dcount, uint32_t flags,
+                                void* stream) {
+  if (!s || !dcount || nmax < 0 || (nmax > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
+  HIPCHECK(lrl_launch_observe(s->dk, &s->S, ids, nmax, dcount, flags, s->step_counter, (hipStream_t)stream));
   return 0;
 }
 

@@ -2432,9 +2432,9 @@ namespace lrl {
 // last_* buffers post_physics_step sets after the reset (last_actions = actions, last_dof_vel = dof_vel,
 // last_root_vel = root velocity).  One thread per listed env.
 __global__ void observe_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
-                               uint32_t flags, int64_t step_counter) {
+                               const int32_t* __restrict__ dn, uint32_t flags, int64_t step_counter) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= (dn ? min(*dn, n) : n)) return;  // (dn: device count, n its bound)
   const int e = ids[t];
   if (e < 0 || e >= S.n) return;
   const lrl_env_params& P = K->p;
@@ -2504,9 +2504,9 @@ extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int
 }
 
 extern "C" hipError_t lrl_launch_observe(const KParams* K, const KState* S, const int32_t* ids, int32_t n,
-                                         uint32_t flags, int64_t step_counter, hipStream_t stream) {
+                                         const int32_t* dn, uint32_t flags, int64_t step_counter, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lrl::observe_kernel, dim3((n + 127) / 128), dim3(128), 0, stream, K, *S, ids, n, flags,
+  hipLaunchKernelGGL(lrl::observe_kernel, dim3((n + 127) / 128), dim3(128), 0, stream, K, *S, ids, n, dn, flags,
                      step_counter);
   return hipGetLastError();
 }

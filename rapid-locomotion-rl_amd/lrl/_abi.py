@@ -109,6 +109,13 @@ class LrlPpoHparams(C.Structure):
                 ("beta2", f32), ("eps", f32)]
 
 
+class LrlDevCurriculum(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in ("weights", "cdf", "state", "mt_key", "ep_rew_lin", "ep_rew_ang", "env_bins",
+                                          "env_bins_f", "command_area", "axes")] + \
+               [("half", C.c_double * 3), ("nx", i32), ("ny", i32), ("nz", i32), ("words", C.c_void_p),
+                ("draws", C.c_void_p)]
+
+
 PPO_CTRL_BYTES = 64  # sizeof(lrl_ppo_ctrl): double lr, double loss_sum[3], float mb[4], float x4
 
 
@@ -136,7 +143,7 @@ _lib = None
 _CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 # the files and order of csrc/Makefile's SRC_HASH (SRCS then HDRS)
 _HASHED = ["lrl_env.hip", "lrl_aux.hip", "lrl_gae.hip", "lrl_gemm.hip", "lrl_ppo.hip", "lrl_capi.cpp", "lrl_curriculum.cpp",
-           "lrl_kparams.h", "lrl_gemm.h", "../../include/lrl.h", "../../include/lrl_philox.h"]
+           "lrl_curriculum_dev.hip", "lrl_kparams.h", "lrl_gemm.h", "../../include/lrl.h", "../../include/lrl_philox.h"]
 
 
 def source_hash():
@@ -174,7 +181,9 @@ def lib():
                      "lrl_sim_terrain_curriculum", "lrl_sim_inject_reset_uniforms", "lrl_sim_inject_push_uniforms", "lrl_sim_timing",
                      "lrl_sim_self_contact_stats", "lrl_ppo_store_step", "lrl_curriculum_sample",
                      "lrl_curriculum_update_weights", "lrl_rows_mean_zero", "lrl_sim_step_code",
-                     "lrl_sim_apply_commands", "lrl_sim_extras_snapshot"]:
+                     "lrl_sim_apply_commands", "lrl_sim_extras_snapshot", "lrl_sim_env_lists",
+                     "lrl_sim_terrain_curriculum_dev", "lrl_sim_reset_idx_dev", "lrl_sim_observe_idx_dev",
+                     "lrl_rows_mean_zero_dev", "lrl_sim_curriculum_resample_dev"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_np_sum_f64.restype = C.c_double
         L.lrl_np_sum_f64.argtypes = [C.c_void_p, C.c_int64]

