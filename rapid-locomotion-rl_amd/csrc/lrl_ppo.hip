@@ -496,7 +496,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
 // flight while this chunk's MFMAs run); step s of the chunk multiplies k = k0 + 4q + s.  16 rows per workgroup puts
 // 4,096 envs on 256 workgroups, one per CU (115 KB of LDS).
 constexpr int FA_R = 16, FA_THREADS = 256;
-constexpr int FA_D = 6;       // weight chunks (16 k each) in flight per wave: the L2 round trip over the MFMA work
+constexpr int FA_D = 2;       // weight chunks (32 k each) in flight per wave: the L2 round trip over the MFMA work
 constexpr int FA_XP = 260;    // X / he1 / h3 pitch (widths <= 256) + 4: conflict-free b128 row reads
 constexpr int FA_BIGP = 1028; // h1 pitch (2 x ac_h0 <= 1024)
 constexpr int FA_MIDP = 516;  // h2 pitch (2 x ac_h1 <= 512); priv / he2 use narrower pitches in the same region
@@ -520,7 +520,7 @@ template <int NB>
 __device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
   const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
   const int tpg = L.Ng >> 4, g = t0 / tpg;  // a run never crosses a group (fa_layer)
-  const float* A = L.A + i * L.pa + g * L.ga + 4 * q;
+  const float* A = L.A + i * L.pa + g * L.ga + 8 * q;
   const float* W = L.W + g * L.gw;
   int nr[NB];
 #pragma unroll
@@ -528,44 +528,51 @@ __device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
   fa_f32x4 acc[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) acc[j] = fa_f32x4{0.f, 0.f, 0.f, 0.f};
-  auto load_b = [&](float4 (&bv)[NB], int k0) {
-    const int k = k0 + 4 * q;
+  // per 32-k chunk lane (i, q) holds the 8 weights W[n][k0 + 8q .. +7] of each tile (one whole 128-B line per row and
+  // chunk over the 4 lane groups) and A[i][k0 + 8q .. +7]; step s multiplies k = k0 + 8q + s
+  auto load_b = [&](float4 (&bv)[NB][2], int k0) {
+    const int k = k0 + 8 * q;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int n = nr[j];
       const float* src = W + (int64_t)n * L.ldw + k;
-      if (L.vec && n < L.Nw && k < L.Kw) {
-        bv[j] = *reinterpret_cast<const float4*>(src);
+      if (L.vec && n < L.Nw && k + 7 < L.Kw) {
+        bv[j][0] = *reinterpret_cast<const float4*>(src);
+        bv[j][1] = *reinterpret_cast<const float4*>(src + 4);
       } else {
         const bool rn = n < L.Nw;
-        bv[j].x = rn && k < L.Kw ? src[0] : 0.f;
-        bv[j].y = rn && k + 1 < L.Kw ? src[1] : 0.f;
-        bv[j].z = rn && k + 2 < L.Kw ? src[2] : 0.f;
-        bv[j].w = rn && k + 3 < L.Kw ? src[3] : 0.f;
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = rn && k + u < L.Kw ? src[u] : 0.f;
+        bv[j][0] = make_float4(v[0], v[1], v[2], v[3]);
+        bv[j][1] = make_float4(v[4], v[5], v[6], v[7]);
       }
     }
   };
   // FA_D chunks of weights in flight (a ring of register sets, indexed at compile time by unrolling FA_D chunks)
-  const int nck = L.K >> 4;
-  float4 ring[FA_D][NB];
+  const int nck = L.K >> 5;
+  float4 ring[FA_D][NB][2];
 #pragma unroll
   for (int d = 0; d < FA_D; ++d)
-    if (d < nck) load_b(ring[d], 16 * d);
+    if (d < nck) load_b(ring[d], 32 * d);
   for (int c0 = 0; c0 < nck; c0 += FA_D) {
 #pragma unroll
     for (int d = 0; d < FA_D; ++d) {
       const int c = c0 + d;
       if (c < nck) {
-        const float4 a = *reinterpret_cast<const float4*>(A + 16 * c);
+        const float4 a0 = *reinterpret_cast<const float4*>(A + 32 * c);
+        const float4 a1 = *reinterpret_cast<const float4*>(A + 32 * c + 4);
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, ring[d][j].x, acc[j], 0, 0, 0);
+        for (int u = 0; u < 8; ++u) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, ring[d][j].y, acc[j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, ring[d][j].z, acc[j], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, ring[d][j].w, acc[j], 0, 0, 0);
-        if (c + FA_D < nck) load_b(ring[d], 16 * (c + FA_D));
+          for (int j = 0; j < NB; ++j) {
+            const float4& bq = ring[d][j][u >> 2];
+            const float b = (u & 3) == 0 ? bq.x : (u & 3) == 1 ? bq.y : (u & 3) == 2 ? bq.z : bq.w;
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b, acc[j], 0, 0, 0);
+          }
+        }
+        if (c + FA_D < nck) load_b(ring[d], 32 * (c + FA_D));
       }
     }
   }
@@ -1210,7 +1217,8 @@ static bool fused_act_fits(const lrl_ppo_net& n) {
     if (T >= 4 && T % 4) return false;
     return tpg % std::min(tpw, 8) == 0;
   };
-  return n.num_priv <= 32 && n.enc_h0 <= 256 && n.enc_h1 + 4 <= FA_MIDP && n.latent <= 32 && xs_of(n) <= 256 &&
+  return xs_of(n) % 32 == 0 && n.enc_h0 % 32 == 0 && n.enc_h1 % 32 == 0 && n.ac_h0 % 32 == 0 && n.ac_h1 % 32 == 0 &&
+         n.num_priv <= 32 && n.enc_h0 <= 256 && n.enc_h1 + 4 <= FA_MIDP && n.latent <= 32 && xs_of(n) <= 256 &&
          2 * n.ac_h0 <= 1024 && 2 * n.ac_h1 <= 512 && 2 * n.ac_h2 <= 256 && n.enc_h0 % 16 == 0 && n.enc_h1 % 16 == 0 &&
          n.ac_h0 % 16 == 0 && n.ac_h1 % 16 == 0 && run_ok(1, n.enc_h0) && run_ok(1, n.enc_h1) &&
          run_ok(1, (n.latent + 15) / 16 * 16) && run_ok(1, 2 * n.ac_h0) && run_ok(2, n.ac_h1) && run_ok(2, n.ac_h2);
