@@ -377,14 +377,15 @@ extern "C" hipError_t lrl_launch_curriculum_dev(const lrl_dev_curriculum* c, con
   const int nb = c->nx * c->ny * c->nz;
   const size_t lds = (size_t)nb * 8 + (size_t)(2 * nb + lrl::MT_N) * 4;
   if (nb / 64 + 2 > lrl::CD_MAX_LEAVES) return hipErrorInvalidValue;
+  constexpr size_t kMaxDyn = 144 * 1024;  // (+ the kernel's ~4 KB of static LDS, inside the CU's 160 KB)
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(lrl::curriculum_dev_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn) != hipSuccess)
       return hipErrorInvalidValue;
     attr = true;
   }
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > kMaxDyn) return hipErrorInvalidValue;
   hipLaunchKernelGGL(lrl::curriculum_dev_kernel, dim3(1), dim3(lrl::CD_THREADS), lds, st, a);
   return hipGetLastError();
 }
