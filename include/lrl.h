@@ -388,7 +388,7 @@ typedef struct lrl_dev_curriculum {
   uint32_t* mt_key;                /* [624] MT19937 key (numpy RandomState.get_state()[1]) */
   double *ep_rew_lin, *ep_rew_ang; /* [nbins] episode_reward_lin / _ang */
   int64_t* env_bins;               /* [num_envs] env_command_bins */
-  float* env_bins_f;               /* [num_envs] the float env bins reset_idx exposes as extras['env_bins'] */
+  float* env_bins_f;               /* [num_envs] every env's bin as of the last reset batch (extras['env_bins']) */
   double* command_area;            /* [1] np.sum(weights) / nbins at the last resample with log_area */
   const double* axes;              /* [nx + ny + nz] the grid axes (np.linspace of each key range) */
   double half[3];                  /* bin_sizes / 2 */

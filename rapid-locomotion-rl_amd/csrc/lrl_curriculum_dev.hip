@@ -347,9 +347,12 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
     cf[1] *= keep;
     const int e = a.ids[j];
     c.env_bins[e] = b;
-    c.env_bins_f[e] = (float)b;
     for (int d = 0; d < 3; ++d) S.commands[(int64_t)d * N + e] = cf[d];
     for (int r = 0; r < a.n_cs; ++r) S.command_sums[(int64_t)r * N + e] = 0.f;
+  }
+  if (a.log_area) {  // reset_idx: extras['env_bins'] = torch.Tensor(env_command_bins), every env's bin at this reset
+    __syncthreads();
+    for (int e = t; e < S.n; e += CD_THREADS) c.env_bins_f[e] = (float)c.env_bins[e];
   }
 }
 

@@ -500,7 +500,24 @@ constexpr int FA_D = 2;       // weight chunks (32 k each) in flight per wave: t
 constexpr int FA_XP = 260;    // X / he1 / h3 pitch (widths <= 256) + 4: conflict-free b128 row reads
 constexpr int FA_BIGP = 1028; // h1 pitch (2 x ac_h0 <= 1024)
 constexpr int FA_MIDP = 516;  // h2 pitch (2 x ac_h1 <= 512); priv / he2 use narrower pitches in the same region
-constexpr int FA_LDS_FLOATS = FA_R * (FA_XP + FA_BIGP + FA_MIDP);
+constexpr int FA_HW_FLOATS = (HEAD_NA + 1) * HEAD_W;  // the heads' weights, staged at the start
+constexpr int FA_LDS_FLOATS = FA_R * (FA_XP + FA_BIGP + FA_MIDP) + FA_HW_FLOATS;
+
+// Phase timers of the fused act (build with -DLRL_ACT_PROFILE, read with lrl_debug_act_profile): shader-clock cycles
+// per phase summed over workgroups (thread 0's view): stage, enc1..3, ac1..3, heads, sampling, storage copies
+#ifdef LRL_ACT_PROFILE
+__device__ unsigned long long g_act_prof[12];
+#define FA_PROF_DECL unsigned long long fa_t = clock64();
+#define FA_PROF(i)                                                  \
+  if (threadIdx.x == 0) {                                           \
+    const unsigned long long t_ = clock64();                        \
+    atomicAdd(&g_act_prof[i], t_ - fa_t);                           \
+    fa_t = t_;                                                      \
+  }
+#else
+#define FA_PROF_DECL
+#define FA_PROF(i)
+#endif
 
 typedef float fa_f32x4 __attribute__((ext_vector_type(4)));
 
@@ -516,34 +533,46 @@ struct FaLayer {
   int elu, vec;     // ELU after the bias; vec: 16-B aligned weight rows with Kw % 4 == 0 (float4 loads)
 };
 
-template <int NB>
+// NB column tiles of one group from t0; VEC: 16-B aligned weight rows (float4 loads), else dword loads.  The loads are
+// branch-free (addresses clamped into the weights, out-of-range elements zeroed by selection) so the compiler keeps the
+// FA_D chunks in flight with counted vmcnt waits instead of draining at every guarded load
+template <int NB, bool VEC>
 __device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
   const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
   const int tpg = L.Ng >> 4, g = t0 / tpg;  // a run never crosses a group (fa_layer)
   const float* A = L.A + i * L.pa + g * L.ga + 8 * q;
   const float* W = L.W + g * L.gw;
-  int nr[NB];
+  const float* rowp[NB];
+  bool rok[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) nr[j] = (t0 + j - g * tpg) * 16 + i;
+  for (int j = 0; j < NB; ++j) {
+    const int n = (t0 + j - g * tpg) * 16 + i;
+    rok[j] = n < L.Nw;
+    rowp[j] = W + (int64_t)(rok[j] ? n : L.Nw - 1) * L.ldw;
+  }
   fa_f32x4 acc[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) acc[j] = fa_f32x4{0.f, 0.f, 0.f, 0.f};
-  // per 32-k chunk lane (i, q) holds the 8 weights W[n][k0 + 8q .. +7] of each tile (one whole 128-B line per row and
+  // per 32-k chunk lane (i, q) holds the 8 weights W[n][k0 + 8q .. +7] of each tile (a whole 128-B line per row and
   // chunk over the 4 lane groups) and A[i][k0 + 8q .. +7]; step s multiplies k = k0 + 8q + s
   auto load_b = [&](float4 (&bv)[NB][2], int k0) {
     const int k = k0 + 8 * q;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int n = nr[j];
-      const float* src = W + (int64_t)n * L.ldw + k;
-      if (L.vec && n < L.Nw && k + 7 < L.Kw) {
-        bv[j][0] = *reinterpret_cast<const float4*>(src);
-        bv[j][1] = *reinterpret_cast<const float4*>(src + 4);
+      if constexpr (VEC) {  // (Kw % 4 == 0: a float4 is wholly inside or wholly outside the row)
+        const int k1 = min(k, L.Kw - 4), k2 = min(k + 4, L.Kw - 4);
+        float4 v0 = *reinterpret_cast<const float4*>(rowp[j] + k1);
+        float4 v1 = *reinterpret_cast<const float4*>(rowp[j] + k2);
+        const bool o0 = rok[j] && k < L.Kw, o1 = rok[j] && k + 4 < L.Kw;
+        bv[j][0] = o0 ? v0 : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[j][1] = o1 ? v1 : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
-        const bool rn = n < L.Nw;
         float v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = rn && k + u < L.Kw ? src[u] : 0.f;
+        for (int u = 0; u < 8; ++u) {
+          const float x = rowp[j][min(k + u, L.Kw - 1)];
+          v[u] = (rok[j] && k + u < L.Kw) ? x : 0.f;
+        }
         bv[j][0] = make_float4(v[0], v[1], v[2], v[3]);
         bv[j][1] = make_float4(v[4], v[5], v[6], v[7]);
       }
@@ -553,8 +582,7 @@ __device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
   const int nck = L.K >> 5;
   float4 ring[FA_D][NB][2];
 #pragma unroll
-  for (int d = 0; d < FA_D; ++d)
-    if (d < nck) load_b(ring[d], 32 * d);
+  for (int d = 0; d < FA_D; ++d) load_b(ring[d], 32 * min(d, nck - 1));
   for (int c0 = 0; c0 < nck; c0 += FA_D) {
 #pragma unroll
     for (int d = 0; d < FA_D; ++d) {
@@ -572,14 +600,14 @@ __device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b, acc[j], 0, 0, 0);
           }
         }
-        if (c + FA_D < nck) load_b(ring[d], 32 * (c + FA_D));
+        load_b(ring[d], 32 * min(c + FA_D, nck - 1));  // (past the end: a harmless re-read of the last chunk)
       }
     }
   }
   // C/D: column i of the tile, rows 4q .. 4q + 3 in the four registers
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int n = nr[j];
+    const int n = (t0 + j - g * tpg) * 16 + i;
     if (n < L.Nw) {
       const float bias = L.b[g * L.Nw + n];
       float* c = L.C + (4 * q) * L.pc + L.coff + g * L.Ng + n;
@@ -593,20 +621,29 @@ __device__ __forceinline__ void fa_tiles(const FaLayer& L, int t0) {
   }
 }
 
-// one layer: the T = groups * Ng / 16 column tiles split into equal runs over the 4 waves (T < 4: one tile per wave)
+// one layer: the T = groups * Ng / 16 column tiles split into equal runs over the 4 waves (T < 4: one tile per wave).
+// NBC > 0: the run length known at compile time (the presets' widths), else dispatched on it
+template <int NBC, bool VEC>
 __device__ __forceinline__ void fa_layer(const FaLayer& L) {
   const int w = threadIdx.x >> 6, T = L.groups * (L.Ng >> 4);
   const int tpw = T >= 4 ? T / 4 : 1;
   if (w * tpw >= T) return;
   const int t0 = w * tpw;
-  switch (tpw) {
-    case 1: fa_tiles<1>(L, t0); break;
-    case 2: fa_tiles<2>(L, t0); break;
-    case 4: fa_tiles<4>(L, t0); break;
-    case 8: fa_tiles<8>(L, t0); break;
-    case 16: fa_tiles<8>(L, t0); fa_tiles<8>(L, t0 + 8); break;
-    default:
-      for (int t = t0; t < t0 + tpw; ++t) fa_tiles<1>(L, t);
+  if constexpr (NBC == 16) {
+    fa_tiles<8, VEC>(L, t0);
+    fa_tiles<8, VEC>(L, t0 + 8);
+  } else if constexpr (NBC > 0) {
+    fa_tiles<NBC, VEC>(L, t0);
+  } else {
+    switch (tpw) {
+      case 1: fa_tiles<1, VEC>(L, t0); break;
+      case 2: fa_tiles<2, VEC>(L, t0); break;
+      case 4: fa_tiles<4, VEC>(L, t0); break;
+      case 8: fa_tiles<8, VEC>(L, t0); break;
+      case 16: fa_tiles<8, VEC>(L, t0); fa_tiles<8, VEC>(L, t0 + 8); break;
+      default:
+        for (int t = t0; t < t0 + tpw; ++t) fa_tiles<1, VEC>(L, t);
+    }
   }
 }
 
@@ -623,11 +660,16 @@ struct FusedActArgs {
   int store_row, do_store;
 };
 
+// PRESET: the presets' network (18 -> 256 -> 128 -> 18 encoder, 2 x (64 -> 512 -> 256 -> 128) bodies, aligned weights):
+// every layer's run length and load width fixed at compile time; otherwise dispatched per layer
+template <bool PRESET>
 __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
   extern __shared__ __attribute__((aligned(16))) float fa_lds[];
   float* X = fa_lds;                     // [16][FA_XP]: obs | latent | 0
   float* BIG = X + FA_R * FA_XP;         // he1 [16][FA_XP], h1 [16][FA_BIGP], h3 [16][FA_XP]
   float* MID = BIG + FA_R * FA_BIGP;     // priv [16][36], he2 [16][enc_h1 + 4], h2 [16][FA_MIDP]
+  float* HW = MID + FA_R * FA_MIDP;      // [NA + 1][HEAD_W]: w4a rows, then w4c
+  FA_PROF_DECL
   const lrl_ppo_net& nt = a.net;
   const int t = threadIdx.x, r0 = blockIdx.x * FA_R, nrows = min(FA_R, a.n - r0);
   const int no = nt.num_obs, np = nt.num_priv, PP = 36, EP2 = nt.enc_h1 + 4;
@@ -640,42 +682,56 @@ __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
     const int r = e >> 5, c = e & 31;
     MID[r * PP + c] = (r < nrows && c < np) ? a.priv[(int64_t)(r0 + r) * np + c] : 0.f;
   }
+  for (int e = t; e < FA_HW_FLOATS; e += FA_THREADS)
+    HW[e] = e < HEAD_NA * HEAD_W ? a.w[nt.w4a + e] : a.w[nt.w4c + (e - HEAD_NA * HEAD_W)];
   __syncthreads();
+  FA_PROF(0)
   const float* w = a.w;
   FaLayer L;
   // env_factor_encoder: priv -> enc_h0 (ELU) -> enc_h1 (ELU) -> latent, the latent into X[:, no:]
   L = FaLayer{MID, PP, 0, 32, w + nt.e1w, np, np, nt.enc_h0, 0, w + nt.e1b, BIG, FA_XP, 0, nt.enc_h0, 1, 1, 0};
-  fa_layer(L);
+  fa_layer<PRESET ? 4 : 0, false>(L);
   __syncthreads();
+  FA_PROF(1)
   L = FaLayer{BIG, FA_XP, 0, nt.enc_h0, w + nt.e2w, nt.enc_h0, nt.enc_h0, nt.enc_h1, 0, w + nt.e2b, MID, EP2, 0,
               nt.enc_h1, 1, 1, (int)(a.vec >> 1) & 1};
-  fa_layer(L);
+  if (PRESET || (a.vec & 2u)) fa_layer<PRESET ? 2 : 0, true>(L);
+  else fa_layer<0, false>(L);
   __syncthreads();
+  FA_PROF(2)
   L = FaLayer{MID, EP2, 0, nt.enc_h1, w + nt.e3w, nt.enc_h1, nt.enc_h1, nt.latent, 0, w + nt.e3b, X, FA_XP, no,
               (nt.latent + 15) / 16 * 16, 1, 0, (int)(a.vec >> 2) & 1};
-  fa_layer(L);
+  if (PRESET || (a.vec & 4u)) fa_layer<PRESET ? 1 : 0, true>(L);
+  else fa_layer<0, false>(L);
   __syncthreads();
+  FA_PROF(3)
   // actor / critic bodies, both at once: [obs | latent] -> 2 x ac_h0 -> 2 x ac_h1 -> 2 x ac_h2 (ELU)
   const int nx = no + nt.latent;
   L = FaLayer{X, FA_XP, 0, a.xs, w + nt.w1, nx, nx, 2 * nt.ac_h0, 0, w + nt.b1, BIG, FA_BIGP, 0, 2 * nt.ac_h0, 1, 1,
               (int)(a.vec >> 3) & 1};
-  fa_layer(L);
+  if (PRESET || (a.vec & 8u)) fa_layer<PRESET ? 16 : 0, true>(L);
+  else fa_layer<0, false>(L);
   __syncthreads();
+  FA_PROF(4)
   L = FaLayer{BIG, FA_BIGP, nt.ac_h0, nt.ac_h0, w + nt.w2, nt.ac_h0, nt.ac_h0, nt.ac_h1, (int64_t)nt.ac_h1 * nt.ac_h0,
               w + nt.b2, MID, FA_MIDP, 0, nt.ac_h1, 2, 1, (int)(a.vec >> 4) & 1};
-  fa_layer(L);
+  if (PRESET || (a.vec & 16u)) fa_layer<PRESET ? 8 : 0, true>(L);
+  else fa_layer<0, false>(L);
   __syncthreads();
+  FA_PROF(5)
   L = FaLayer{MID, FA_MIDP, nt.ac_h1, nt.ac_h1, w + nt.w3, nt.ac_h1, nt.ac_h1, nt.ac_h2, (int64_t)nt.ac_h2 * nt.ac_h1,
               w + nt.b3, BIG, FA_XP, 0, nt.ac_h2, 2, 1, (int)(a.vec >> 5) & 1};
-  fa_layer(L);
+  if (PRESET || (a.vec & 32u)) fa_layer<PRESET ? 4 : 0, true>(L);
+  else fa_layer<0, false>(L);
   __syncthreads();
+  FA_PROF(6)
   // heads: thread (r, j) j < na: mu; (r, na): value — sequential fmaf over k, as act_head_kernel's mu
   constexpr int NA = HEAD_NA;
   float* MU = X;  // the obs tile is dead: [16][NA + 1] mu, then log-prob terms; value in column NA
   if (t < FA_R * (NA + 1)) {
     const int r = t / (NA + 1), j = t - r * (NA + 1);
     const float* h = BIG + r * FA_XP + (j < NA ? 0 : HEAD_W);
-    const float* wr = j < NA ? w + nt.w4a + j * HEAD_W : w + nt.w4c;
+    const float* wr = HW + j * HEAD_W;  // (row NA: w4c)
     float s = 0.f;
 #pragma unroll 8
     for (int k = 0; k < HEAD_W; ++k) s = fmaf(h[k], wr[k], s);
@@ -683,6 +739,7 @@ __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
     MU[r * 16 + j] = s;
   }
   __syncthreads();
+  FA_PROF(7)
   const int64_t so = (int64_t)a.store_row * a.n;
   if (t < FA_R * NA) {
     const int r = t / NA, j = t - r * NA, g = r0 + r;
@@ -724,6 +781,7 @@ __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
       a.store.logp[so + g] = lp;
     }
   }
+  FA_PROF(8)
   if (a.do_store) {  // obs / priv / history rows of this tile into storage row `store_row`
     const int64_t b = so + r0;
     copy_rows(a.obs + (int64_t)r0 * no, no, a.store.obs + b * no, no, nrows, no, t);
@@ -733,6 +791,7 @@ __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
       copy_rows(a.hist + (int64_t)r0 * hd, hd, a.store.hist + b * ld, ld, nrows, hd, t);
     }
   }
+  FA_PROF(9)
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1229,6 +1288,21 @@ extern "C" int64_t lrl_ppo_act_workspace_bytes(const lrl_ppo_net* net, int32_t n
   return make_act_plan(*net, n, nullptr).bytes;
 }
 
+extern "C" int lrl_debug_act_profile(unsigned long long* out, int reset) {
+#ifdef LRL_ACT_PROFILE
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_act_prof), sizeof(unsigned long long) * 12) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[12] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_act_prof), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 12;
+#else
+  (void)out;
+  (void)reset;
+  return 0;
+#endif
+}
+
 extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, const float* obs, const float* priv,
                                const float* hist, int32_t n, const float* eps, uint64_t seed, uint64_t counter,
                                int64_t row_offset, float* actions, float* mu, float* values, float* logp, const lrl_rollout_store* store,
@@ -1242,9 +1316,14 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   const lrl_ppo_net& nt = *net;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (fused_act_fits(nt)) {  // one launch: act_fused_kernel
-    static const bool ok = [] { return hipFuncSetAttribute(reinterpret_cast<const void*>(act_fused_kernel),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           FA_LDS_FLOATS * sizeof(float)) == hipSuccess; }();
+    static const bool ok = [] {
+      auto set = [](const void* f) {
+        return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, FA_LDS_FLOATS * sizeof(float)) ==
+               hipSuccess;
+      };
+      return set(reinterpret_cast<const void*>(act_fused_kernel<true>)) &&
+             set(reinterpret_cast<const void*>(act_fused_kernel<false>));
+    }();
     if (!ok) return lrl_set_error(LRL_E_HIP, "lrl_ppo_act: fused kernel LDS attribute");
     FusedActArgs fa{};
     fa.w = params; fa.net = nt; fa.obs = obs; fa.priv = priv; fa.hist = hist; fa.eps = eps;
@@ -1257,8 +1336,14 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
     fa.actions = actions; fa.mu = mu; fa.values = values; fa.logp = logp;
     if (store) fa.store = *store;
     fa.store_row = store_row; fa.do_store = store ? 1 : 0;
-    hipLaunchKernelGGL(act_fused_kernel, dim3((n + FA_R - 1) / FA_R), dim3(FA_THREADS), FA_LDS_FLOATS * sizeof(float),
-                       st, fa);
+    const bool preset = nt.enc_h0 == 256 && nt.enc_h1 == 128 && nt.latent <= 32 && nt.ac_h0 == 512 && nt.ac_h1 == 256 &&
+                        nt.ac_h2 == 128 && fa.vec == 62u;
+    if (preset)
+      hipLaunchKernelGGL(act_fused_kernel<true>, dim3((n + FA_R - 1) / FA_R), dim3(FA_THREADS),
+                         FA_LDS_FLOATS * sizeof(float), st, fa);
+    else
+      hipLaunchKernelGGL(act_fused_kernel<false>, dim3((n + FA_R - 1) / FA_R), dim3(FA_THREADS),
+                         FA_LDS_FLOATS * sizeof(float), st, fa);
     return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_ppo_act: launch failed");
   }
   ActPlan P = make_act_plan(nt, n, static_cast<char*>(workspace));

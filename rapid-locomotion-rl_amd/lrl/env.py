@@ -444,7 +444,8 @@ class LeggedRobotEnv:
         d["state"].copy_(torch.tensor([0, int(cur._mt_pos[0]), 0, 0], dtype=torch.int32))
         bins = np.ascontiguousarray(self._env_command_bins, np.int64)
         d["env_bins"].copy_(torch.from_numpy(bins))
-        d["env_bins_f"].copy_(torch.from_numpy(bins.astype(np.float32)))
+        if self.env_command_bins_t is not d["env_bins_f"]:  # (the bins the last reset exposed, not the current ones)
+            d["env_bins_f"].copy_(self.env_command_bins_t.reshape(-1)[:self.num_envs].to(torch.float32))
         self._dev_auth = True
 
     # -------------------------------------------------------------------------------- plumbing
