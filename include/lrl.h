@@ -541,11 +541,18 @@ int32_t lrl_ppo_adaptation_step(const lrl_ppo_net* net, float* params, const flo
  * (either pointer may be NULL), clears them, and sets the enable flag for what follows. */
 int32_t lrl_ppo_timing(int32_t enable, double* total_ms, int64_t* launches);
 
+/* Development switch of the update's GEMM kernels (tests compare them in one process): bit 0 set = no pre-split-B
+ * kernel for the weight products, bit 1 set = no LDS-DMA weight-gradient kernel; the fp32-staged x6 kernel takes
+ * those products instead.  Returns the previous mask. */
+int32_t lrl_debug_gemm_paths(int32_t disable_mask);
+
 /* Test entry point of the GEMM the update is built from: C = op(A) op(B) with
  * layout 0 (NT: C[m][n] = sum_k A[m][k] B[n][k]), 2 (NN: sum_k A[m][k] B[k][n]),
  * 3 (TN: sum_k A[k][m] B[k][n], split over k, partials reduced in place);
  * epi 0 store, 1 +bias[n], 2 elu(+bias[n]), 3 *elu'(aux[m][n]).  rows (optional) gathers A's rows
- * (NT/NN) or B's rows (TN). */
+ * (NT/NN) or B's rows (TN).  layout | 0x100 (NT / NN): B is first split into hi / mid / lo bf16 planes in the
+ * workspace (3 * N * round16(K) / 2 floats) and the product runs on the pre-split-B kernel the update uses for its
+ * weight products, or fails if the shape is not one it takes. */
 int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda,
                      const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, const float* aux,
                      int64_t ld_aux, const int64_t* rows, float* workspace, int64_t workspace_floats, void* stream);

@@ -23,6 +23,12 @@
 #pragma once
 #include <stdint.h>
 
+#ifdef __HIPCC__
+#define LRL_GHD __host__ __device__
+#else
+#define LRL_GHD
+#endif
+
 namespace lrl {
 
 enum GemmEpi : int {
@@ -49,7 +55,37 @@ struct GemmP {
   int64_t lda, ldb, ldc, ld_aux;
   int64_t ga, gb, gc, gbias, gaux;  // per-group element offsets
   int64_t part_stride;              // EPI_PARTIAL: elements between split slices of C ([split][group][M][N])
+  // pre-split B (x6p kernel, NT / NN): hi / mid / lo bf16 planes of op(B) in [n][k] form (x6_planes_launch), k padded
+  // to bpl_ld (a multiple of 16, zero past K); plane pl of group g at bpl + pl * bpl_ps + g * gbp.  nullptr: B is read
+  // as fp32 from `B` by the other kernels
+  const uint16_t* bpl;
+  int64_t bpl_ld, bpl_ps, gbp;
 };
+
+// One weight matrix to split into planes: W is [rows][cols] (ldw) per group (gsrc elements apart); op(B) in [n][k]
+// form is W itself (trans = 0: n = row, k = col — the forward's B) or its transpose (trans = 1: n = col, k = row — the
+// backward-data B).  dst receives [3][groups][n][kp] bf16 (kp = k rounded up to 16; the padding is zero).
+struct PlaneJob {
+  const float* W;
+  int64_t ldw, gsrc;
+  int rows, cols, trans, groups;
+  uint16_t* dst;
+};
+constexpr int MAX_PLANE_JOBS = 8;
+LRL_GHD inline int plane_kp(const PlaneJob& j) { return ((j.trans ? j.rows : j.cols) + 15) / 16 * 16; }
+LRL_GHD inline int plane_n(const PlaneJob& j) { return j.trans ? j.cols : j.rows; }
+LRL_GHD inline int64_t plane_elems(const PlaneJob& j) { return 3ll * j.groups * plane_n(j) * plane_kp(j); }
+// Split every job's matrix into its planes (one launch for up to MAX_PLANE_JOBS jobs).
+int x6_planes_launch(const PlaneJob* jobs, int n, void* stream);
+// false when LRL_GEMM_X6P=0 (no planes: every product reads fp32 B)
+bool gemm_x6p_enabled();
+// Point p's pre-split B at job j's planes.
+inline void gemm_use_planes(GemmP& p, const PlaneJob& j) {
+  p.bpl = j.dst;
+  p.bpl_ld = plane_kp(j);
+  p.gbp = (int64_t)plane_n(j) * plane_kp(j);
+  p.bpl_ps = p.gbp * j.groups;
+}
 
 // layout: bit0 = A m-contiguous, bit1 = B n-contiguous
 enum GemmLayout : int { GEMM_NT = 0, GEMM_NN = 2, GEMM_TN = 3 };
@@ -57,6 +93,9 @@ enum GemmLayout : int { GEMM_NT = 0, GEMM_NN = 2, GEMM_TN = 3 };
 // Enqueue C = op(A, B) for `groups` independent problems of the same shape.  Returns 0 or a negative
 // lrl error code (bad shape / unsupported layout).
 int gemm_launch(const GemmP& p, int layout, int epi, int groups, void* stream);
+
+// 1 when this thread's last gemm_launch ran the x6p kernel (test entry point)
+int gemm_last_path();
 
 // How a weight-gradient product (reduction over K rows, `groups` problems) is split: the split count.
 int gemm_pick_splits(int M, int N, int K, int groups);

@@ -1327,6 +1327,441 @@ static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t s
   return rc ? rc : 1;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// x6 with a pre-split B ("x6p", NT / NN products whose B is a weight matrix).  The weights are split into their
+// hi / mid / lo bf16 planes once per optimiser step (x6_planes_kernel, op(B) already in [n][k] form — the transpose
+// of the backward-data B is taken there), so nothing in the product transposes or splits B.  Both operands then
+// stage global -> LDS by LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass) into a 3-deep ring
+// of 16-k stages with counted vmcnt waits and a raw s_barrier, so two stages stay in flight across each barrier;
+// only A (fp32 activations) is split, in registers, right after its ds_read: one split per element and reading wave,
+// 11 VALU per pair of floats, which the MFMAs of the other workgroup on the SIMD (2 per CU) hide.
+//   A image per stage: [BM][16] fp32 (64-B rows), 16-B chunk c of row r in slot c ^ ((r >> 2) & 3); a DMA
+//   wave-instruction fills 16 rows (lane l: row l / 4, slot l % 4, source chunk pre-swizzled).
+//   B images per stage: 3 planes of [128][16] bf16 (32-B rows), chunk c of row r in slot c ^ ((r >> 3) & 1); a DMA
+//   wave-instruction fills 32 rows of one plane.
+// Tile BM x 128 (BM = 64 / 128), 4 waves in a 2 x 2 grid, wave tile (BM/2) x 64; the six MFMA products per 32x32x16
+// step in the order of gemm_x6_kernel over the same k order, so the result is bit-identical to it.
+template <int BM, int EPI, bool GATHER>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_x6p_kernel(GemmP p) {
+  constexpr int BN = 128, NST = 3, TM = BM / 64, TN = 2;
+  constexpr int AIMG = BM * 64, BIMG = BN * 32, STB = AIMG + 3 * BIMG;  // bytes
+  constexpr int NA = BM / 64, NB = 3;  // DMA wave-instructions per wave and stage
+  constexpr int NPW = NA + NB;
+  static_assert(NPW == 4 || NPW == 5, "vmcnt table");
+  __shared__ __attribute__((aligned(16))) uint8_t S[NST * STB];  // the only LDS object (see the glds rules)
+  const int mt = p.M / BM, nt = p.N / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, g = L / (nt * mt);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const float* __restrict__ A = p.A + g * p.ga;
+  const uint16_t* __restrict__ Bp = p.bpl + g * p.gbp;
+  const float* asrc[NA];
+#pragma unroll
+  for (int d = 0; d < NA; ++d) {
+    const int r = (w * NA + d) * 16 + (lane >> 2), ch = (lane & 3) ^ ((r >> 2) & 3);
+    asrc[d] = A + (GATHER ? p.a_rows[m0 + r] : (int64_t)(m0 + r)) * p.lda + 4 * ch;
+  }
+  const uint16_t* bsrc[NB];
+#pragma unroll
+  for (int d = 0; d < NB; ++d) {
+    const int j = w * NB + d, r = (j & 3) * 32 + (lane >> 1), ch = (lane & 1) ^ ((r >> 3) & 1);
+    bsrc[d] = Bp + (j >> 2) * p.bpl_ps + (int64_t)(n0 + r) * p.bpl_ld + 8 * ch;
+  }
+  const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
+  // the DMA is issued from inline asm so the compiler does not track it; completion is ordered by the counted waits
+  auto dma = [&](const void* src, uint32_t lds_off) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_off)
+                 : "memory");
+  };
+  auto issue = [&](int st, int k0) {
+    const uint32_t base = s_lds + (uint32_t)(st * STB);
+#pragma unroll
+    for (int d = 0; d < NA; ++d) dma(asrc[d] + k0, __builtin_amdgcn_readfirstlane(base + (w * NA + d) * 1024));
+#pragma unroll
+    for (int d = 0; d < NB; ++d) dma(bsrc[d] + k0, __builtin_amdgcn_readfirstlane(base + AIMG + (w * NB + d) * 1024));
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int ns = p.K / 16;
+  issue(0, 0);
+  if (ns > 1) issue(1, 16);
+  for (int s = 0; s < ns; ++s) {
+    // this wave's DMAs of stage s have landed (stage s + 1's may stay in flight) ...
+    if (s + 1 < ns) {
+      if constexpr (NPW == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // ... and every wave's; every wave is also done reading stage s - 1, whose buffer stage s + 2 refills
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < ns) issue((s + 2) % NST, (s + 2) * 16);
+    const uint8_t* As = S + (s % NST) * STB;
+    const uint8_t* Bs = As + AIMG;
+    bf16x8_t a[TM][3], b[TN][3];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = wn + 32 * j + li, off = r * 32 + 16 * (h ^ ((r >> 3) & 1));
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) b[j][pl] = *reinterpret_cast<const bf16x8_t*>(Bs + pl * BIMG + off);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm + 32 * i + li, sw = (r >> 2) & 3;
+      const float4 x0 = *reinterpret_cast<const float4*>(As + r * 64 + 16 * ((2 * h) ^ sw));
+      const float4 x1 = *reinterpret_cast<const float4*>(As + r * 64 + 16 * ((2 * h + 1) ^ sw));
+      uint32_t hh[4], mm[4], ll[4];
+      x6_split2(x0.x, x0.y, hh[0], mm[0], ll[0]);
+      x6_split2(x0.z, x0.w, hh[1], mm[1], ll[1]);
+      x6_split2(x1.x, x1.y, hh[2], mm[2], ll[2]);
+      x6_split2(x1.z, x1.w, hh[3], mm[3], ll[3]);
+      uint4 vh = make_uint4(hh[0], hh[1], hh[2], hh[3]), vm = make_uint4(mm[0], mm[1], mm[2], mm[3]),
+            vl = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+      a[i][0] = *reinterpret_cast<bf16x8_t*>(&vh);
+      a[i][1] = *reinterpret_cast<bf16x8_t*>(&vm);
+      a[i][2] = *reinterpret_cast<bf16x8_t*>(&vl);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+  }
+
+  float* __restrict__ C = p.C + g * p.gc;
+  const float* __restrict__ bias = p.bias ? p.bias + g * p.gbias : nullptr;
+  const float* __restrict__ ax = EPI == EPI_DELU ? p.aux + g * p.gaux : nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn + 32 * j + li;
+    float bj = 0.f;
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = bias[col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // rows 8q + 4h .. +3 of the MFMA tile: accumulator registers 4q .. 4q+3
+        const int row0 = m0 + wm + 32 * i + 8 * q + 4 * h;
+        float* __restrict__ crow = C + (int64_t)row0 * p.ldc + col;
+        float xa[4];
+        if constexpr (EPI == EPI_DELU) {
+          const float* __restrict__ xrow = ax + (int64_t)row0 * p.ld_aux + col;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xa[r] = xrow[r * p.ld_aux];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][4 * q + r];
+          if (EPI == EPI_BIAS) v += bj;
+          if (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+          if constexpr (EPI == EPI_DELU) {
+            const float x = xa[r];
+            v = x > 0.f ? v : v * (x + 1.f);
+          }
+          crow[r * p.ldc] = v;
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// x6 weight gradient with LDS-DMA staging ("x6t", TN, split-k partials): both operands are [k][r] activations
+// (r = the output row / column), so they land as [16 k][128 r] fp32 images by LDS-DMA (a wave-instruction fills two
+// k-rows; 16-B chunk c of k-row k sits in slot c ^ (8 * ((k >> 3) & 1)), so the two lane halves of a read, k and
+// k + 8, use opposite bank halves), in a 3-deep ring with counted vmcnt and a raw barrier.  Each lane gathers its
+// 8 k-values per MFMA operand with ds_read_b32 (immediate offsets) and splits them in registers.  128 x 128 tiles,
+// 4 waves of 2 x 2 MFMA tiles, the six products in gemm_x6_kernel's order over the same k order, and the bias
+// gradient partial summed in its (row, k-half) order: bit-identical to it.
+template <int TAG>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
+  constexpr int BM = 128, BN = 128, NST = 3, TM = 2, TN = 2;
+  constexpr int IMG = 16 * 128 * 4, STB = 2 * IMG;  // bytes: A image then B image
+  constexpr int NPW = 4;                            // DMA wave-instructions per wave and stage (2 per operand)
+  __shared__ __attribute__((aligned(16))) uint8_t S[NST * STB];
+  const int mt = p.M / BM, nt = p.N / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, zz = L / (nt * mt);
+  const int g = zz / p.splits, sp = zz - g * p.splits;
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int kbeg = sp * p.kps, kend = min(p.K, kbeg + p.kps);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ Bm = p.B + g * p.gb;
+  // this lane's DMA sources: k-row 2 (2w + d) + lane / 32, slot lane % 32 (source chunk pre-swizzled)
+  const float* asrc[2];
+  const float* bsrc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int kr = 2 * (2 * w + d) + (lane >> 5), ch = (lane & 31) ^ (8 * ((kr >> 3) & 1));
+    asrc[d] = A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * ch;
+    bsrc[d] = Bm + (int64_t)(kbeg + kr) * p.ldb + n0 + 4 * ch;
+  }
+  const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
+  auto dma = [&](const void* src, uint32_t lds_off) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_off)
+                 : "memory");
+  };
+  auto issue = [&](int st, int s) {
+    const uint32_t base = s_lds + (uint32_t)(st * STB);
+    const int64_t ka = (int64_t)16 * s * p.lda, kb = (int64_t)16 * s * p.ldb;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) dma(asrc[d] + ka, __builtin_amdgcn_readfirstlane(base + (2 * w + d) * 1024));
+#pragma unroll
+    for (int d = 0; d < 2; ++d) dma(bsrc[d] + kb, __builtin_amdgcn_readfirstlane(base + IMG + (2 * w + d) * 1024));
+  };
+  const bool do_bsum = p.bias_part != nullptr && tn_ == 0 && wn == 0;
+  float bsum[TM] = {0.f, 0.f};
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int ns = (kend - kbeg) / 16;
+  if (ns > 0) issue(0, 0);
+  if (ns > 1) issue(1, 1);
+  // lane's element offsets (floats) into an image: k-row 8h + t at + 128 t, row / column r ^ 32 h
+  const int sw = 32 * h;
+  for (int s = 0; s < ns; ++s) {
+    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < ns) issue((s + 2) % NST, s + 2);
+    static_assert(NPW == 4, "vmcnt above");
+    const float* As = reinterpret_cast<const float*>(S + (s % NST) * STB);
+    const float* Bs = As + IMG / 4;
+    bf16x8_t a[TM][3], b[TN][3];
+    auto gather_split = [&](const float* img, int r, bf16x8_t (&o)[3], float* vs) {
+      const float* src = img + 8 * h * 128 + (r ^ sw);
+      float v[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = src[128 * t];
+      if (vs) {
+        float s8 = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s8 += v[t];
+        *vs += s8;
+      }
+      uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x6_split2(v[2 * e], v[2 * e + 1], hh[e], mm[e], ll[e]);
+      uint4 vh = make_uint4(hh[0], hh[1], hh[2], hh[3]), vm = make_uint4(mm[0], mm[1], mm[2], mm[3]),
+            vl = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+      o[0] = *reinterpret_cast<bf16x8_t*>(&vh);
+      o[1] = *reinterpret_cast<bf16x8_t*>(&vm);
+      o[2] = *reinterpret_cast<bf16x8_t*>(&vl);
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) gather_split(As, wm + 32 * i + li, a[i], do_bsum ? &bsum[i] : nullptr);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) gather_split(Bs, wn + 32 * j + li, b[j], nullptr);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+  }
+
+  float* __restrict__ C = p.C + g * p.gc + (int64_t)sp * p.part_stride;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn + 32 * j + li;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row0 = m0 + wm + 32 * i + 8 * q + 4 * h;
+        float* __restrict__ crow = C + (int64_t)row0 * p.ldc + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) crow[r * p.ldc] = acc[i][j][4 * q + r];
+      }
+  }
+  if (p.bias_part != nullptr && tn_ == 0) {
+    // bias-gradient partial: row r's two k-halves added in gemm_x6_kernel's order (k-half 0 first, from 0)
+    __syncthreads();  // every stage read has retired (no DMA is in flight after the last vmcnt(0))
+    float* red = reinterpret_cast<float*>(S);
+    if (wn == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) red[h * BM + wm + 32 * i + li] = bsum[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < BM) {
+      float s = 0.f;
+      s += red[threadIdx.x];
+      s += red[BM + threadIdx.x];
+      p.bias_part[((int64_t)sp * p.groups + g) * p.M + m0 + threadIdx.x] = s;
+    }
+  }
+}
+
+// run-time path mask (lrl_debug_gemm_paths: tests compare the paths in one process): bit 0 off = no x6p, bit 1 = no x6t
+static int g_path_off = 0;
+// x6t path switch: LRL_GEMM_X6T=0 keeps the weight gradients on gemm_x6_kernel
+static bool x6t_enabled() {
+  static const int on = [] {
+    const char* e = getenv("LRL_GEMM_X6T");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0 && !(__atomic_load_n(&g_path_off, __ATOMIC_RELAXED) & 2);
+}
+
+// returns 1 when launched on the x6t kernel (0: not eligible, <0: error)
+static int try_x6t(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
+  if (!x6t_enabled() || layout != GEMM_TN || epi != EPI_PARTIAL || p.b_rows) return 0;
+  if (p.M % 128 || p.N % 128 || p.K % 16 || p.kps % 16 || p.kps < 16 || p.avec != 4 || p.bvec != 4) return 0;
+  if ((int64_t)(p.splits - 1) * p.kps >= p.K) return 0;  // (every split has a non-empty range)
+  dim3 grid((unsigned)((p.M / 128) * (p.N / 128) * groups * p.splits));
+  switch (tn_shape_tag(p.M, p.N, groups)) {
+    case 1: hipLaunchKernelGGL((gemm_x6t_kernel<1>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm_x6t_kernel<2>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((gemm_x6t_kernel<6>), grid, dim3(GTHREADS), 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x6t_kernel<0>), grid, dim3(GTHREADS), 0, st, p); break;
+  }
+  return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
+}
+
+// x6p path switch for the update: off unless LRL_GEMM_X6P=1 — measured slower than gemm_x6_kernel on every update
+// shape (the 6-byte planes of B cost more DMA issue and LDS traffic than the staging split saves, and A
+// is split by both waves that read it); products whose caller hands over planes (lrl_gemm_f32 layout | 0x100) run it
+static bool x6p_enabled() {
+  static const int on = [] {
+    const char* e = getenv("LRL_GEMM_X6P");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on != 0 && !(__atomic_load_n(&g_path_off, __ATOMIC_RELAXED) & 1);
+}
+
+bool gemm_x6p_enabled() { return x6p_enabled(); }
+
+// returns 1 when launched on the x6p kernel (0: not eligible, <0: error)
+static int try_x6p(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
+  if (!p.bpl || (__atomic_load_n(&g_path_off, __ATOMIC_RELAXED) & 1) || (layout != GEMM_NT && layout != GEMM_NN) ||
+      p.splits != 1)
+    return 0;
+  if (epi != EPI_STORE && epi != EPI_BIAS && epi != EPI_BIAS_ELU && epi != EPI_DELU) return 0;
+  if (p.M % 64 || p.N % 128 || p.K % 16 || p.K < 32 || p.avec != 4 || p.bpl_ld != p.K) return 0;
+  if ((reinterpret_cast<uintptr_t>(p.bpl) & 15) || p.gbp % 8 || p.bpl_ps % 8) return 0;
+  // 128-row tiles when they give at least three per CU pair of workgroup slots, 64 otherwise
+  const int64_t t128 = (int64_t)(p.M / 128) * (p.N / 128) * groups;
+  const bool big = p.M % 128 == 0 && t128 >= 768;
+  const bool gat = p.a_rows != nullptr;
+  dim3 grid((unsigned)((p.M / (big ? 128 : 64)) * (p.N / 128) * groups));
+#define LRL_X6P(BMV, E)                                                                                         \
+  do {                                                                                                          \
+    if (gat) hipLaunchKernelGGL((gemm_x6p_kernel<BMV, E, true>), grid, dim3(GTHREADS), 0, st, p);              \
+    else hipLaunchKernelGGL((gemm_x6p_kernel<BMV, E, false>), grid, dim3(GTHREADS), 0, st, p);                 \
+  } while (0)
+#define LRL_X6P_E(E)      \
+  do {                    \
+    if (big) LRL_X6P(128, E); \
+    else LRL_X6P(64, E);  \
+  } while (0)
+  switch (epi) {
+    case EPI_STORE: LRL_X6P_E(EPI_STORE); break;
+    case EPI_BIAS: LRL_X6P_E(EPI_BIAS); break;
+    case EPI_BIAS_ELU: LRL_X6P_E(EPI_BIAS_ELU); break;
+    default: LRL_X6P_E(EPI_DELU); break;
+  }
+#undef LRL_X6P_E
+#undef LRL_X6P
+  return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
+}
+
+// ---- weight planes: op(B) of each job split into hi / mid / lo bf16 planes, [3][groups][n][kp] ----
+struct PlaneJobs {
+  PlaneJob j[MAX_PLANE_JOBS];
+  int64_t start[MAX_PLANE_JOBS + 1];  // first element (of one plane) of each job
+  int n;
+};
+
+__global__ __launch_bounds__(256) void x6_planes_kernel(PlaneJobs J) {
+  const int64_t total = J.start[J.n];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    int q = 0;
+    while (q + 1 < J.n && e >= J.start[q + 1]) ++q;
+    const PlaneJob& jb = J.j[q];
+    const int kp = plane_kp(jb), nn = plane_n(jb), kk = jb.trans ? jb.rows : jb.cols;
+    const int64_t t = e - J.start[q];
+    const int k = (int)(t % kp);
+    const int64_t rn = t / kp;
+    const int n = (int)(rn % nn), g = (int)(rn / nn);
+    float x = 0.f;
+    if (k < kk) x = jb.trans ? jb.W[g * jb.gsrc + (int64_t)k * jb.ldw + n] : jb.W[g * jb.gsrc + (int64_t)n * jb.ldw + k];
+    // the truncation split of x6_split2, one element
+    uint32_t u = __float_as_uint(x);
+    const uint16_t hi = (uint16_t)(u >> 16);
+    float r = x - __uint_as_float(u & 0xffff0000u);
+    u = __float_as_uint(r);
+    const uint16_t mid = (uint16_t)(u >> 16);
+    r = r - __uint_as_float(u & 0xffff0000u);
+    const uint16_t lo = (uint16_t)(__float_as_uint(r) >> 16);
+    const int64_t ps = (int64_t)jb.groups * nn * kp;
+    jb.dst[t] = hi;
+    jb.dst[ps + t] = mid;
+    jb.dst[2 * ps + t] = lo;
+  }
+}
+
+int x6_planes_launch(const PlaneJob* jobs, int n, void* stream) {
+  if (n <= 0 || n > MAX_PLANE_JOBS) return LRL_E_INVALID;
+  PlaneJobs J{};
+  J.n = n;
+  J.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    J.j[i] = jobs[i];
+    if (!jobs[i].W || !jobs[i].dst || jobs[i].rows <= 0 || jobs[i].cols <= 0 || jobs[i].groups <= 0) return LRL_E_INVALID;
+    J.start[i + 1] = J.start[i] + plane_elems(jobs[i]) / 3;
+  }
+  const int blocks = (int)std::min<int64_t>((J.start[n] + 255) / 256, 2048);
+  hipLaunchKernelGGL(x6_planes_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), J);
+  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
+}
+
 template <int BM, int BN>
 static int launch_bm(const GemmP& p, int layout, int epi, dim3 grid, hipStream_t st) {
 #define LRL_GEMM_LAUNCH(L, E) hipLaunchKernelGGL((gemm_kernel<BM, BN, L, E>), grid, dim3(GTHREADS), 0, st, p)
@@ -1400,6 +1835,9 @@ int gemm_pick_splits(int M, int N, int K, int groups) {
   return splits;
 }
 
+static thread_local int g_last_path = 0;
+int gemm_last_path() { return g_last_path; }
+
 int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) {
   GemmP p = p0;
   if (p.M <= 0 || p.N <= 0 || p.K < 0 || groups <= 0) return LRL_E_INVALID;
@@ -1417,6 +1855,16 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
   if (trace)
     fprintf(stderr, "gemm layout=%d epi=%d M=%d N=%d K=%d groups=%d splits=%d avec=%d bvec=%d arows=%d brows=%d\n",
             layout, epi, p.M, p.N, p.K, groups, p.splits, p.avec, p.bvec, p.a_rows != nullptr, p.b_rows != nullptr);
+  // weight products with a pre-split B: the LDS-DMA x6p kernel
+  g_last_path = 0;
+  if (int xr = try_x6p(p, layout, epi, groups, st)) {
+    if (xr > 0) g_last_path = 1;
+    return xr > 0 ? 0 : xr;
+  }
+  if (int xr = try_x6t(p, layout, epi, groups, st)) {
+    if (xr > 0) g_last_path = 2;
+    return xr > 0 ? 0 : xr;
+  }
   // fp32 on the bf16 MFMA (exact split, fp32-class error) wherever the tile shapes fit
   if (int xr = try_x6(p, layout, epi, groups, st)) return xr > 0 ? 0 : xr;
   // LDS-DMA path: batch-major product, every tile interior, float4-aligned operands, single split
@@ -1483,3 +1931,7 @@ int gemm_launch(const GemmP& p0, int layout, int epi, int groups, void* stream) 
 }
 
 }  // namespace lrl
+
+extern "C" int32_t lrl_debug_gemm_paths(int32_t disable_mask) {
+  return __atomic_exchange_n(&lrl::g_path_off, (int)disable_mask, __ATOMIC_RELAXED);
+}

@@ -1029,8 +1029,60 @@ struct Plan {
   float* wd1p;     // adaptation layer-1 weights at the padded history pitch (zero columns past num_hist)
   float* part;     // partial area (reused by phases 1 and 3)
   int64_t part_floats;
+  uint16_t* wpl;   // pre-split weight planes (x6p products): the caller's jobs, built once per call
   int64_t bytes;
 };
+
+// The weight products of the update that run on the x6p kernel (pre-split B, csrc/lrl_gemm.hip): their planes are
+// split from the current parameters at the start of each forward_backward / adaptation call (one launch).
+enum MainPlane { PL_W1, PL_W2, PL_W3, PL_E2, PL_W2T, PL_W3T, PL_E2T, PL_MAIN };
+enum AdaptPlane { PL_D1, PL_AE2, PL_D2T, PL_ADAPT };
+static int hist_pad(int h);
+static int xs_of(const lrl_ppo_net& n);
+// main: forward W1 (k padded to X's pitch), W2, W3, the encoder's W2; backward-data W2^T, W3^T, encoder W2^T
+static void main_plane_jobs(const lrl_ppo_net& n, const float* w, uint16_t* base, PlaneJob (&j)[PL_MAIN]) {
+  const int h0 = n.ac_h0, h1 = n.ac_h1, h2 = n.ac_h2, nx = n.num_obs + n.latent;
+  auto set = [&](PlaneJob& q, int64_t off, int rows, int cols, int64_t ldw, int trans, int groups, int64_t gsrc) {
+    q.W = w ? w + off : nullptr; q.rows = rows; q.cols = cols; q.ldw = ldw; q.trans = trans; q.groups = groups;
+    q.gsrc = gsrc;
+  };
+  set(j[PL_W1], n.w1, 2 * h0, nx, nx, 0, 1, 0);
+  set(j[PL_W2], n.w2, h1, h0, h0, 0, 2, (int64_t)h1 * h0);
+  set(j[PL_W3], n.w3, h2, h1, h1, 0, 2, (int64_t)h2 * h1);
+  set(j[PL_E2], n.e2w, n.enc_h1, n.enc_h0, n.enc_h0, 0, 1, 0);
+  set(j[PL_W2T], n.w2, h1, h0, h0, 1, 2, (int64_t)h1 * h0);
+  set(j[PL_W3T], n.w3, h2, h1, h1, 1, 2, (int64_t)h2 * h1);
+  set(j[PL_E2T], n.e2w, n.enc_h1, n.enc_h0, n.enc_h0, 1, 1, 0);
+  int64_t off = 0;
+  for (auto& q : j) {
+    q.dst = base ? base + off : nullptr;
+    off += (plane_elems(q) + 127) / 128 * 128;
+  }
+}
+// adaptation: forward Wd1 (k padded to the history pitch), the encoder-target W2 (from `we`), backward-data Wd2^T
+static void adapt_plane_jobs(const lrl_ppo_net& n, const float* w, const float* we, uint16_t* base,
+                             PlaneJob (&j)[PL_ADAPT]) {
+  auto set = [&](PlaneJob& q, const float* src, int rows, int cols, int64_t ldw, int trans) {
+    q.W = src; q.rows = rows; q.cols = cols; q.ldw = ldw; q.trans = trans; q.groups = 1; q.gsrc = 0;
+  };
+  set(j[PL_D1], w ? w + n.d1w : nullptr, n.ad_h0, n.num_hist, n.num_hist, 0);
+  set(j[PL_AE2], we ? we + n.e2w : nullptr, n.enc_h1, n.enc_h0, n.enc_h0, 0);
+  set(j[PL_D2T], w ? w + n.d2w : nullptr, n.ad_h1, n.ad_h0, n.ad_h0, 1);
+  int64_t off = 0;
+  for (auto& q : j) {
+    q.dst = base ? base + off : nullptr;
+    off += (plane_elems(q) + 127) / 128 * 128;
+  }
+}
+static int64_t plane_area_elems(const lrl_ppo_net& n) {
+  PlaneJob a[PL_MAIN], b[PL_ADAPT];
+  main_plane_jobs(n, nullptr, nullptr, a);
+  adapt_plane_jobs(n, nullptr, nullptr, nullptr, b);
+  int64_t m = 0, d = 0;
+  for (auto& q : a) m += (plane_elems(q) + 127) / 128 * 128;
+  for (auto& q : b) d += (plane_elems(q) + 127) / 128 * 128;
+  return std::max(m, d);
+}
 
 // X = [obs | latent] row pitch: 64 for the blind policies (42 + 18), else rounded up to 16 floats (a height-scan
 // policy: 235 + 18 -> 256).  Columns nx..XS-1 are zero.
@@ -1085,6 +1137,7 @@ static Plan make_plan(const lrl_ppo_net& n, int B, char* base) {
                 (int64_t)hb * (n.latent * n.ad_h1 + n.latent + 1) + 64 * 4;
   p.part_floats = std::max(ph1, ph3);
   p.part = take(p.part_floats);
+  p.wpl = reinterpret_cast<uint16_t*>(take((plane_area_elems(n) + 1) / 2));
   p.bytes = off;
   return p;
 }
@@ -1129,6 +1182,15 @@ struct G {
   hipStream_t st;
   float* part_end;  // end of the partial area: a product that would not fit is refused before launch
   int rc = 0;
+  const PlaneJob* pl = nullptr;  // pre-split B of the next nt / nn product (consumed by it)
+  G& with(const PlaneJob& j) {
+    pl = &j;
+    return *this;
+  }
+  void take_planes(GemmP& p) {
+    if (pl) gemm_use_planes(p, *pl);
+    pl = nullptr;
+  }
   void nt(const float* A, int64_t lda, const int64_t* rows, const float* W, int64_t ldw, float* C, int64_t ldc,
           const float* bias, int M, int N, int K, bool elu, int groups = 1, int64_t ga = 0, int64_t gw = 0,
           int64_t gc = 0, int64_t gbias = 0) {
@@ -1137,6 +1199,7 @@ struct G {
     p.A = A; p.lda = lda; p.a_rows = rows; p.B = W; p.ldb = ldw; p.C = C; p.ldc = ldc; p.bias = bias;
     p.M = M; p.N = N; p.K = K; p.splits = 1;
     p.ga = ga; p.gb = gw; p.gc = gc; p.gbias = gbias;
+    take_planes(p);
     rc = gemm_launch(p, GEMM_NT, elu ? EPI_BIAS_ELU : EPI_BIAS, groups, st);
   }
   // dX = dY W (* elu'(aux) if aux)
@@ -1148,6 +1211,7 @@ struct G {
     p.A = dY; p.lda = ldy; p.B = W; p.ldb = ldw; p.C = dX; p.ldc = ldx; p.aux = aux; p.ld_aux = ldaux;
     p.M = M; p.N = N; p.K = K; p.splits = 1;
     p.ga = gy; p.gb = gw; p.gc = gx; p.gaux = gaux;
+    take_planes(p);
     rc = gemm_launch(p, GEMM_NN, aux ? EPI_DELU : EPI_STORE, groups, st);
   }
   // partial dW[o][i] = sum_b dY[b][o] X[rows(b)][i]; returns the segments (weights then biases)
@@ -1243,8 +1307,15 @@ using namespace lrl;
 // rollout forward workspace: X [n][64], HE1, HE2, H1 [n][2 h0], H2, H3
 struct ActPlan {
   float *xa, *he1, *he2, *h1, *h2, *h3;
+  uint16_t* wpl;  // forward weight planes (LRL_ACT_PLANES=1: the x6p kernel for the act's weight products)
   int64_t bytes;
 };
+// the forward jobs of main_plane_jobs (PL_W1 .. PL_E2) are the act's weight products
+constexpr int PL_FWD = PL_E2 + 1;
+static bool act_planes_on() {
+  const char* e = getenv("LRL_ACT_PLANES");  // (read per call: A/B timing in one process)
+  return e && e[0] == '1' && gemm_x6p_enabled();
+}
 static ActPlan make_act_plan(const lrl_ppo_net& n, int rows, char* base) {
   ActPlan p;
   int64_t off = 0;
@@ -1260,6 +1331,13 @@ static ActPlan make_act_plan(const lrl_ppo_net& n, int rows, char* base) {
   p.h1 = take(R * 2 * n.ac_h0);
   p.h2 = take(R * 2 * n.ac_h1);
   p.h3 = take(R * 2 * n.ac_h2);
+  {
+    PlaneJob j[PL_MAIN];
+    main_plane_jobs(n, nullptr, nullptr, j);
+    int64_t e = 0;
+    for (int i = 0; i < PL_FWD; ++i) e += (plane_elems(j[i]) + 127) / 128 * 128;
+    p.wpl = reinterpret_cast<uint16_t*>(take((e + 1) / 2));
+  }
   p.bytes = off;
   return p;
 }
@@ -1350,16 +1428,24 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   G g{st, nullptr};
   const float* w = params;
   const int nx = nt.num_obs + nt.latent, XS = xs_of(nt);
+  PlaneJob pj[PL_MAIN];
+  main_plane_jobs(nt, w, P.wpl, pj);
+  if (act_planes_on()) {
+    if (int rc = x6_planes_launch(pj, PL_FWD, st)) return lrl_set_error(rc, "lrl_ppo_act: planes launch failed");
+  } else {
+    for (auto& q : pj) q.dst = nullptr;
+  }
   hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(n, XS)), dim3(256), 0, st, obs,
                      (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
   g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
-  g.nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1, nt.enc_h0, true);
+  g.with(pj[PL_E2]).nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1,
+                       nt.enc_h0, true);
   g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, false);
-  g.nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, XS, true);  // see phase 1
-  g.nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1, nt.ac_h0, true, 2,
-       nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);
-  g.nt(P.h2, 2 * nt.ac_h1, nullptr, w + nt.w3, nt.ac_h1, P.h3, 2 * nt.ac_h2, w + nt.b3, n, nt.ac_h2, nt.ac_h1, true, 2,
-       nt.ac_h1, (int64_t)nt.ac_h2 * nt.ac_h1, nt.ac_h2, nt.ac_h2);
+  g.with(pj[PL_W1]).nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, XS, true);
+  g.with(pj[PL_W2]).nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1,
+                       nt.ac_h0, true, 2, nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);
+  g.with(pj[PL_W3]).nt(P.h2, 2 * nt.ac_h1, nullptr, w + nt.w3, nt.ac_h1, P.h3, 2 * nt.ac_h2, w + nt.b3, n, nt.ac_h2,
+                       nt.ac_h1, true, 2, nt.ac_h1, (int64_t)nt.ac_h2 * nt.ac_h1, nt.ac_h2, nt.ac_h2);
   if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_act: GEMM launch failed");
   ActHeadArgs ah{};
   ah.h3 = P.h3; ah.w4a = w + nt.w4a; ah.b4a = w + nt.b4a; ah.w4c = w + nt.w4c; ah.b4c = w + nt.b4c;
@@ -1462,19 +1548,27 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   const float* w = params;
   const int nx = n.num_obs + n.latent, XS = xs_of(n);
   // ---- forward ----
+  PlaneJob pj[PL_MAIN];
+  main_plane_jobs(n, w, P.wpl, pj);
+  if (gemm_x6p_enabled()) {
+    if (int rc = x6_planes_launch(pj, PL_MAIN, st)) return lrl_set_error(rc, "lrl_ppo_forward_backward: planes launch failed");
+  } else {
+    for (auto& q : pj) q.dst = nullptr;
+  }
+  auto PJ = [&](int i) -> const PlaneJob& { return pj[i]; };
   hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(B, XS)), dim3(256), 0, st, bt->obs,
                      bt->rows, B, n.num_obs, XS, P.xa);
   g.nt(bt->priv, n.num_priv, bt->rows, w + n.e1w, n.num_priv, P.he1, n.enc_h0, w + n.e1b, B, n.enc_h0, n.num_priv, true);
-  g.nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
+  g.with(PJ(PL_E2)).nt(P.he1, n.enc_h0, nullptr, w + n.e2w, n.enc_h0, P.he2, n.enc_h1, w + n.e2b, B, n.enc_h1, n.enc_h0, true);
   g.nt(P.he2, n.enc_h1, nullptr, w + n.e3w, n.enc_h1, P.xa + n.num_obs, XS, w + n.e3b, B, n.latent, n.enc_h1, false);
   // k runs over all XS columns of X: columns nx..XS-1 are zero, so the extra products (with the next
-  // row's first weights, or the first biases after the last row — finite values) add exactly 0, and the
-  // product takes the unguarded float4 path
-  g.nt(P.xa, XS, nullptr, w + n.w1, nx, P.h1, 2 * n.ac_h0, w + n.b1, B, 2 * n.ac_h0, XS, true);
-  g.nt(P.h1, 2 * n.ac_h0, nullptr, w + n.w2, n.ac_h0, P.h2, 2 * n.ac_h1, w + n.b2, B, n.ac_h1, n.ac_h0, true, 2,
-       n.ac_h0, (int64_t)n.ac_h1 * n.ac_h0, n.ac_h1, n.ac_h1);
-  g.nt(P.h2, 2 * n.ac_h1, nullptr, w + n.w3, n.ac_h1, P.h3, 2 * n.ac_h2, w + n.b3, B, n.ac_h2, n.ac_h1, true, 2,
-       n.ac_h1, (int64_t)n.ac_h2 * n.ac_h1, n.ac_h2, n.ac_h2);
+  // row's first weights, or the first biases after the last row — finite values; zero planes on the x6p path) add
+  // exactly 0, and the product takes the unguarded float4 path
+  g.with(PJ(PL_W1)).nt(P.xa, XS, nullptr, w + n.w1, nx, P.h1, 2 * n.ac_h0, w + n.b1, B, 2 * n.ac_h0, XS, true);
+  g.with(PJ(PL_W2)).nt(P.h1, 2 * n.ac_h0, nullptr, w + n.w2, n.ac_h0, P.h2, 2 * n.ac_h1, w + n.b2, B, n.ac_h1, n.ac_h0,
+                       true, 2, n.ac_h0, (int64_t)n.ac_h1 * n.ac_h0, n.ac_h1, n.ac_h1);
+  g.with(PJ(PL_W3)).nt(P.h2, 2 * n.ac_h1, nullptr, w + n.w3, n.ac_h1, P.h3, 2 * n.ac_h2, w + n.b3, B, n.ac_h2, n.ac_h1,
+                       true, 2, n.ac_h1, (int64_t)n.ac_h2 * n.ac_h1, n.ac_h2, n.ac_h2);
   if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_forward_backward: forward GEMM launch failed");
   // ---- head ----
   SegList L{};
@@ -1507,8 +1601,8 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   // the data-gradient chain first (dH2, dH1, the latent gradient), then the encoder's chain forks to the library's
   // second stream while the actor / critic weight gradients run here; the split-k reduction joins both
   const int h0 = n.ac_h0, h1 = n.ac_h1, h2 = n.ac_h2;
-  g.nn(P.dh3, 2 * h2, w + n.w3, h1, P.dh2, 2 * h1, P.h2, 2 * h1, B, h1, h2, 2, h2, (int64_t)h2 * h1, h1, h1);
-  g.nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
+  g.with(PJ(PL_W3T)).nn(P.dh3, 2 * h2, w + n.w3, h1, P.dh2, 2 * h1, P.h2, 2 * h1, B, h1, h2, 2, h2, (int64_t)h2 * h1, h1, h1);
+  g.with(PJ(PL_W2T)).nn(P.dh2, 2 * h1, w + n.w2, h0, P.dh1, 2 * h0, P.h1, 2 * h0, B, h0, h1, 2, h1, (int64_t)h1 * h0, h0, h0);
   // d latent = dH1 [W1a; W1c][:, num_obs:]  (sum over actor and critic halves: one reduction of length 2*h0)
   g.nn(P.dh1, 2 * h0, w + n.w1 + n.num_obs, nx, P.dlat, LATS, nullptr, 0, B, n.latent, 2 * h0);
   Fork* fk = fork_for_device(st);
@@ -1520,7 +1614,7 @@ extern "C" int32_t lrl_ppo_forward_backward(const lrl_ppo_net* net, const float*
   ge.tn(P.dlat, LATS, P.he2, n.enc_h1, nullptr, n.latent, n.enc_h1, B, 1, 0, 0, part, grads + n.e3w, grads + n.e3b, L);
   ge.nn(P.dlat, LATS, w + n.e3w, n.enc_h1, P.dhe2, n.enc_h1, P.he2, n.enc_h1, B, n.enc_h1, n.latent);
   ge.tn(P.dhe2, n.enc_h1, P.he1, n.enc_h0, nullptr, n.enc_h1, n.enc_h0, B, 1, 0, 0, part, grads + n.e2w, grads + n.e2b, L);
-  ge.nn(P.dhe2, n.enc_h1, w + n.e2w, n.enc_h0, P.dhe1, n.enc_h0, P.he1, n.enc_h0, B, n.enc_h0, n.enc_h1);
+  ge.with(PJ(PL_E2T)).nn(P.dhe2, n.enc_h1, w + n.e2w, n.enc_h0, P.dhe1, n.enc_h0, P.he1, n.enc_h0, B, n.enc_h0, n.enc_h1);
   ge.tn(P.dhe1, n.enc_h0, bt->priv, n.num_priv, bt->rows, n.enc_h0, n.num_priv, B, 1, 0, 0, part, grads + n.e1w,
         grads + n.e1b, L);
   if (fk && hipEventRecord(fk->done, fk->st) != hipSuccess)
@@ -1578,8 +1672,15 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
   // target = env_factor_encoder(priv) with the just-updated weights (torch.no_grad, ppo.py:159-160), read from
   // enc_params (a snapshot of them taken right after the optimiser step, so the next step may proceed) or params
   const float* we = enc_params ? enc_params : params;
+  PlaneJob pj[PL_ADAPT];
+  adapt_plane_jobs(n, w, we, P.wpl, pj);
+  if (gemm_x6p_enabled()) {
+    if (int rc = x6_planes_launch(pj, PL_ADAPT, st)) return lrl_set_error(rc, "lrl_ppo_adaptation: planes launch failed");
+  } else {
+    for (auto& q : pj) q.dst = nullptr;
+  }
   g.nt(bt->priv, n.num_priv, bt->rows, we + n.e1w, n.num_priv, P.he1, n.enc_h0, we + n.e1b, B, n.enc_h0, n.num_priv, true);
-  g.nt(P.he1, n.enc_h0, nullptr, we + n.e2w, n.enc_h0, P.he2, n.enc_h1, we + n.e2b, B, n.enc_h1, n.enc_h0, true);
+  g.with(pj[PL_AE2]).nt(P.he1, n.enc_h0, nullptr, we + n.e2w, n.enc_h0, P.he2, n.enc_h1, we + n.e2b, B, n.enc_h1, n.enc_h0, true);
   g.nt(P.he2, n.enc_h1, nullptr, we + n.e3w, n.enc_h1, P.tgt, LATS, we + n.e3b, B, n.latent, n.enc_h1, false);
   // prediction = adaptation_module(obs_history)
   const int hld = bt->hist_ld ? bt->hist_ld : n.num_hist, hpad = hist_pad(n.num_hist);
@@ -1589,7 +1690,7 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
     const int64_t cnt = (int64_t)n.ad_h0 * hpad;
     hipLaunchKernelGGL(pad_cols_kernel, dim3((unsigned)std::min<int64_t>((cnt + 255) / 256, 1024)), dim3(256), 0, st,
                        w + n.d1w, n.ad_h0, n.num_hist, hpad, P.wd1p);
-    g.nt(bt->hist, hld, bt->rows, P.wd1p, hpad, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, hpad, true);
+    g.with(pj[PL_D1]).nt(bt->hist, hld, bt->rows, P.wd1p, hpad, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, hpad, true);
   } else {
     g.nt(bt->hist, hld, bt->rows, w + n.d1w, n.num_hist, P.hd1, n.ad_h0, w + n.d1b, B, n.ad_h0, n.num_hist, true);
   }
@@ -1614,7 +1715,7 @@ extern "C" int32_t lrl_ppo_adaptation_forward_backward(const lrl_ppo_net* net, c
     part += ((hb * pl + 63) / 64) * 64;
   }
   g.tn(P.dhd2, HD2S, P.hd1, n.ad_h0, nullptr, n.ad_h1, n.ad_h0, B, 1, 0, 0, part, grads + n.d2w, grads + n.d2b, L);
-  g.nn(P.dhd2, HD2S, w + n.d2w, n.ad_h0, P.dhd1, n.ad_h0, P.hd1, n.ad_h0, B, n.ad_h0, n.ad_h1);
+  g.with(pj[PL_D2T]).nn(P.dhd2, HD2S, w + n.d2w, n.ad_h0, P.dhd1, n.ad_h0, P.hd1, n.ad_h0, B, n.ad_h0, n.ad_h1);
   g.tn(P.dhd1, n.ad_h0, bt->hist, hld, bt->rows, n.ad_h0, n.num_hist, B, 1, 0, 0, part, grads + n.d1w,
        grads + n.d1b, L);
   if (g.rc) return lrl_set_error(g.rc, "lrl_ppo_adaptation: backward GEMM launch failed");
@@ -1672,6 +1773,22 @@ extern "C" int32_t lrl_gemm_f32(int32_t layout, int32_t epi, int32_t M, int32_t 
     return hipGetLastError() == hipSuccess ? 0 : lrl_set_error(LRL_E_HIP, "lrl_gemm_f32: launch failed");
   }
   p.a_rows = rows;
+  if (layout & 0x100) {
+    // pre-split B: planes of op(B) built in the workspace, then the x6p kernel (and nothing else) runs the product
+    layout &= 0xff;
+    if (layout != GEMM_NT && layout != GEMM_NN) return lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: planes need NT / NN");
+    PlaneJob j{};
+    j.W = B; j.ldw = ldb; j.gsrc = 0; j.groups = 1; j.trans = layout == GEMM_NN ? 1 : 0;
+    j.rows = layout == GEMM_NN ? K : N; j.cols = layout == GEMM_NN ? N : K;
+    j.dst = reinterpret_cast<uint16_t*>(workspace);
+    if (!workspace || plane_elems(j) > 2 * workspace_floats)
+      return lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: workspace too small for the planes");
+    if (int rc = x6_planes_launch(&j, 1, st)) return lrl_set_error(rc, "lrl_gemm_f32: planes launch failed");
+    gemm_use_planes(p, j);
+    int rc = gemm_launch(p, layout, epi, 1, st);
+    if (rc) return lrl_set_error(rc, "lrl_gemm_f32: launch failure");
+    return gemm_last_path() == 1 ? 0 : lrl_set_error(LRL_E_INVALID, "lrl_gemm_f32: shape not eligible for the x6p kernel");
+  }
   int rc = gemm_launch(p, layout, epi, 1, st);
   return rc ? lrl_set_error(rc, "lrl_gemm_f32: bad layout/epilogue or launch failure") : 0;
 }

@@ -136,3 +136,50 @@ def test_x6_error_is_fp32_class(layout, M, N, K):
         assert ((db.double() - dY.double().sum(0)).abs() / dY.double().abs().sum(0)).max().item() <= 1e-6
     rel = ((out.double() - ref).abs() / mag).max().item()
     assert rel <= 1e-6, rel
+
+
+@pytest.mark.parametrize("layout,epi,M,N,K,gather", [(0, 2, 24576, 256, 512, False), (0, 2, 4096, 1024, 64, False),
+                                                     (0, 1, 1024, 128, 256, False), (0, 2, 2048, 256, 640, True),
+                                                     (0, 0, 192, 384, 48, False), (2, 3, 24576, 512, 256, False),
+                                                     (2, 3, 1024, 256, 32, False), (2, 0, 640, 256, 128, False)])
+def test_pre_split_weight_kernel_is_bit_identical(layout, epi, M, N, K, gather):
+    """The LDS-DMA pre-split-B kernel (gemm_x6p_kernel: weights split into bf16 planes once, layout | 0x100) gives the
+    same bits as gemm_x6_kernel (fp32 B split while staging): same split, same six products in the same k order."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K + epi)
+    src = torch.randn(M + 50 if gather else M, K, device=dev, generator=g)
+    rows = torch.randperm(M + 50, device=dev, generator=g)[:M].contiguous() if gather else None
+    W = torch.randn(N, K, device=dev, generator=g) if layout == 0 else torch.randn(K, N, device=dev, generator=g)
+    ldb = K if layout == 0 else N
+    bias = torch.randn(N, device=dev, generator=g)
+    aux = torch.randn(M, N, device=dev, generator=g) if epi == 3 else None
+    ws = torch.empty(3 * N * ((K + 15) // 16 * 16), device=dev)
+    c0, c1 = torch.empty(M, N, device=dev), torch.full((M, N), float("nan"), device=dev)
+    _gemm(layout, epi, M, N, K, src, K, W, ldb, c0, N, bias=bias, aux=aux, ld_aux=N, rows=rows)
+    _gemm(layout | 0x100, epi, M, N, K, src, K, W, ldb, c1, N, bias=bias, aux=aux, ld_aux=N, rows=rows, ws=ws)
+    assert torch.equal(c0, c1), (c0 - c1).abs().max().item()
+
+
+@pytest.mark.parametrize("M,N,K,groups_rows", [(256, 512, 24576, 0), (128, 256, 24576, 0), (128, 128, 4096, 0),
+                                               (256, 256, 3000 * 16, 0)])
+def test_lds_dma_weight_gradient_is_bit_identical(M, N, K, groups_rows):
+    """The LDS-DMA weight-gradient kernel (gemm_x6t_kernel) against gemm_x6_kernel (lrl_debug_gemm_paths(2) turns it
+    off): the split-k partials and the bias-gradient partials, hence the reduced dW / db, are bit-identical."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    dY = torch.randn(K, M, device=dev, generator=g)
+    X = torch.randn(K, N, device=dev, generator=g)
+    ws = torch.empty(256 * (M * N + M), device=dev)
+    outs = []
+    lib = _abi.lib()
+    for mask in (2, 0):
+        prev = lib.lrl_debug_gemm_paths(C.c_int32(mask))
+        try:
+            out, db = torch.empty(M, N, device=dev), torch.empty(M, device=dev)
+            _gemm(3, 4, M, N, K, dY, M, X, N, out, N, bias=db, ws=ws)
+            outs.append((out, db))
+        finally:
+            lib.lrl_debug_gemm_paths(C.c_int32(prev))
+    assert torch.equal(outs[0][0], outs[1][0]), (outs[0][0] - outs[1][0]).abs().max().item()
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = dY.double().T @ X.double()
+    mag = dY.double().abs().T @ X.double().abs()
+    assert ((outs[1][0].double() - ref).abs() / mag).max().item() <= 1e-6

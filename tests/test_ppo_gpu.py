@@ -106,6 +106,27 @@ def test_one_launch_act_matches_gemm_chain(n, no, monkeypatch):
     assert torch.equal(sl.flatten(), lp.flatten())
 
 
+@pytest.mark.parametrize("n", [4096, 1000])
+def test_act_with_weight_planes_is_bit_identical(n, monkeypatch):
+    """The act's GEMM chain with its weight products on the pre-split-planes kernel (LRL_ACT_PLANES=1, gemm_x6p_kernel
+    where the shapes fit) gives the same bits as without (gemm_x6_kernel): actions, means, values, log-probs."""
+    from lrl.ppo.actor_critic import ActorCritic
+    monkeypatch.setenv("LRL_ACT_FUSED", "0")
+    ac = ActorCritic(42, 18, 630, 12).cuda()
+    init_params(ac)
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    obs = torch.randn(n, 42, device="cuda:0", generator=g)
+    priv = torch.randn(n, 18, device="cuda:0", generator=g)
+    outs = []
+    for planes in ("1", "0"):
+        monkeypatch.setenv("LRL_ACT_PLANES", planes)
+        res = ac.act_fused(obs, priv, seed=3, counter=2)
+        torch.cuda.synchronize()
+        outs.append([r.clone() for r in res])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
 def test_fused_policy_sampling_statistics():
     """Counter-RNG Box-Muller sampling: actions - mu ~ N(0, std^2)."""
     from lrl.ppo.actor_critic import ActorCritic
