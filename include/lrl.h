@@ -542,8 +542,10 @@ int32_t lrl_ppo_adaptation_step(const lrl_ppo_net* net, float* params, const flo
 int32_t lrl_ppo_timing(int32_t enable, double* total_ms, int64_t* launches);
 
 /* Development switch of the update's GEMM kernels (tests compare them in one process): bit 0 set = no pre-split-B
- * kernel for the weight products, bit 1 set = no LDS-DMA weight-gradient kernel; the fp32-staged x6 kernel takes
- * those products instead.  Returns the previous mask. */
+ * kernel for the weight products, bit 1 set = no LDS-DMA weight-gradient kernel, bit 2 set = no LDS-DMA
+ * forward / backward-data kernel (the fp32-staged x6 kernel takes those products instead); bit 3 set (bit 2 clear) =
+ * the LDS-DMA kernel for every forward / backward-data product it fits (it is off by default).  Returns the previous
+ * mask. */
 int32_t lrl_debug_gemm_paths(int32_t disable_mask);
 
 /* Test entry point of the GEMM the update is built from: C = op(A) op(B) with

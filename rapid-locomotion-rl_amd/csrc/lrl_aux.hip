@@ -253,32 +253,37 @@ __global__ void rigid_body_kernel(const KParams* __restrict__ K, KState S, const
 // rows of n floats (lrl.h LRL_EXTRAS_*): dof_pos, dof_vel, joint_pos_target (12 each), base_lin_vel, base_ang_vel (3),
 // commands (4), contact states of the feet (contact force z > 1: 1 / 0), foot positions (4 x 3, the rigid-body state's
 // feet), root position (3), torques (12).  Coalesced: thread e reads row r of every SoA field at word e.
-__global__ void extras_snapshot_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ body_leg,
-                                       const int32_t* __restrict__ body_link, const float* __restrict__ foot_xyz,
-                                       float* __restrict__ out) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
+// four threads per env (wave-uniform quarter q = threadIdx.x / 64, 64 consecutive envs per wave: every store row is
+// coalesced): the plain rows split over the quarters, foot q's forward kinematics on quarter q
+__global__ __launch_bounds__(256) void extras_snapshot_kernel(const KParams* __restrict__ K, KState S,
+                                                              const int32_t* __restrict__ body_leg,
+                                                              const int32_t* __restrict__ body_link,
+                                                              const float* __restrict__ foot_xyz, float* __restrict__ out) {
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
   if (e >= S.n) return;
   const int N = S.stride, n = S.n;
   const lrl_env_params& P = K->p;
-  int r = 0;
-  auto put = [&](float v) { out[(int64_t)(r++) * n + e] = v; };
-  for (int k = 0; k < 12; ++k) put(S.dof_pos[k * N + e]);
-  for (int k = 0; k < 12; ++k) put(S.dof_vel[k * N + e]);
-  for (int k = 0; k < 12; ++k) put(S.joint_pos_target[k * N + e]);
-  for (int k = 0; k < 3; ++k) put(S.base_lin_vel[k * N + e]);
-  for (int k = 0; k < 3; ++k) put(S.base_ang_vel[k * N + e]);
-  for (int k = 0; k < 4; ++k) put(S.commands[k * N + e]);
-  for (int f = 0; f < LRL_NUM_LEGS; ++f)
-    put(f < P.num_feet && S.contact[(P.feet[f] * 3 + 2) * N + e] > 1.f ? 1.f : 0.f);
+  // rows: dof_pos 0-11, dof_vel 12-23, joint_pos_target 24-35, base lin / ang vel 36-41, commands 42-45,
+  // foot contacts 46-49, foot positions 50-61, base position 62-64, torques 65-76
+  auto put = [&](int r, float v) { out[(int64_t)r * n + e] = v; };
+  for (int k = q; k < 12; k += 4) {
+    put(k, S.dof_pos[k * N + e]);
+    put(12 + k, S.dof_vel[k * N + e]);
+    put(24 + k, S.joint_pos_target[k * N + e]);
+    put(65 + k, S.torques[k * N + e]);
+  }
+  if (q < 3) {
+    put(36 + q, S.base_lin_vel[q * N + e]);
+    put(39 + q, S.base_ang_vel[q * N + e]);
+  }
+  put(42 + q, S.commands[q * N + e]);
+  put(46 + q, q < P.num_feet && S.contact[(P.feet[q] * 3 + 2) * N + e] > 1.f ? 1.f : 0.f);
   float R[9], p[3], vo[3], W[3];
   base_pose(S, e, R, p, vo, W);
-  for (int f = 0; f < LRL_NUM_LEGS; ++f) {
-    float Rb[9], ob[3] = {0.f, 0.f, 0.f}, vb[3], wb[3];
-    if (f < P.num_feet) body_fk(K, S, e, body_leg[P.feet[f]], body_link[P.feet[f]], foot_xyz, R, p, vo, W, Rb, ob, vb, wb);
-    for (int k = 0; k < 3; ++k) put(ob[k]);
-  }
-  for (int k = 0; k < 3; ++k) put(p[k]);
-  for (int k = 0; k < 12; ++k) put(S.torques[k * N + e]);
+  if (q < 3) put(62 + q, p[q]);
+  float Rb[9], ob[3] = {0.f, 0.f, 0.f}, vb[3], wb[3];
+  if (q < P.num_feet) body_fk(K, S, e, body_leg[P.feet[q]], body_link[P.feet[q]], foot_xyz, R, p, vo, W, Rb, ob, vb, wb);
+  for (int k = 0; k < 3; ++k) put(50 + 3 * q + k, ob[k]);
 }
 
 // HistoryWrapper.get_observations shift: hist = cat(hist[:, NO:], obs)  (history_wrapper.py:26-30)
@@ -487,7 +492,8 @@ hipError_t lrl_launch_rigid_body(const KParams* K, const KState* S, const int32_
 }
 hipError_t lrl_launch_extras_snapshot(const KParams* K, const KState* S, const int32_t* body_leg, const int32_t* body_link,
                                       const float* foot_xyz, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(lrl::extras_snapshot_kernel, dim3((S->n + 63) / 64), dim3(64), 0, st, K, *S, body_leg,
+  static_assert(LRL_NUM_LEGS == 4, "one quarter-thread per foot");
+  hipLaunchKernelGGL(lrl::extras_snapshot_kernel, dim3((S->n + 63) / 64), dim3(256), 0, st, K, *S, body_leg,
                      body_link, foot_xyz, out);
   return hipGetLastError();
 }

@@ -1285,6 +1285,8 @@ static bool x6_enabled() {
   return on != 0;
 }
 
+static int try_x6d(const GemmP& p, int layout, int epi, int groups, int bm, int bn, hipStream_t st);
+
 // returns 1 when the product was launched on the x6 kernel (0: not eligible, <0: error)
 static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
   if (!x6_enabled()) return 0;
@@ -1319,6 +1321,8 @@ static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t s
     // 128-row tiles when they still give two workgroups per CU, 64 otherwise
     const int64_t wg128 = (int64_t)((p.M + 127) / 128) * ((p.N + bn - 1) / bn) * groups;
     const int bm = wg128 >= 512 ? 128 : 64;
+    // the same tile on the LDS-DMA kernel where the tiles are interior
+    if (int dr = try_x6d(p, layout, epi, groups, bm, bn, st)) return dr;
     if (bm == 128 && bn == 128) rc = launch_x6_tile<128, 128>(p, layout, epi, groups, st);
     else if (bm == 128) rc = launch_x6_tile<128, 64>(p, layout, epi, groups, st);
     else if (bn == 128) rc = launch_x6_tile<64, 128>(p, layout, epi, groups, st);
@@ -1497,13 +1501,15 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6p_kernel(GemmP p) {
 // 8 k-values per MFMA operand with ds_read_b32 (immediate offsets) and splits them in registers.  128 x 128 tiles,
 // 4 waves of 2 x 2 MFMA tiles, the six products in gemm_x6_kernel's order over the same k order, and the bias
 // gradient partial summed in its (row, k-half) order: bit-identical to it.
-template <int TAG>
+constexpr int X6T_MAX_GATHER_KPS = 1024;  // gathered-B splits of at most this many rows (the row list in LDS)
+template <int TAG, bool BGATHER>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
   constexpr int BM = 128, BN = 128, NST = 3, TM = 2, TN = 2;
   constexpr int IMG = 16 * 128 * 4, STB = 2 * IMG;  // bytes: A image then B image
   constexpr int NPW = 4;                            // DMA wave-instructions per wave and stage (2 per operand)
-  __shared__ __attribute__((aligned(16))) uint8_t S[NST * STB];
-  const int mt = p.M / BM, nt = p.N / BN;
+  constexpr int XROWS = BGATHER ? X6T_MAX_GATHER_KPS : 0;  // gathered B: the split's row list (int32) after the ring
+  __shared__ __attribute__((aligned(16))) uint8_t S[NST * STB + 4 * XROWS];
+  const int mt = p.M / BM, nt = (p.N + BN - 1) / BN;  // (ragged n: see try_x6t)
   int L;
   {
     const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
@@ -1522,11 +1528,19 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
   // this lane's DMA sources: k-row 2 (2w + d) + lane / 32, slot lane % 32 (source chunk pre-swizzled)
   const float* asrc[2];
   const float* bsrc[2];
+  int bkr[2];
+  int* xrows = reinterpret_cast<int*>(S + NST * STB);
+  if constexpr (BGATHER) {
+    // the split's B row list into LDS before the ring starts (no DMA in flight: a plain barrier is safe)
+    for (int t = threadIdx.x; t < kend - kbeg; t += GTHREADS) xrows[t] = (int)p.b_rows[kbeg + t];
+    __syncthreads();
+  }
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
     const int kr = 2 * (2 * w + d) + (lane >> 5), ch = (lane & 31) ^ (8 * ((kr >> 3) & 1));
     asrc[d] = A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * ch;
-    bsrc[d] = Bm + (int64_t)(kbeg + kr) * p.ldb + n0 + 4 * ch;
+    bsrc[d] = BGATHER ? Bm + n0 + 4 * ch : Bm + (int64_t)(kbeg + kr) * p.ldb + n0 + 4 * ch;
+    bkr[d] = kr;
   }
   const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
   auto dma = [&](const void* src, uint32_t lds_off) {
@@ -1542,7 +1556,10 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
 #pragma unroll
     for (int d = 0; d < 2; ++d) dma(asrc[d] + ka, __builtin_amdgcn_readfirstlane(base + (2 * w + d) * 1024));
 #pragma unroll
-    for (int d = 0; d < 2; ++d) dma(bsrc[d] + kb, __builtin_amdgcn_readfirstlane(base + IMG + (2 * w + d) * 1024));
+    for (int d = 0; d < 2; ++d) {
+      const float* bs = BGATHER ? bsrc[d] + (int64_t)xrows[16 * s + bkr[d]] * p.ldb : bsrc[d] + kb;
+      dma(bs, __builtin_amdgcn_readfirstlane(base + IMG + (2 * w + d) * 1024));
+    }
   };
   const bool do_bsum = p.bias_part != nullptr && tn_ == 0 && wn == 0;
   float bsum[TM] = {0.f, 0.f};
@@ -1611,6 +1628,7 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn + 32 * j + li;
+    if (col >= p.N) continue;  // (ragged n: the DMA read the row pitch's padding columns, which no output keeps)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1639,8 +1657,242 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
   }
 }
 
-// run-time path mask (lrl_debug_gemm_paths: tests compare the paths in one process): bit 0 off = no x6p, bit 1 = no x6t
+// run-time path mask (lrl_debug_gemm_paths: tests compare the paths in one process): bit 0 off = no x6p, bit 1 = no x6t,
+// bit 2 = no x6d, bit 3 = x6d on (NT and NN) unless bit 2
 static int g_path_off = 0;
+
+// ---------------------------------------------------------------------------------------------------
+// x6 forward / backward-data with LDS-DMA staging ("x6d", NT / NN, fp32 operands): gemm_x6t_kernel's structure for
+// the batch-major products.  Both operands land fp32 by LDS-DMA in a 3-deep ring of 16-k stages (counted vmcnt, raw
+// barrier, two stages in flight across it); each lane reads its 8 k-values per MFMA operand and splits them in
+// registers.  k-contiguous operands (A; B of NT): [R][16] images (64-B rows, 16-B chunk c of row r in slot
+// c ^ ((r >> 2) & 3)), read with two ds_read_b128; the n-contiguous B of NN: [16][BN] (chunk c of k-row k in slot
+// c ^ (8 * ((k >> 3) & 1))), read with ds_read_b32.  Tile shapes as gemm_x6_kernel picks them; the six products in
+// its order over the same k order: bit-identical to it.
+template <int BM, int BN, int LAYOUT, int EPI, bool GATHER>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_x6d_kernel(GemmP p) {
+  constexpr bool BNC = LAYOUT == GEMM_NN;
+  constexpr int NST = 3, TM = BM / 64, TN = BN / 64;
+  constexpr int AIMG = BM * 64, BIMG = BN * 64, STB = AIMG + BIMG;  // bytes
+  constexpr int NAI = BM / 16, NBI = BN / 16, NPW = (NAI + NBI) / 4;  // DMA wave-instructions (per stage; per wave)
+  static_assert((NAI + NBI) % 4 == 0 && NPW >= 2 && NPW <= 4, "DMA split");
+  __shared__ __attribute__((aligned(16))) uint8_t S[NST * STB];
+  const int mt = p.M / BM, nt = p.N / BN;
+  int L;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  const int tn_ = L % nt, tm_ = (L / nt) % mt, g = L / (nt * mt);
+  const int m0 = tm_ * BM, n0 = tn_ * BN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ Bm = p.B + g * p.gb;
+  // this wave's DMA pieces j = NPW w + d: A image pieces first (16 rows each), then B's (16 rows, or 1024 / (4 BN)
+  // k-rows of the NN image); the LDS destination of piece j is j KiB into the stage
+  const float* src[NPW];
+  int64_t kstep[NPW];
+#pragma unroll
+  for (int d = 0; d < NPW; ++d) {
+    const int j = NPW * w + d;
+    if (j < NAI) {
+      const int r = 16 * j + (lane >> 2), ch = (lane & 3) ^ ((r >> 2) & 3);
+      src[d] = A + (GATHER ? p.a_rows[m0 + r] : (int64_t)(m0 + r)) * p.lda + 4 * ch;
+      kstep[d] = 16;
+    } else if (!BNC) {
+      const int r = 16 * (j - NAI) + (lane >> 2), ch = (lane & 3) ^ ((r >> 2) & 3);
+      src[d] = Bm + (int64_t)(n0 + r) * p.ldb + 4 * ch;
+      kstep[d] = 16;
+    } else {
+      constexpr int KPP = 256 / BN;  // k-rows per piece
+      const int kr = KPP * (j - NAI) + lane / (BN / 4), c = lane % (BN / 4), ch = c ^ (8 * ((kr >> 3) & 1));
+      src[d] = Bm + (int64_t)kr * p.ldb + n0 + 4 * ch;
+      kstep[d] = 16 * p.ldb;
+    }
+  }
+  const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
+  auto dma = [&](const void* s, uint32_t lds_off) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(s), "s"(lds_off)
+                 : "memory");
+  };
+  auto issue = [&](int st, int s) {
+    const uint32_t base = s_lds + (uint32_t)(st * STB);
+#pragma unroll
+    for (int d = 0; d < NPW; ++d)
+      dma(src[d] + s * kstep[d], __builtin_amdgcn_readfirstlane(base + (NPW * w + d) * 1024));
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto split8 = [&](const float (&v)[8], bf16x8_t (&o)[3]) {
+    uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x6_split2(v[2 * e], v[2 * e + 1], hh[e], mm[e], ll[e]);
+    uint4 vh = make_uint4(hh[0], hh[1], hh[2], hh[3]), vm = make_uint4(mm[0], mm[1], mm[2], mm[3]),
+          vl = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+    o[0] = *reinterpret_cast<bf16x8_t*>(&vh);
+    o[1] = *reinterpret_cast<bf16x8_t*>(&vm);
+    o[2] = *reinterpret_cast<bf16x8_t*>(&vl);
+  };
+  // k-contiguous image: row r's k-values 8h .. 8h+7
+  auto read_kc = [&](const uint8_t* img, int r, float (&v)[8]) {
+    const int sw = (r >> 2) & 3;
+    const float4 x0 = *reinterpret_cast<const float4*>(img + r * 64 + 16 * ((2 * h) ^ sw));
+    const float4 x1 = *reinterpret_cast<const float4*>(img + r * 64 + 16 * ((2 * h + 1) ^ sw));
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+  };
+
+  const int ns = p.K / 16;
+  issue(0, 0);
+  if (ns > 1) issue(1, 1);
+  for (int s = 0; s < ns; ++s) {
+    if (s + 1 < ns) {
+      if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (NPW == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < ns) issue((s + 2) % NST, s + 2);
+    const uint8_t* As = S + (s % NST) * STB;
+    const uint8_t* Bs = As + AIMG;
+    bf16x8_t a[TM][3], b[TN][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float v[8];
+      read_kc(As, wm + 32 * i + li, v);
+      split8(v, a[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float v[8];
+      if constexpr (!BNC) {
+        read_kc(Bs, wn + 32 * j + li, v);
+      } else {
+        const float* img = reinterpret_cast<const float*>(Bs) + 8 * h * BN + ((wn + 32 * j + li) ^ (32 * h));
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = img[BN * t];
+      }
+      split8(v, b[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+  }
+
+  float* __restrict__ C = p.C + g * p.gc;
+  const float* __restrict__ bias = p.bias ? p.bias + g * p.gbias : nullptr;
+  const float* __restrict__ ax = EPI == EPI_DELU ? p.aux + g * p.gaux : nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn + 32 * j + li;
+    float bj = 0.f;
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = bias[col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row0 = m0 + wm + 32 * i + 8 * q + 4 * h;
+        float* __restrict__ crow = C + (int64_t)row0 * p.ldc + col;
+        float xa[4];
+        if constexpr (EPI == EPI_DELU) {
+          const float* __restrict__ xrow = ax + (int64_t)row0 * p.ld_aux + col;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xa[r] = xrow[r * p.ld_aux];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][4 * q + r];
+          if (EPI == EPI_BIAS) v += bj;
+          if (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+          if constexpr (EPI == EPI_DELU) {
+            const float x = xa[r];
+            v = x > 0.f ? v : v * (x + 1.f);
+          }
+          crow[r * p.ldc] = v;
+        }
+      }
+  }
+}
+
+template <int BM, int BN, int LAYOUT>
+static void launch_x6d_l(const GemmP& p, int epi, int groups, hipStream_t st) {
+  dim3 grid((unsigned)((p.M / BM) * (p.N / BN) * groups));
+  const bool gat = p.a_rows != nullptr;
+#define LRL_X6D(E)                                                                                             \
+  do {                                                                                                         \
+    if (gat) hipLaunchKernelGGL((gemm_x6d_kernel<BM, BN, LAYOUT, E, true>), grid, dim3(GTHREADS), 0, st, p);   \
+    else hipLaunchKernelGGL((gemm_x6d_kernel<BM, BN, LAYOUT, E, false>), grid, dim3(GTHREADS), 0, st, p);      \
+  } while (0)
+  if (LAYOUT == GEMM_NT) {
+    if (epi == EPI_STORE) LRL_X6D(EPI_STORE);
+    else if (epi == EPI_BIAS) LRL_X6D(EPI_BIAS);
+    else LRL_X6D(EPI_BIAS_ELU);
+  } else {
+    if (epi == EPI_STORE) LRL_X6D(EPI_STORE);
+    else LRL_X6D(EPI_DELU);
+  }
+#undef LRL_X6D
+}
+
+// x6d path switch, off by default: measured 1.00-1.05x gemm_x6_kernel on the backward-data products in isolation but
+// slower inside the update (79 against 68 us for the 2-group dH1, profiles/r4o_kernel_stats.csv), and 0.79-0.97x on
+// the forward ones, whose float4-staged operands gemm_x6_kernel splits once per workgroup instead of once per reading
+// wave (profiles/r4n_x6d_vs_x6.jsonl).  LRL_GEMM_X6D=1: the backward-data products, =2: the forward too
+static int x6d_mode() {
+  static const int m = [] {
+    const char* e = getenv("LRL_GEMM_X6D");
+    return e ? atoi(e) : 0;
+  }();
+  const int off = __atomic_load_n(&g_path_off, __ATOMIC_RELAXED);
+  return (off & 4) ? 0 : (off & 8) ? 2 : m;
+}
+static bool x6d_enabled() { return x6d_mode() != 0; }
+
+// returns 1 when launched on the x6d kernel (0: not eligible, <0: error); bm / bn: the tile gemm_x6_kernel would take
+static int try_x6d(const GemmP& p, int layout, int epi, int groups, int bm, int bn, hipStream_t st) {
+  if (!x6d_enabled() || (layout != GEMM_NT && layout != GEMM_NN) || p.splits != 1) return 0;
+  if (layout == GEMM_NT && x6d_mode() != 2) return 0;
+  if (layout == GEMM_NT && epi != EPI_STORE && epi != EPI_BIAS && epi != EPI_BIAS_ELU) return 0;
+  if (layout == GEMM_NN && epi != EPI_STORE && epi != EPI_DELU) return 0;
+  if (p.M % bm || p.N % bn || p.K % 16 || p.K < 32 || p.avec != 4 || p.bvec != 4) return 0;
+  if (layout == GEMM_NN && p.b_rows) return 0;
+  const int key = (bm == 128 ? 2 : 0) | (bn == 128 ? 1 : 0) | (layout == GEMM_NN ? 4 : 0);
+  switch (key) {
+    case 0: launch_x6d_l<64, 64, GEMM_NT>(p, epi, groups, st); break;
+    case 1: launch_x6d_l<64, 128, GEMM_NT>(p, epi, groups, st); break;
+    case 2: launch_x6d_l<128, 64, GEMM_NT>(p, epi, groups, st); break;
+    case 3: launch_x6d_l<128, 128, GEMM_NT>(p, epi, groups, st); break;
+    case 4: launch_x6d_l<64, 64, GEMM_NN>(p, epi, groups, st); break;
+    case 5: launch_x6d_l<64, 128, GEMM_NN>(p, epi, groups, st); break;
+    case 6: launch_x6d_l<128, 64, GEMM_NN>(p, epi, groups, st); break;
+    default: launch_x6d_l<128, 128, GEMM_NN>(p, epi, groups, st); break;
+  }
+  return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
+}
 // x6t path switch: LRL_GEMM_X6T=0 keeps the weight gradients on gemm_x6_kernel
 static bool x6t_enabled() {
   static const int on = [] {
@@ -1650,17 +1902,25 @@ static bool x6t_enabled() {
   return on != 0 && !(__atomic_load_n(&g_path_off, __ATOMIC_RELAXED) & 2);
 }
 
-// returns 1 when launched on the x6t kernel (0: not eligible, <0: error)
+// returns 1 when launched on the x6t kernel (0: not eligible, <0: error).  n may be ragged when B's row pitch covers
+// the last tile (the DMA reads whole 128-wide tiles); a gathered B keeps its split's row list in LDS
 static int try_x6t(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
-  if (!x6t_enabled() || layout != GEMM_TN || epi != EPI_PARTIAL || p.b_rows) return 0;
-  if (p.M % 128 || p.N % 128 || p.K % 16 || p.kps % 16 || p.kps < 16 || p.avec != 4 || p.bvec != 4) return 0;
+  if (!x6t_enabled() || layout != GEMM_TN || epi != EPI_PARTIAL) return 0;
+  const int nt = (p.N + 127) / 128;
+  if (p.M % 128 || p.K % 16 || p.kps % 16 || p.kps < 16 || p.avec != 4 || p.bvec != 4) return 0;
+  if ((int64_t)nt * 128 > p.ldb) return 0;
+  if (p.b_rows && p.kps > X6T_MAX_GATHER_KPS) return 0;
   if ((int64_t)(p.splits - 1) * p.kps >= p.K) return 0;  // (every split has a non-empty range)
-  dim3 grid((unsigned)((p.M / 128) * (p.N / 128) * groups * p.splits));
+  dim3 grid((unsigned)((p.M / 128) * nt * groups * p.splits));  // (stores stop at p.N)
+  if (p.b_rows) {
+    hipLaunchKernelGGL((gemm_x6t_kernel<4, true>), grid, dim3(GTHREADS), 0, st, p);
+    return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
+  }
   switch (tn_shape_tag(p.M, p.N, groups)) {
-    case 1: hipLaunchKernelGGL((gemm_x6t_kernel<1>), grid, dim3(GTHREADS), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((gemm_x6t_kernel<2>), grid, dim3(GTHREADS), 0, st, p); break;
-    case 6: hipLaunchKernelGGL((gemm_x6t_kernel<6>), grid, dim3(GTHREADS), 0, st, p); break;
-    default: hipLaunchKernelGGL((gemm_x6t_kernel<0>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((gemm_x6t_kernel<1, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm_x6t_kernel<2, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((gemm_x6t_kernel<6, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x6t_kernel<0, false>), grid, dim3(GTHREADS), 0, st, p); break;
   }
   return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
 }

@@ -159,14 +159,19 @@ def test_pre_split_weight_kernel_is_bit_identical(layout, epi, M, N, K, gather):
     assert torch.equal(c0, c1), (c0 - c1).abs().max().item()
 
 
-@pytest.mark.parametrize("M,N,K,groups_rows", [(256, 512, 24576, 0), (128, 256, 24576, 0), (128, 128, 4096, 0),
-                                               (256, 256, 3000 * 16, 0)])
-def test_lds_dma_weight_gradient_is_bit_identical(M, N, K, groups_rows):
+@pytest.mark.parametrize("M,N,K,ldx,gather", [(256, 512, 24576, 512, False), (128, 256, 24576, 256, False),
+                                              (128, 128, 4096, 128, False), (256, 256, 3000 * 16, 256, False),
+                                              (256, 630, 24576, 640, True), (128, 200, 8192, 256, False),
+                                              (128, 60, 4096, 128, True)])
+def test_lds_dma_weight_gradient_is_bit_identical(M, N, K, ldx, gather):
     """The LDS-DMA weight-gradient kernel (gemm_x6t_kernel) against gemm_x6_kernel (lrl_debug_gemm_paths(2) turns it
-    off): the split-k partials and the bias-gradient partials, hence the reduced dW / db, are bit-identical."""
+    off): the split-k partials and the bias-gradient partials, hence the reduced dW / db, are bit-identical — also for
+    a ragged n inside the row pitch and for gathered rows (the adaptation layer's history)."""
     g = torch.Generator(device=dev).manual_seed(M + N + K)
     dY = torch.randn(K, M, device=dev, generator=g)
-    X = torch.randn(K, N, device=dev, generator=g)
+    Xs = torch.randn(K + 77 if gather else K, ldx, device=dev, generator=g)
+    rows = torch.randperm(K + 77, device=dev, generator=g)[:K].contiguous() if gather else None
+    X = (Xs[rows] if gather else Xs)[:, :N]
     ws = torch.empty(256 * (M * N + M), device=dev)
     outs = []
     lib = _abi.lib()
@@ -174,7 +179,7 @@ def test_lds_dma_weight_gradient_is_bit_identical(M, N, K, groups_rows):
         prev = lib.lrl_debug_gemm_paths(C.c_int32(mask))
         try:
             out, db = torch.empty(M, N, device=dev), torch.empty(M, device=dev)
-            _gemm(3, 4, M, N, K, dY, M, X, N, out, N, bias=db, ws=ws)
+            _gemm(3, 4, M, N, K, dY, M, Xs, ldx, out, N, bias=db, rows=rows, ws=ws)
             outs.append((out, db))
         finally:
             lib.lrl_debug_gemm_paths(C.c_int32(prev))
@@ -183,3 +188,31 @@ def test_lds_dma_weight_gradient_is_bit_identical(M, N, K, groups_rows):
     ref = dY.double().T @ X.double()
     mag = dY.double().abs().T @ X.double().abs()
     assert ((outs[1][0].double() - ref).abs() / mag).max().item() <= 1e-6
+
+
+@pytest.mark.parametrize("layout,epi,M,N,K,gather", [(0, 2, 24576, 256, 512, False), (0, 2, 4096, 1024, 64, False),
+                                                     (0, 1, 24576, 128, 256, False), (0, 2, 4096, 256, 640, True),
+                                                     (0, 0, 192, 384, 48, False), (2, 3, 24576, 512, 256, False),
+                                                     (2, 3, 4096, 256, 32, False), (2, 0, 640, 256, 128, False),
+                                                     (2, 3, 8192, 64, 128, False), (0, 2, 8192, 64, 96, True)])
+def test_lds_dma_batch_products_are_bit_identical(layout, epi, M, N, K, gather):
+    """The LDS-DMA forward / backward-data kernel (gemm_x6d_kernel) against gemm_x6_kernel (lrl_debug_gemm_paths(4)
+    turns it off) on the same tile shapes: bit-identical outputs for every epilogue, gathered rows, 64 / 128 tiles."""
+    g = torch.Generator(device=dev).manual_seed(M + N + K + epi + layout)
+    src = torch.randn(M + 50 if gather else M, K, device=dev, generator=g)
+    rows = torch.randperm(M + 50, device=dev, generator=g)[:M].contiguous() if gather else None
+    W = torch.randn(N, K, device=dev, generator=g) if layout == 0 else torch.randn(K, N, device=dev, generator=g)
+    ldb = K if layout == 0 else N
+    bias = torch.randn(N, device=dev, generator=g)
+    aux = torch.randn(M, N, device=dev, generator=g) if epi == 3 else None
+    lib = _abi.lib()
+    outs = []
+    for mask in (4, 8):  # (bit 3: the forward products on the x6d kernel too, as LRL_GEMM_X6D=2)
+        prev = lib.lrl_debug_gemm_paths(C.c_int32(mask))
+        try:
+            c = torch.full((M, N), float("nan"), device=dev)
+            _gemm(layout, epi, M, N, K, src, K, W, ldb, c, N, bias=bias, aux=aux, ld_aux=N, rows=rows)
+            outs.append(c)
+        finally:
+            lib.lrl_debug_gemm_paths(C.c_int32(prev))
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()
