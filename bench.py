@@ -327,8 +327,9 @@ def main():
         gemm_tf = gemm_flop / (gemm_ms * 1e-3) / 1e12 if g_n.value else None
         # dW2 has its own symbol (trace tag 1, csrc/lrl_gemm.hip tn_shape_tag: the LDS-DMA x6t kernel since round 4, the
         # x6 kernel in round 3): its PMC row is this launch's traffic
-        gemm_kernel = "lrl::gemm_x6t_kernel<1, false>"
-        gemm_traffic, gemm_traffic_src = pmc_traffic(gemm_kernel, "lrl::gemm_x6_kernel<128, 128, 3, 4, true, false, 1>")
+        gemm_kernel = "lrl::gemm_x6t_kernel<128, 1, false>"
+        gemm_traffic, gemm_traffic_src = pmc_traffic(gemm_kernel, "lrl::gemm_x6t_kernel<1, false>",
+                                                     "lrl::gemm_x6_kernel<128, 128, 3, 4, true, false, 1>")
         # whole iteration against the fp32 MFMA peak: SURVEY.md §8(d)'s 3.92 MFLOP per minibatch row and epoch of
         # the update (5 epochs over the 98,304 rollout rows) + 0.94 MFLOP per rollout row of the act
         rows_iter = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env

@@ -1502,11 +1502,13 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6p_kernel(GemmP p) {
 // 4 waves of 2 x 2 MFMA tiles, the six products in gemm_x6_kernel's order over the same k order, and the bias
 // gradient partial summed in its (row, k-half) order: bit-identical to it.
 constexpr int X6T_MAX_GATHER_KPS = 1024;  // gathered-B splits of at most this many rows (the row list in LDS)
-template <int TAG, bool BGATHER>
+template <int BN, int TAG, bool BGATHER>
 __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
-  constexpr int BM = 128, BN = 128, NST = 3, TM = 2, TN = 2;
-  constexpr int IMG = 16 * 128 * 4, STB = 2 * IMG;  // bytes: A image then B image
-  constexpr int NPW = 4;                            // DMA wave-instructions per wave and stage (2 per operand)
+  constexpr int BM = 128, NST = 3, TM = 2, TN = BN / 64;
+  constexpr int IMG = 16 * 128 * 4, STB = IMG + 16 * BN * 4;  // bytes: A image [16][128], then B image [16][BN]
+  constexpr int NAP = IMG / 1024, NBP = BN / 16;              // DMA pieces (1 KiB wave-instructions) per stage
+  constexpr int NPW = (NAP + NBP) / 4;                        // per wave: 4 (BN 128) or 3 (BN 64)
+  constexpr int KPP = 256 / BN;                               // k-rows per B piece
   constexpr int XROWS = BGATHER ? X6T_MAX_GATHER_KPS : 0;  // gathered B: the split's row list (int32) after the ring
   __shared__ __attribute__((aligned(16))) uint8_t S[NST * STB + 4 * XROWS];
   const int mt = p.M / BM, nt = (p.N + BN - 1) / BN;  // (ragged n: see try_x6t)
@@ -1525,10 +1527,11 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
   const float* __restrict__ A = p.A + g * p.ga;
   const float* __restrict__ Bm = p.B + g * p.gb;
-  // this lane's DMA sources: k-row 2 (2w + d) + lane / 32, slot lane % 32 (source chunk pre-swizzled)
-  const float* asrc[2];
-  const float* bsrc[2];
-  int bkr[2];
+  // this wave's DMA pieces j = NPW w + d: A's first (two k-rows each: lane / 32, slot lane % 32), then B's (KPP k-rows
+  // each); the source chunk is pre-swizzled, the LDS destination of piece j is j KiB into the stage
+  const float* src[NPW];
+  int64_t kstep[NPW];
+  int bkr[NPW];
   int* xrows = reinterpret_cast<int*>(S + NST * STB);
   if constexpr (BGATHER) {
     // the split's B row list into LDS before the ring starts (no DMA in flight: a plain barrier is safe)
@@ -1536,11 +1539,19 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
     __syncthreads();
   }
 #pragma unroll
-  for (int d = 0; d < 2; ++d) {
-    const int kr = 2 * (2 * w + d) + (lane >> 5), ch = (lane & 31) ^ (8 * ((kr >> 3) & 1));
-    asrc[d] = A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * ch;
-    bsrc[d] = BGATHER ? Bm + n0 + 4 * ch : Bm + (int64_t)(kbeg + kr) * p.ldb + n0 + 4 * ch;
-    bkr[d] = kr;
+  for (int d = 0; d < NPW; ++d) {
+    const int j = NPW * w + d;
+    if (j < NAP) {
+      const int kr = 2 * j + (lane >> 5), ch = (lane & 31) ^ (8 * ((kr >> 3) & 1));
+      src[d] = A + (int64_t)(kbeg + kr) * p.lda + m0 + 4 * ch;
+      kstep[d] = (int64_t)16 * p.lda;
+      bkr[d] = -1;
+    } else {
+      const int kr = KPP * (j - NAP) + lane / (BN / 4), ch = (lane % (BN / 4)) ^ (8 * ((kr >> 3) & 1));
+      src[d] = BGATHER ? Bm + n0 + 4 * ch : Bm + (int64_t)(kbeg + kr) * p.ldb + n0 + 4 * ch;
+      kstep[d] = (int64_t)16 * p.ldb;
+      bkr[d] = kr;
+    }
   }
   const uint32_t s_lds = (uint32_t)(uintptr_t)(lds_ptr_t)S;
   auto dma = [&](const void* src, uint32_t lds_off) {
@@ -1552,13 +1563,10 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
   };
   auto issue = [&](int st, int s) {
     const uint32_t base = s_lds + (uint32_t)(st * STB);
-    const int64_t ka = (int64_t)16 * s * p.lda, kb = (int64_t)16 * s * p.ldb;
 #pragma unroll
-    for (int d = 0; d < 2; ++d) dma(asrc[d] + ka, __builtin_amdgcn_readfirstlane(base + (2 * w + d) * 1024));
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      const float* bs = BGATHER ? bsrc[d] + (int64_t)xrows[16 * s + bkr[d]] * p.ldb : bsrc[d] + kb;
-      dma(bs, __builtin_amdgcn_readfirstlane(base + IMG + (2 * w + d) * 1024));
+    for (int d = 0; d < NPW; ++d) {
+      const float* sr = (BGATHER && bkr[d] >= 0) ? src[d] + (int64_t)xrows[16 * s + bkr[d]] * p.ldb : src[d] + s * kstep[d];
+      dma(sr, __builtin_amdgcn_readfirstlane(base + (NPW * w + d) * 1024));
     }
   };
   const bool do_bsum = p.bias_part != nullptr && tn_ == 0 && wn == 0;
@@ -1576,20 +1584,24 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
   if (ns > 1) issue(1, 1);
   // lane's element offsets (floats) into an image: k-row 8h + t at + 128 t, row / column r ^ 32 h
   const int sw = 32 * h;
+  static_assert(NPW == 3 || NPW == 4, "vmcnt below");
   for (int s = 0; s < ns; ++s) {
-    if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (s + 1 < ns) {
+      if constexpr (NPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     if (s + 2 < ns) issue((s + 2) % NST, s + 2);
-    static_assert(NPW == 4, "vmcnt above");
     const float* As = reinterpret_cast<const float*>(S + (s % NST) * STB);
     const float* Bs = As + IMG / 4;
     bf16x8_t a[TM][3], b[TN][3];
-    auto gather_split = [&](const float* img, int r, bf16x8_t (&o)[3], float* vs) {
-      const float* src = img + 8 * h * 128 + (r ^ sw);
+    auto gather_split = [&](const float* img, int pitch, int r, bf16x8_t (&o)[3], float* vs) {
+      const float* p0 = img + 8 * h * pitch + (r ^ sw);
       float v[8];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = src[128 * t];
+      for (int t = 0; t < 8; ++t) v[t] = p0[pitch * t];
       if (vs) {
         float s8 = 0.f;
 #pragma unroll
@@ -1606,9 +1618,9 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_x6t_kernel(GemmP p) {
       o[2] = *reinterpret_cast<bf16x8_t*>(&vl);
     };
 #pragma unroll
-    for (int i = 0; i < TM; ++i) gather_split(As, wm + 32 * i + li, a[i], do_bsum ? &bsum[i] : nullptr);
+    for (int i = 0; i < TM; ++i) gather_split(As, 128, wm + 32 * i + li, a[i], do_bsum ? &bsum[i] : nullptr);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) gather_split(Bs, wn + 32 * j + li, b[j], nullptr);
+    for (int j = 0; j < TN; ++j) gather_split(Bs, BN, wn + 32 * j + li, b[j], nullptr);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1906,21 +1918,26 @@ static bool x6t_enabled() {
 // the last tile (the DMA reads whole 128-wide tiles); a gathered B keeps its split's row list in LDS
 static int try_x6t(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
   if (!x6t_enabled() || layout != GEMM_TN || epi != EPI_PARTIAL) return 0;
-  const int nt = (p.N + 127) / 128;
+  const int bn = p.N <= 64 ? 64 : 128, nt = (p.N + bn - 1) / bn;
   if (p.M % 128 || p.K % 16 || p.kps % 16 || p.kps < 16 || p.avec != 4 || p.bvec != 4) return 0;
-  if ((int64_t)nt * 128 > p.ldb) return 0;
+  if ((int64_t)nt * bn > p.ldb) return 0;
   if (p.b_rows && p.kps > X6T_MAX_GATHER_KPS) return 0;
   if ((int64_t)(p.splits - 1) * p.kps >= p.K) return 0;  // (every split has a non-empty range)
   dim3 grid((unsigned)((p.M / 128) * nt * groups * p.splits));  // (stores stop at p.N)
+  if (bn == 64) {
+    if (p.b_rows) hipLaunchKernelGGL((gemm_x6t_kernel<64, 5, true>), grid, dim3(GTHREADS), 0, st, p);
+    else hipLaunchKernelGGL((gemm_x6t_kernel<64, 3, false>), grid, dim3(GTHREADS), 0, st, p);
+    return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
+  }
   if (p.b_rows) {
-    hipLaunchKernelGGL((gemm_x6t_kernel<4, true>), grid, dim3(GTHREADS), 0, st, p);
+    hipLaunchKernelGGL((gemm_x6t_kernel<128, 4, true>), grid, dim3(GTHREADS), 0, st, p);
     return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
   }
   switch (tn_shape_tag(p.M, p.N, groups)) {
-    case 1: hipLaunchKernelGGL((gemm_x6t_kernel<1, false>), grid, dim3(GTHREADS), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((gemm_x6t_kernel<2, false>), grid, dim3(GTHREADS), 0, st, p); break;
-    case 6: hipLaunchKernelGGL((gemm_x6t_kernel<6, false>), grid, dim3(GTHREADS), 0, st, p); break;
-    default: hipLaunchKernelGGL((gemm_x6t_kernel<0, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 1: hipLaunchKernelGGL((gemm_x6t_kernel<128, 1, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm_x6t_kernel<128, 2, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((gemm_x6t_kernel<128, 6, false>), grid, dim3(GTHREADS), 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x6t_kernel<128, 0, false>), grid, dim3(GTHREADS), 0, st, p); break;
   }
   return hipGetLastError() == hipSuccess ? 1 : LRL_E_HIP;
 }

@@ -11,7 +11,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 B = int(os.environ.get("GEMM_BENCH_B", "24576"))
 dev = "cuda:0"
-SHAPES = [("dW2 TN 256x512", 256, 512), ("dW3 TN 128x256", 128, 256), ("dWe2 TN 128x256", 128, 256)]
+SHAPES = [("dW2 TN 256x512", 256, 512, 512), ("dW3 TN 128x256", 128, 256, 256), ("dWe2 TN 128x256", 128, 256, 256),
+          ("dW1 TN 1024x60", 1024, 60, 64)]
 
 
 def main():
@@ -21,16 +22,16 @@ def main():
     p = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
     torch.manual_seed(0)
     ok = True
-    for name, M, N in SHAPES:
+    for name, M, N, ldx in SHAPES:
         K = B
-        dY, X = torch.randn(K, M, device=dev), torch.randn(K, N, device=dev)
+        dY, X = torch.randn(K, M, device=dev), torch.randn(K, ldx, device=dev)
         ws = torch.empty(256 * (M * N + M), device=dev)
         outs = {}
 
         def call(mask, out, db):
             L.lrl_debug_gemm_paths(mask)
             st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-            rc = L.lrl_gemm_f32(3, 4, M, N, K, p(dY), C.c_int64(M), p(X), C.c_int64(N), p(out), C.c_int64(N), p(db),
+            rc = L.lrl_gemm_f32(3, 4, M, N, K, p(dY), C.c_int64(M), p(X), C.c_int64(ldx), p(out), C.c_int64(N), p(db),
                                 None, C.c_int64(0), None, p(ws), C.c_int64(ws.numel()), st)
             assert rc == 0
 

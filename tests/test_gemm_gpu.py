@@ -162,7 +162,8 @@ def test_pre_split_weight_kernel_is_bit_identical(layout, epi, M, N, K, gather):
 @pytest.mark.parametrize("M,N,K,ldx,gather", [(256, 512, 24576, 512, False), (128, 256, 24576, 256, False),
                                               (128, 128, 4096, 128, False), (256, 256, 3000 * 16, 256, False),
                                               (256, 630, 24576, 640, True), (128, 200, 8192, 256, False),
-                                              (128, 60, 4096, 128, True)])
+                                              (128, 60, 4096, 128, True), (1024, 60, 24576, 64, False),
+                                              (256, 40, 8192, 64, True)])
 def test_lds_dma_weight_gradient_is_bit_identical(M, N, K, ldx, gather):
     """The LDS-DMA weight-gradient kernel (gemm_x6t_kernel) against gemm_x6_kernel (lrl_debug_gemm_paths(2) turns it
     off): the split-k partials and the bias-gradient partials, hence the reduced dW / db, are bit-identical — also for
