@@ -30,9 +30,14 @@ __device__ inline double clip01(double x) { return fmin(fmax(x, 0.0), 1.0); }
 // elements (8 interleaved partial sums, or a plain loop below 8), a node's sum = left + right with the split at
 // n2 = n / 2 - (n / 2) % 8.  cd_walk visits the tree on one thread: mode 0 lists the leaves left to right (offsets,
 // lengths; returns their count), mode 1 combines the leaf sums `val` (in that order) as the recursion does.
-__device__ double cd_walk(int n, int mode, int* leaf_off, int* leaf_len, const double* val, int* nleaves) {
+// (its stack lives in LDS: as a private array it was scratch memory, a global round trip per step of the walk)
+struct CdStack {
   double res[32];
   int off[32], len[32], st[32];
+};
+__device__ double cd_walk(int n, int mode, int* leaf_off, int* leaf_len, const double* val, int* nleaves, CdStack& K) {
+  double* res = K.res;
+  int *off = K.off, *len = K.len, *st = K.st;
   int sp = 0, li = 0;
   off[0] = 0; len[0] = n; st[0] = 0;
   double ret = 0.0;
@@ -158,6 +163,7 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
   __shared__ int leaf_off[CD_MAX_LEAVES], leaf_len[CD_MAX_LEAVES];
   __shared__ double leaf_val[CD_MAX_LEAVES];
   __shared__ double Ssum;
+  __shared__ CdStack cstack;
   const int t = threadIdx.x;
   const int n = min(*a.dcount, a.nmax);
   if (n <= 0) return;  // (resample_commands returns before touching the generator)
@@ -237,14 +243,14 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
   if (need_cdf || a.log_area) {
     for (int b = t; b < nb; b += CD_THREADS) cdf[b] = c.weights[b];
     if (t == 0) {
-      cd_walk(nb, 0, leaf_off, leaf_len, nullptr, &nleaves);
+      cd_walk(nb, 0, leaf_off, leaf_len, nullptr, &nleaves, cstack);
       bad = 0;
     }
     __syncthreads();
     for (int l = t; l < nleaves; l += CD_THREADS) leaf_val[l] = cd_leaf(cdf + leaf_off[l], leaf_len[l]);
     __syncthreads();
     if (t == 0) {
-      Ssum = 0.0 + cd_walk(nb, 1, nullptr, nullptr, leaf_val, nullptr);
+      Ssum = 0.0 + cd_walk(nb, 1, nullptr, nullptr, leaf_val, nullptr, cstack);
       if (a.log_area) c.command_area[0] = Ssum / (double)nb;
     }
     __syncthreads();
@@ -266,18 +272,29 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
       }
       return;
     }
-    if (t == 0) {  // cumsum: a sequential chain of adds, as add.accumulate (the loads issue ahead of the chain)
+    if (t == 0) {  // cumsum: a sequential chain of adds, as add.accumulate (the next 16 loads in flight under the chain)
       double acc = cdf[0];
       int b = 1;
-      for (; b + 8 <= nb; b += 8) {
-        double v[8];
+      double nx[16];
+      if (b + 16 <= nb) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = cdf[b + j];
+        for (int j = 0; j < 16; ++j) nx[j] = cdf[b + j];
+      }
+      for (; b + 16 <= nb; b += 16) {
+        double v[16];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          acc = acc + v[j];
-          cdf[b + j] = acc;
+        for (int j = 0; j < 16; ++j) v[j] = nx[j];
+        if (b + 32 <= nb) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) nx[j] = cdf[b + 16 + j];
         }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          acc = acc + v[j];
+          v[j] = acc;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) cdf[b + j] = v[j];
       }
       for (; b < nb; ++b) {
         acc = acc + cdf[b];

@@ -357,7 +357,8 @@ class LeggedRobotEnv:
         # observation launches all read device-side lists and counts (_step_device).  LRL_DEVICE_RESETS=0 or
         # device_resets=False keeps the host path (one device->host copy per step), the check for this one.
         if device_resets is None:
-            device_resets = os.environ.get("LRL_DEVICE_RESETS", "0") == "1"  # (default: after GPU validation)
+            # (default on: 2.81-2.82 M against 2.59-2.63 M env-steps/s on configs[2], profiles/r4u_sec_ab.jsonl)
+            device_resets = os.environ.get("LRL_DEVICE_RESETS", "1") != "0"
         self._dev_path = bool(device_resets) and not self.legacy_fork and self._dist is None and eval_cfg is None \
             and self._track_rows is not None and len(self._curriculum.keys) == 3
         self._dcur = None      # device curriculum buffers (allocated at the first device step)
