@@ -97,6 +97,84 @@ __device__ double cd_leaf(const double* a, int m) {
   return r;
 }
 
+// The same pairwise sum, level by level: wave 0 lays the recursion out top-down (each level's nodes in LDS, a node of
+// more than 128 elements splitting at n2 = n / 2 - (n / 2) % 8 into two children on the next level, placed by a ballot
+// prefix count), every thread sums the leaves, wave 0 adds each internal node's left + right bottom-up.  The same
+// leaves, the same adds in the same tree as cd_walk, without its serial chain of dependent LDS stack operations.
+// Returns false (nothing written) when the tree exceeds CD_LV levels or CD_LN nodes on a level.
+constexpr int CD_LV = 10, CD_LN = 128;
+struct CdLevels {
+  int off[CD_LV][CD_LN], len[CD_LV][CD_LN], child[CD_LV][CD_LN];
+  double val[CD_LV][CD_LN];
+  int cnt[CD_LV + 1];
+  int ok, depth;
+};
+__device__ bool cd_pairwise_levels(const double* a, int n, CdLevels& T, double* out) {
+  const int t = threadIdx.x, lane = t & 63;
+  if (t == 0) {
+    T.off[0][0] = 0;
+    T.len[0][0] = n;
+    T.cnt[0] = 1;
+    T.ok = 1;
+    T.depth = 0;
+  }
+  __syncthreads();
+  if (t < 64) {
+    for (int L = 0; L < CD_LV; ++L) {
+      const int c = T.cnt[L];
+      int base = 0;
+      for (int i0 = 0; i0 < c; i0 += 64) {
+        const int i = i0 + lane;
+        const bool in = i < c;
+        const int m = in ? T.len[L][i] : 0;
+        const bool internal = in && m > 128;
+        const uint64_t mask = __ballot(internal);
+        const int rank = base + __popcll(mask & ((1ull << lane) - 1ull));
+        if (in) T.child[L][i] = internal ? 2 * rank : -1;
+        if (internal) {
+          if (L + 1 >= CD_LV || 2 * rank + 1 >= CD_LN) {
+            T.ok = 0;
+          } else {
+            int n2 = m / 2;
+            n2 -= n2 % 8;
+            const int o = T.off[L][i];
+            T.off[L + 1][2 * rank] = o;
+            T.len[L + 1][2 * rank] = n2;
+            T.off[L + 1][2 * rank + 1] = o + n2;
+            T.len[L + 1][2 * rank + 1] = m - n2;
+          }
+        }
+        base += __popcll(mask);
+      }
+      if (lane == 0) {
+        T.cnt[L + 1] = 2 * base;
+        if (base == 0) T.depth = L + 1;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (base == 0 || !T.ok) break;
+    }
+  }
+  __syncthreads();
+  if (!T.ok || T.depth == 0) return false;
+  const int D = T.depth;
+  for (int L = 0; L < D; ++L)
+    for (int i = t; i < T.cnt[L]; i += blockDim.x)
+      if (T.child[L][i] < 0) T.val[L][i] = cd_leaf(a + T.off[L][i], T.len[L][i]);
+  __syncthreads();
+  if (t < 64) {
+    for (int L = D - 2; L >= 0; --L) {
+      for (int i = lane; i < T.cnt[L]; i += 64) {
+        const int ch = T.child[L][i];
+        if (ch >= 0) T.val[L][i] = T.val[L + 1][ch] + T.val[L + 1][ch + 1];
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) *out = T.val[0][0];
+  }
+  __syncthreads();
+  return true;
+}
+
 __device__ inline uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
@@ -164,6 +242,7 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
   __shared__ double leaf_val[CD_MAX_LEAVES];
   __shared__ double Ssum;
   __shared__ CdStack cstack;
+  __shared__ CdLevels clev;
   const int t = threadIdx.x;
   const int n = min(*a.dcount, a.nmax);
   if (n <= 0) return;  // (resample_commands returns before touching the generator)
@@ -242,17 +321,18 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
   const bool need_cdf = changed || c.state[0] == 0;
   if (need_cdf || a.log_area) {
     for (int b = t; b < nb; b += CD_THREADS) cdf[b] = c.weights[b];
-    if (t == 0) {
-      cd_walk(nb, 0, leaf_off, leaf_len, nullptr, &nleaves, cstack);
-      bad = 0;
-    }
+    if (t == 0) bad = 0;
     __syncthreads();
-    for (int l = t; l < nleaves; l += CD_THREADS) leaf_val[l] = cd_leaf(cdf + leaf_off[l], leaf_len[l]);
-    __syncthreads();
-    if (t == 0) {
-      Ssum = 0.0 + cd_walk(nb, 1, nullptr, nullptr, leaf_val, nullptr, cstack);
-      if (a.log_area) c.command_area[0] = Ssum / (double)nb;
+    if (cd_pairwise_levels(cdf, nb, clev, &Ssum)) {
+      if (t == 0) Ssum = 0.0 + Ssum;
+    } else {  // (a tree past the level tables: the serial walk)
+      if (t == 0) cd_walk(nb, 0, leaf_off, leaf_len, nullptr, &nleaves, cstack);
+      __syncthreads();
+      for (int l = t; l < nleaves; l += CD_THREADS) leaf_val[l] = cd_leaf(cdf + leaf_off[l], leaf_len[l]);
+      __syncthreads();
+      if (t == 0) Ssum = 0.0 + cd_walk(nb, 1, nullptr, nullptr, leaf_val, nullptr, cstack);
     }
+    if (t == 0 && a.log_area) c.command_area[0] = Ssum / (double)nb;
     __syncthreads();
   }
   // ---- the sampling cdf (cached while the weights are unchanged), staged in LDS ----
@@ -397,7 +477,7 @@ extern "C" hipError_t lrl_launch_curriculum_dev(const lrl_dev_curriculum* c, con
   const int nb = c->nx * c->ny * c->nz;
   const size_t lds = (size_t)nb * 8 + (size_t)(2 * nb + lrl::MT_N) * 4;
   if (nb / 64 + 2 > lrl::CD_MAX_LEAVES) return hipErrorInvalidValue;
-  constexpr size_t kMaxDyn = 144 * 1024;  // (+ the kernel's ~4 KB of static LDS, inside the CU's 160 KB)
+  constexpr size_t kMaxDyn = 124 * 1024;  // (+ the kernel's ~31 KB of static LDS, inside the CU's 160 KB)
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(lrl::curriculum_dev_kernel),
