@@ -32,6 +32,7 @@ from helpers import (MAX_EXCLUDED, SEP_EPS_1, VEL_EPS, make, make_rough, oracle_
                      record_errors, within_tolerance)
 from lrl import _abi
 from oracle import oracle
+from ranks import rank_env
 
 pytestmark = pytest.mark.gpu
 
@@ -360,10 +361,8 @@ STORE_KEYS = ["observations", "privileged_observations", "observation_histories"
 def _rank_worker(rank, world, port, robot, tmp, out, n=N_BENCH, rollout_only=False):
     sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    if world > 1:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    from ranks import init_rank
+    init_rank(rank, world, port)
     out[rank] = _iteration(robot, rank, world, tmp, n, rollout_only)
     if world > 1:
         dist.destroy_process_group()
@@ -405,6 +404,7 @@ def _single_rank_first_grad(path):
     return cap[0]
 
 
+@pytest.mark.multiproc
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("robot,world", [("mc", 2), ("go1", 2), ("mc", 8)])
 def test_multi_rank_full_iteration_at_bench_shape(robot, world):
@@ -415,7 +415,8 @@ def test_multi_rank_full_iteration_at_bench_shape(robot, world):
     mgr = mp.Manager()
     out = mgr.dict()
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_rank_worker, args=(world, _port(), robot, tmp, out), nprocs=world, join=True)
+        with rank_env(world):
+            mp.spawn(_rank_worker, args=(world, _port(), robot, tmp, out), nprocs=world, join=True)
         res = [out[r] for r in range(world)]
         a = res[0]
         assert np.isfinite(a["params"]).all()
@@ -433,6 +434,7 @@ def test_multi_rank_full_iteration_at_bench_shape(robot, world):
     assert np.abs(single[0] - single[1]).max() > 1e-4
 
 
+@pytest.mark.multiproc
 @pytest.mark.timeout(600)
 def test_rollout_does_not_depend_on_the_gpu_count():
     """every draw is keyed by the global env id (env: env_offset; policy noise: PPO.row_offset) and the

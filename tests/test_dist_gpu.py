@@ -12,7 +12,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.multiproc]
 
 
 def _port():
@@ -28,9 +28,8 @@ def _worker(rank, world, port, out):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "rapid-locomotion-rl_amd"))
     sys.path.insert(0, os.path.join(root, "tests"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    from ranks import init_rank
+    init_rank(rank, world, port)
     from lrl.ppo.actor_critic import ActorCritic
     from lrl.ppo.ppo import PPO
     from test_ppo_gpu import _random_storage, init_params
@@ -143,9 +142,9 @@ def _curriculum_worker(rank, world, port, n, out):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "rapid-locomotion-rl_amd"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from ranks import init_rank
+    init_rank(rank, world, port)
     out[rank] = _run_curriculum_env(n, rank * n)
     dist.destroy_process_group()
 
@@ -175,9 +174,8 @@ def _overlap_worker(rank, world, port, out):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "rapid-locomotion-rl_amd"))
     sys.path.insert(0, os.path.join(root, "tests"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    from ranks import init_rank
+    init_rank(rank, world, port)
     from lrl.ppo.actor_critic import ActorCritic
     from lrl.ppo.ppo import PPO
     from test_ppo_gpu import _random_storage, init_params
