@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define LRL_ABI_VERSION 3
+#define LRL_ABI_VERSION 4
 
 #define LRL_OK 0
 #define LRL_E_INVALID (-1)  /* bad argument / unsupported configuration */
@@ -376,9 +376,11 @@ int32_t lrl_sim_reset_idx_dev(lrl_sim* sim, const int32_t* ids, int32_t nmax, co
 int32_t lrl_sim_observe_idx_dev(lrl_sim* sim, const int32_t* ids, int32_t nmax, const int32_t* dcount, uint32_t flags,
                                 void* stream);
 /* reset_idx's episode logging (torch.mean of each row over the ids, then zeroed) with a device count; an empty batch
- * leaves `means` as they were (the reference's extras keep the last reset batch's dict) */
+ * writes `prev` into `means` (the reference's extras keep the last reset batch's values), or leaves `means` as they
+ * were when prev is null.  With a fresh `means` buffer per step and the previous step's as `prev`, every step
+ * publishes values no later step overwrites (ABI 4: `prev` added). */
 int32_t lrl_rows_mean_zero_dev(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t nmax,
-                               const int32_t* dcount, float* means, int32_t zero, void* stream);
+                               const int32_t* dcount, float* means, const float* prev, int32_t zero, void* stream);
 /* The grid-adaptive command curriculum on the device (RewardThresholdCurriculum, curriculum.py:16-124): its state in
  * caller-owned device buffers, bit-exact with the host forms (numpy RandomState MT19937, pairwise sums). */
 typedef struct lrl_dev_curriculum {
@@ -395,6 +397,8 @@ typedef struct lrl_dev_curriculum {
   int32_t nx, ny, nz;
   uint32_t* words;                 /* scratch [8 * num_envs] */
   double* draws;                   /* scratch [4 * num_envs] */
+  const float* env_bins_f_prev;    /* optional: with log_area and an empty batch, env_bins_f / command_area are */
+  const double* command_area_prev; /* copied from these (fresh output buffers per step keep earlier steps' values) */
 } lrl_dev_curriculum;
 /* _resample_commands (legged_robot.py:595-626) of the listed envs: update(old bins, tracking sums / ep_len vs the
  * thresholds, local_range) when `update`, sample(count), then commands[ids, :3] (|xy| > 0.2 mask), command_sums[:, ids]

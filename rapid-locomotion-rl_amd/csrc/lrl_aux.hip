@@ -23,26 +23,28 @@ namespace lrl {
 // xy draw xy_span * u + xy_lo and the (x_off, y_off) init offsets.  Uniform draws: (motor strength, Kp, Kd, x, y)
 // from Philox keyed by (global env, reset counter), or row t of S.inj_reset (the reference's torch.rand draws,
 // one row per env id in id order).  Float32 arithmetic in the reference's operation order, uncontracted.
-// (dn: the id count on the device, the host's n is then the launch bound — the upstream step's asynchronous path;
-// dctr: the reset counter, bumped on the device by bump_counter_kernel when the batch is not empty)
+// (dn: the id count on the device, the host's n is then the launch bound — the upstream step's asynchronous path.)
+// The draws' counter is the env's own reset count (S.reset_count, bumped here), so a global env draws the same values
+// whatever the sharding: it depends on that env's history only, not on which other envs share its process.
 __global__ void reset_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
                              const int32_t* __restrict__ dn, int32_t root_mode, float xy_lo, float xy_span, float x_off,
-                             float y_off, int32_t inject, const int64_t* __restrict__ dctr) {
+                             float y_off, int32_t inject) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (dn ? min(*dn, n) : n)) return;
-  const int64_t counter = *dctr;
   const lrl_env_params& P = K->p;
   const int N = S.stride;
   int e = ids[t];
   if (e < 0 || e >= S.n) return;
+  const uint32_t counter = (uint32_t)S.reset_count[e];
+  S.reset_count[e] = (int32_t)(counter + 1u);
   float u[5];
   if (inject) {
     for (int k = 0; k < 5; ++k) u[k] = S.inj_reset[(size_t)t * 5 + k];
   } else {
     uint64_t genv = (uint64_t)(S.env_offset + e);
-    const uint32_t key = (LRL_RNG_RESET << 16) ^ (uint32_t)(counter >> 32);
-    lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)counter, key, 0, S.seed);
-    lrl_u32x4 r2 = lrl_philox((uint32_t)genv, (uint32_t)counter, key, 1, S.seed);
+    const uint32_t key = (uint32_t)LRL_RNG_RESET << 16;
+    lrl_u32x4 r = lrl_philox((uint32_t)genv, counter, key, 0, S.seed);
+    lrl_u32x4 r2 = lrl_philox((uint32_t)genv, counter, key, 1, S.seed);
     for (int k = 0; k < 4; ++k) u[k] = lrl_u01(r.v[k]);
     u[4] = lrl_u01(r2.v[0]);
   }
@@ -327,11 +329,15 @@ __global__ void randomize_kernel(KState S, float f0, float f1, float r0, float r
 // (dn: the id count on the device, n its bound; an empty batch then leaves the previous means in place, as the
 // reference's extras keep the last reset batch's episode dict)
 __global__ void rows_mean_zero_kernel(float* __restrict__ tab, int64_t ld, const int32_t* __restrict__ ids, int32_t n,
-                                      const int32_t* __restrict__ dn, float* __restrict__ means, int32_t zero) {
+                                      const int32_t* __restrict__ dn, float* __restrict__ means,
+                                      const float* __restrict__ prev, int32_t zero) {
   __shared__ float red[256];
   if (dn) {
     n = min(*dn, n);
-    if (n == 0) return;
+    if (n == 0) {
+      if (prev && threadIdx.x == 0) means[blockIdx.x] = prev[blockIdx.x];
+      return;
+    }
   }
   float* row = tab + (int64_t)blockIdx.x * ld;
   float s = 0.f;
@@ -393,11 +399,6 @@ __global__ __launch_bounds__(1024) void compact_kernel(KState S, int32_t interva
   if (count_out && t == 1023) count_out[0] = cnt[1023];
 }
 
-// the reset counter of a non-empty batch (the host's count n, or the device count dn)
-__global__ void bump_counter_kernel(int64_t* ctr, const int32_t* __restrict__ dn, int32_t n) {
-  if (threadIdx.x == 0 && (dn ? min(*dn, n) : n) > 0) ctr[0] += 1;
-}
-
 // _resample_commands' device writes (legged_robot.py:595-626 as lrl/env.py restates it): commands[ids, :3] = cmds,
 // command_sums[:, ids] = 0 (every row); then, when given, bins_out[:nb] = bins_in[:nb] (the env-bins tensor).
 __global__ void apply_commands_kernel(KState S, int32_t ncs, const int32_t* __restrict__ ids, int32_t n,
@@ -444,24 +445,26 @@ int32_t lrl_rows_mean_zero(float* table, int64_t ld, int32_t rows, const int32_t
   if (!table || !means || rows < 0 || n < 0 || (n > 0 && !ids)) return 1;
   if (rows == 0) return 0;
   hipLaunchKernelGGL(lrl::rows_mean_zero_kernel, dim3(rows), dim3(256), 0, static_cast<hipStream_t>(stream), table,
-                     ld, ids, n, (const int32_t*)nullptr, means, zero);
+                     ld, ids, n, (const int32_t*)nullptr, means, (const float*)nullptr, zero);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 int32_t lrl_rows_mean_zero_dev(float* table, int64_t ld, int32_t rows, const int32_t* ids, int32_t nmax,
-                               const int32_t* dcount, float* means, int32_t zero, void* stream) {
+                               const int32_t* dcount, float* means, const float* prev, int32_t zero, void* stream) {
   if (!table || !means || rows < 0 || nmax < 0 || !dcount || (nmax > 0 && !ids)) return 1;
-  if (rows == 0 || nmax == 0) return 0;
+  if (rows == 0) return 0;
+  if (nmax == 0)
+    return !prev || hipMemcpyAsync(means, prev, rows * sizeof(float), hipMemcpyDeviceToDevice,
+                                   static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : 2;
   hipLaunchKernelGGL(lrl::rows_mean_zero_kernel, dim3(rows), dim3(256), 0, static_cast<hipStream_t>(stream), table,
-                     ld, ids, nmax, dcount, means, zero);
+                     ld, ids, nmax, dcount, means, prev, zero);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 hipError_t lrl_launch_reset(const KParams* K, const KState* S, const int32_t* ids, int32_t n, const int32_t* dn,
                             int32_t root_mode, float xy_lo, float xy_span, float x_off, float y_off, int32_t inject,
-                            int64_t* dctr, hipStream_t st) {
+                            hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lrl::bump_counter_kernel, dim3(1), dim3(64), 0, st, dctr, dn, n);
   hipLaunchKernelGGL(lrl::reset_kernel, dim3((n + 255) / 256), dim3(256), 0, st, K, *S, ids, n, dn, root_mode, xy_lo,
-                     xy_span, x_off, y_off, inject, (const int64_t*)dctr);
+                     xy_span, x_off, y_off, inject);
   return hipGetLastError();
 }
 hipError_t lrl_launch_terrain_curriculum(const KState* S, const int32_t* ids, int32_t n, const int32_t* dn,

@@ -33,7 +33,7 @@ hipError_t lrl_launch_observe(const KParams*, const KState*, const int32_t*, int
                               hipStream_t);
 hipError_t lrl_env_kernel_setup(int lds_bytes);
 hipError_t lrl_launch_reset(const KParams*, const KState*, const int32_t*, int32_t, const int32_t*, int32_t, float, float,
-                            float, float, int32_t, int64_t*, hipStream_t);
+                            float, float, int32_t, hipStream_t);
 hipError_t lrl_launch_env_lists(const KState*, int32_t, int32_t, int32_t*, int32_t*, hipStream_t);
 hipError_t lrl_launch_curriculum_dev(const lrl_dev_curriculum*, const KState*, int32_t, const int32_t*, int32_t,
                                      const int32_t*, int32_t, int32_t, int32_t, double, double, double, int32_t,
@@ -64,7 +64,6 @@ struct lrl_sim {
   size_t arena_bytes = 0;
   int lds_bytes = 0;
   int64_t step_counter = 0;
-  int64_t* d_reset_ctr = nullptr;  // reset_idx's counter-RNG counter, on the device (bumped per non-empty batch)
   lrl_tensor t[LRL_T_NUM];
   int32_t* d_body_leg = nullptr;
   int32_t* d_body_link = nullptr;
@@ -284,6 +283,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   addf(&S.priv, (size_t)N * LRL_NUM_PRIV); addf(&S.hist, (size_t)N * H); addf(&S.rew, N);
   fields.push_back({(void**)&S.reset, (size_t)N}); fields.push_back({(void**)&S.time_out, (size_t)N});
   fields.push_back({(void**)&S.last_contacts, 4ull * N}); fields.push_back({(void**)&S.episode_length, 4ull * N});
+  fields.push_back({(void**)&S.reset_count, 4ull * N});
   addf(&S.episode_sums, (size_t)nes * N); addf(&S.command_sums, (size_t)ncs * N); addf(&S.feet_air_time, 4ull * N);
   addf(&S.friction, N); addf(&S.restitution, N); addf(&S.payload, N); addf(&S.com, 3ull * N);
   addf(&S.motor_strength, 12ull * N); addf(&S.kp, 12ull * N); addf(&S.kd, 12ull * N); addf(&S.env_origins, 3ull * N);
@@ -300,8 +300,6 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   size_t off = 0;
   for (auto& f : fields) { *f.p = (char*)arena + off; off += (f.bytes + 255) / 256 * 256; }
   HIPCHECK(hipMemset(arena, 0, total));
-  HIPCHECK(hipMalloc(&s->d_reset_ctr, sizeof(int64_t)));
-  HIPCHECK(hipMemset(s->d_reset_ctr, 0, sizeof(int64_t)));
   // initial values: identity quaternion, unit DR factors, default friction 1
   std::vector<float> ones(N, 1.f);
   HIPCHECK(hipMemcpy(S.root + 6ull * N, ones.data(), N * 4, hipMemcpyHostToDevice));
@@ -477,7 +475,6 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->terr);
   (void)hipFree(s->self_stats);
   (void)hipFree(s->d_code);
-  (void)hipFree(s->d_reset_ctr);
   for (auto& pr : s->ev) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -594,7 +591,7 @@ int32_t lrl_sim_reset_idx_ex(lrl_sim* s, const int32_t* ids, int32_t n, int32_t 
   const bool inject = (flags & LRL_STEP_INJECT_UNIFORM) != 0;
   if (inject && n > 0 && !s->S.inj_reset) return fail(LRL_E_INVALID, "injected reset uniforms not set");
   HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, n, nullptr, root_mode, xy_lo, xy_span, x_off, y_off, inject ? 1 : 0,
-                            s->d_reset_ctr, (hipStream_t)stream));
+                            (hipStream_t)stream));
   return 0;
 }
 
@@ -603,7 +600,7 @@ int32_t lrl_sim_reset_idx_dev(lrl_sim* s, const int32_t* ids, int32_t nmax, cons
   if (!s || !dcount || nmax < 0 || (nmax > 0 && !ids)) return fail(LRL_E_INVALID, "null argument");
   if (root_mode < 0 || root_mode > 2) return fail(LRL_E_INVALID, "root_mode %d", root_mode);
   HIPCHECK(lrl_launch_reset(s->dk, &s->S, ids, nmax, dcount, root_mode, xy_lo, xy_span, x_off, y_off, 0,
-                            s->d_reset_ctr, (hipStream_t)stream));
+                            (hipStream_t)stream));
   return 0;
 }
 

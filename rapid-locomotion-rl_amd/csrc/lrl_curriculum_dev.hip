@@ -245,7 +245,14 @@ __global__ __launch_bounds__(CD_THREADS) void curriculum_dev_kernel(CurDevArgs a
   __shared__ CdLevels clev;
   const int t = threadIdx.x;
   const int n = min(*a.dcount, a.nmax);
-  if (n <= 0) return;  // (resample_commands returns before touching the generator)
+  if (n <= 0) {  // (resample_commands returns before touching the generator)
+    if (a.log_area && c.env_bins_f_prev) {  // the step's fresh log buffers keep the last reset batch's values
+      const int N0 = a.S.n;
+      for (int e = t; e < N0; e += CD_THREADS) c.env_bins_f[e] = c.env_bins_f_prev[e];
+      if (t == 0 && c.command_area_prev) c.command_area[0] = c.command_area_prev[0];
+    }
+    return;
+  }
   const KState& S = a.S;
   const int N = S.stride;
   if (t == 0) changed = 0;

@@ -73,6 +73,7 @@ struct KState {
       *last_root_vel, *commands, *obs, *priv, *hist, *rew;
   uint8_t *reset, *time_out, *last_contacts;
   int32_t* episode_length;
+  int32_t* reset_count;  // per-env reset_idx count: the reset draws' counter (independent of the sharding)
   float *episode_sums, *command_sums, *feet_air_time, *friction, *restitution, *payload, *com, *motor_strength,
       *kp, *kd, *env_origins, *base_lin_vel, *base_ang_vel, *projected_gravity, *joint_pos_target;
   float* heights;  // measured_heights [num_height_points][N]

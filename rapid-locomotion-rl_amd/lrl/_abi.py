@@ -113,7 +113,7 @@ class LrlDevCurriculum(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("weights", "cdf", "state", "mt_key", "ep_rew_lin", "ep_rew_ang", "env_bins",
                                           "env_bins_f", "command_area", "axes")] + \
                [("half", C.c_double * 3), ("nx", i32), ("ny", i32), ("nz", i32), ("words", C.c_void_p),
-                ("draws", C.c_void_p)]
+                ("draws", C.c_void_p), ("env_bins_f_prev", C.c_void_p), ("command_area_prev", C.c_void_p)]
 
 
 PPO_CTRL_BYTES = 64  # sizeof(lrl_ppo_ctrl): double lr, double loss_sum[3], float mb[4], float x4

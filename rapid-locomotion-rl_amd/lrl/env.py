@@ -44,12 +44,27 @@ class _LazyExtras(dict):
         super().__init__()
         self._env = env
         self._lazy = {}
+        self._cond = {}  # key -> (value, present()): an entry whose presence is decided on first access
 
     def set_lazy(self, key, fn):
+        self._cond.pop(key, None)
         self._lazy[key] = fn
         dict.pop(self, key, None)
 
+    def set_conditional(self, key, value, present):
+        """``key`` holds ``value`` if ``present()`` is true when the dict is first asked about it (membership, a read,
+        keys()); otherwise the key is absent for this step."""
+        self._lazy.pop(key, None)
+        dict.pop(self, key, None)
+        self._cond[key] = (value, present)
+
+    def _resolve(self, key):
+        c = self._cond.pop(key, None)
+        if c is not None and c[1]():
+            dict.__setitem__(self, key, c[0])
+
     def _get(self, key):
+        self._resolve(key)
         fn = self._lazy.pop(key, None)
         if fn is not None:  # materialise once: later reads return the same array
             dict.__setitem__(self, key, fn())
@@ -60,20 +75,26 @@ class _LazyExtras(dict):
 
     def __setitem__(self, key, value):
         self._lazy.pop(key, None)
+        self._cond.pop(key, None)
         dict.__setitem__(self, key, value)
 
     def __delitem__(self, key):
-        if self._lazy.pop(key, None) is None:
+        found = self._cond.pop(key, None) is not None
+        found = self._lazy.pop(key, None) is not None or found
+        if dict.__contains__(self, key):
             dict.__delitem__(self, key)
+        elif not found:
+            raise KeyError(key)
 
     def __contains__(self, key):
+        self._resolve(key)
         return dict.__contains__(self, key) or key in self._lazy
 
     def __iter__(self):
         return iter(self.keys())
 
     def __len__(self):
-        return dict.__len__(self) + len(self._lazy)
+        return len(self.keys())
 
     def get(self, key, default=None):
         return self._get(key) if key in self else default
@@ -88,6 +109,8 @@ class _LazyExtras(dict):
         raise KeyError(key)
 
     def keys(self):
+        for k in list(self._cond):
+            self._resolve(k)
         return list(dict.keys(self)) + [k for k in self._lazy if not dict.__contains__(self, k)]
 
     def items(self):
@@ -144,7 +167,7 @@ class _Upload:
 
 class LeggedRobotEnv:
     def __init__(self, sim_device="cuda:0", headless=True, num_envs=None, prone=False, deploy=False, cfg=None,
-                 eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=0,
+                 eval_cfg=None, initial_dynamics_dict=None, physics_engine="SIM_PHYSX", seed=0, env_offset=None,
                  solver_iterations=None, legacy_fork=True, num_envs_global=None, device_resets=None):
         if cfg is None:
             from .config import Cfg as cfg
@@ -186,11 +209,14 @@ class LeggedRobotEnv:
         # data-parallel sharding: this sim holds global envs [env_offset, env_offset + num_envs) of
         # num_envs_global.  Every per-env draw is keyed by the global id and the env origins are the global grid's, so
         # a rank's envs evolve exactly as the same envs of one process holding all of them.  Default: equal shards over
-        # the initialised process group (the bench's layout), else env_offset + num_envs.
+        # the initialised process group (the bench's layout: env_offset = rank x num_envs), else env_offset + num_envs.
+        import torch.distributed as tdist
+        _pg = tdist.is_available() and tdist.is_initialized()
+        world = tdist.get_world_size() if _pg else 1
+        if env_offset is None:  # (a rank > 0 left at offset 0 would repeat rank 0's draws and origins)
+            env_offset = tdist.get_rank() * self.num_envs if _pg else 0
         self.env_offset = int(env_offset)
         if num_envs_global is None:
-            import torch.distributed as tdist
-            world = tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
             num_envs_global = max(self.num_envs * world, self.env_offset + self.num_envs) if self.env_offset or \
                 world > 1 else self.num_envs
         if num_envs_global < self.env_offset + self.num_envs:
@@ -660,7 +686,7 @@ class LeggedRobotEnv:
             tm.mark("entry")
         if not self.legacy_fork:  # _post_physics_step_callback resampling (legged_robot.py:578-581): the
             # envs whose episode length reaches a multiple of resampling_time in this step, before its rewards
-            interval = int(self.cfg.commands.resampling_time / self.dt)
+            interval = self._resample_interval()
             cached = self._due_next
             if cached is not None and cached[0] == self.episode_length_buf._version:
                 due, due_np = None, cached[1]  # known from the previous step's single device->host copy (the ids
@@ -754,6 +780,14 @@ class LeggedRobotEnv:
         for key in self._EXTRAS:
             ex.set_lazy(key, lambda key=key: read(key))
 
+    _INT32_MAX = 2 ** 31 - 1
+
+    def _resample_interval(self):
+        """resampling_time / dt in steps, clamped to int32 for the device launches: an interval past the int32 range
+        (e.g. the reference's eval settings, resampling_time = 1e9) is never reached by an int32 episode length, so
+        the clamp changes no decision."""
+        return min(int(self.cfg.commands.resampling_time / self.dt), self._INT32_MAX)
+
     def _step_device(self, actions, flags):
         """step() on the upstream path with every reset / resampling decision on the device (no host wait): the same
         launches and draws as the host path below (legged_robot.py:139-188, 227-290, 578-581, 595-626), with id lists
@@ -764,8 +798,9 @@ class LeggedRobotEnv:
         d = self._dcur
         n = self.num_envs
         vp = lambda t: C.c_void_p(t.data_ptr())
-        interval = int(self.cfg.commands.resampling_time / self.dt)
-        ep_len = min(self.cfg.env.max_episode_length, interval)
+        interval = self._resample_interval()
+        # (max_episode_length is a float, np.ceil's; an integral value either way, as the divisor of the tracking sums)
+        ep_len = int(min(self.cfg.env.max_episode_length, interval))
         lin_thr = self.cfg.commands.forward_curriculum_threshold * self.reward_scales["tracking_lin_vel"]
         ang_thr = self.cfg.commands.yaw_curriculum_threshold * self.reward_scales["tracking_ang_vel"]
         due, rst = d["ids"]
@@ -798,10 +833,32 @@ class LeggedRobotEnv:
             k = int(cnt[1].item())  # (the uniform command-range curriculum's step: once per episode length, host sync)
             if k:
                 self.update_command_curriculum(rst[:k].long(), cfg)
+        # This step's logged values land in fresh buffers (an empty reset batch copies the previous step's), so the
+        # dict published below holds values no later step overwrites, as the reference's fresh tensors per reset batch.
+        ex = self.extras
+        ep_host = dict.get(ex, "train/episode")
+        if ep_host is not None and ep_host is not d.get("ep"):  # continue from what the host path logged last (reset())
+            for i, k in enumerate(self.episode_sums):
+                v = ep_host.get("rew_" + k)
+                if isinstance(v, torch.Tensor) and v.numel() == 1:
+                    d["means"][i].copy_(v.reshape(()))
+            if "command_area" in ep_host:
+                d["command_area"].fill_(float(ep_host["command_area"]))
+            d["seen"] = True
+        desc = d["desc"]
+        bins_new = torch.empty_like(d["env_bins_f"])
+        area_new = torch.empty_like(d["command_area"])
+        desc.env_bins_f, desc.command_area = bins_new.data_ptr(), area_new.data_ptr()
+        desc.env_bins_f_prev, desc.command_area_prev = d["env_bins_f"].data_ptr(), d["command_area"].data_ptr()
         resample(rst, rst_n, 1)
+        desc.env_bins_f_prev = desc.command_area_prev = None
+        d["env_bins_f"], d["command_area"] = bins_new, area_new
         es = self._episode_sums
-        _abi.check(L.lrl_rows_mean_zero_dev(vp(es), C.c_int64(es.stride(0)), C.c_int32(es.shape[0]), vp(rst),
-                                            C.c_int32(n), rst_n, vp(d["means"]), C.c_int32(1), st))
+        R = es.shape[0]
+        pub = torch.empty(R + 1, device=self.device)  # [means of the last reset batch | terrain level]
+        _abi.check(L.lrl_rows_mean_zero_dev(vp(es), C.c_int64(es.stride(0)), C.c_int32(R), vp(rst), C.c_int32(n), rst_n,
+                                            vp(pub), vp(d["means"]), C.c_int32(1), st))
+        d["means"] = pub[:R]
         t = cfg.terrain
         _abi.check(L.lrl_sim_reset_idx_dev(sim, vp(rst), C.c_int32(n), rst_n, C.c_int32(self._root_mode()),
                                            C.c_float(float(t.x_init_range)),
@@ -810,27 +867,26 @@ class LeggedRobotEnv:
         _abi.check(L.lrl_sim_observe_idx_dev(sim, vp(rst), C.c_int32(n), rst_n, C.c_uint32(flags), st))
         self._due_next = None
         self._sums_host = None
-        ex = self.extras
-        ep = ex.get("train/episode")
-        if ep is None or ep is not d.get("ep"):  # views of the device buffers (the last reset batch's means), made once
-            if ep is not None:  # (continuing the means the host path logged last, e.g. by reset())
-                for i, k in enumerate(self.episode_sums):
-                    v = ep.get("rew_" + k)
-                    if isinstance(v, torch.Tensor) and v.numel() == 1:
-                        d["means"][i].copy_(v.reshape(()))
-                if "command_area" in ep:
-                    d["command_area"].fill_(float(ep["command_area"]))
-            ep = d["ep"] = {"rew_" + k: m for k, m in zip(self.episode_sums, d["means"].unbind(0))}
-            ex["train/episode"] = ep
+        ep = d["ep"] = {"rew_" + k: m for k, m in zip(self.episode_sums, pub[:R].unbind(0))}
         if cfg.terrain.curriculum and self.custom_origins:
-            torch.mean(self.terrain_levels[:self.num_train_envs].float(), out=d["level_mean"])
-            ep["terrain_level"] = d["level_mean"]
+            torch.mean(self.terrain_levels[:self.num_train_envs].float(), out=pub[R])
+            ep["terrain_level"] = pub[R]
         if c.command_curriculum:
-            self.env_command_bins_t = d["env_bins_f"]
-            ex["env_bins"] = d["env_bins_f"][:self.num_train_envs]
-            ep["command_area"] = d["command_area"][0]
+            self.env_command_bins_t = bins_new
+            ex["env_bins"] = bins_new[:self.num_train_envs]
+            ep["command_area"] = area_new[0]
         if c.yaw_command_curriculum:
             ep["max_command_yaw"] = cfg.command_ranges["ang_vel_yaw"][1]
+        if d.get("seen"):
+            ex["train/episode"] = ep
+        else:  # no reset logged yet: the key appears once one has been (the means are NaN until then), as the
+            # reference's extras gain it at the first reset batch; deciding that reads one device value, on access only
+            def seen(ep=ep, m0=pub[0]):
+                if bool(torch.isnan(m0).item()):
+                    return False
+                d["seen"] = True
+                return True
+            ex.set_conditional("train/episode", ep, seen)
         if cfg.env.send_timeouts:
             ex["time_outs"] = self.time_out_buf[:self.num_train_envs]
         ex["privileged_obs"] = self.privileged_obs_buf

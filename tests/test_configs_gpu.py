@@ -287,7 +287,7 @@ def _port():
     return p
 
 
-def _iteration(robot, rank, world, tmp, n=N_BENCH, rollout_only=False):
+def _iteration(robot, rank, world, tmp, n=N_BENCH, rollout_only=False, legacy_fork=True):
     """One Runner.learn iteration of ``robot`` at ``n`` envs for global rank ``rank`` (env_offset rank x n), the
     bench's setup.  The rollout the update sees (storage + the CUDA generator state its randperm draws from) and
     the initial parameters are written to ``tmp`` for the single-rank recomputation.  ``rollout_only``: the update is
@@ -300,7 +300,7 @@ def _iteration(robot, rank, world, tmp, n=N_BENCH, rollout_only=False):
     (lcfg.config_mini_cheetah if robot == "mc" else lcfg.config_go1)(cfg)
     cfg.env.num_envs = n
     R.RunnerArgs.save_interval = 0
-    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=1234, env_offset=rank * n))
+    env = HistoryWrapper(LeggedRobotEnv("cuda:0", cfg=cfg, seed=1234, env_offset=rank * n, legacy_fork=legacy_fork))
     torch.manual_seed(0)  # same initial weights on every rank (as DDP broadcasts them)
     runner = R.Runner(env, device="cuda:0", seed=1234)
     alg = runner.alg
@@ -358,12 +358,12 @@ STORE_KEYS = ["observations", "privileged_observations", "observation_histories"
               "actions_log_prob", "advantages", "mu", "sigma", "rewards", "dones"]
 
 
-def _rank_worker(rank, world, port, robot, tmp, out, n=N_BENCH, rollout_only=False):
+def _rank_worker(rank, world, port, robot, tmp, out, n=N_BENCH, rollout_only=False, legacy_fork=True):
     sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from ranks import init_rank
     init_rank(rank, world, port)
-    out[rank] = _iteration(robot, rank, world, tmp, n, rollout_only)
+    out[rank] = _iteration(robot, rank, world, tmp, n, rollout_only, legacy_fork)
     if world > 1:
         dist.destroy_process_group()
 
@@ -436,19 +436,21 @@ def test_multi_rank_full_iteration_at_bench_shape(robot, world):
 
 @pytest.mark.multiproc
 @pytest.mark.timeout(600)
-def test_rollout_does_not_depend_on_the_gpu_count():
+@pytest.mark.parametrize("legacy_fork,n", [(True, N_BENCH), (False, N_BENCH), (False, 128)])
+def test_rollout_does_not_depend_on_the_gpu_count(legacy_fork, n):
     """every draw is keyed by the global env id (env: env_offset; policy noise: PPO.row_offset) and the
     env origins are the global layout's, so 2 ranks x 2048 Mini Cheetah envs roll out exactly what 1 x 4096 does: a
     24-step Runner rollout's storage (observations, histories, actions, values, log-probs, means, rewards, dones,
     returns) and the final env state are bit-identical per global env; the advantages, normalised with all-reduced
-    statistics (another summation order), agree to fp32 rounding."""
+    statistics (another summation order), agree to fp32 rounding.  With the upstream resets (legacy_fork=False) the
+    reset draws too; at 128 envs some step resets envs of one shard only."""
     mgr = mp.Manager()
     one, two = mgr.dict(), mgr.dict()
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_rank_worker, args=(1, 0, "mc", tmp, one, N_BENCH, True), nprocs=1, join=True)
-        mp.spawn(_rank_worker, args=(2, _port(), "mc", tmp, two, N_BENCH // 2, True), nprocs=2, join=True)
+        mp.spawn(_rank_worker, args=(1, 0, "mc", tmp, one, n, True, legacy_fork), nprocs=1, join=True)
+        mp.spawn(_rank_worker, args=(2, _port(), "mc", tmp, two, n // 2, True, legacy_fork), nprocs=2, join=True)
     ref = one[0]
-    h = N_BENCH // 2
+    h = n // 2
     for k in STORE_KEYS + ["root", "dof_pos", "dof_vel", "contact", "hist", "origins"]:
         whole = ref[k]
         ax = 1 if k in STORE_KEYS else 0  # storage is [T, N, ...]
@@ -458,6 +460,12 @@ def test_rollout_does_not_depend_on_the_gpu_count():
             continue
         np.testing.assert_array_equal(parts, whole, err_msg=k)
     assert np.abs(ref["actions"][:, :h] - ref["actions"][:, h:]).max() > 0.1  # the halves are different envs
+    if not legacy_fork:  # upstream resets happened; at 128 envs some step resets envs of one shard only (ADVICE r4:
+        # the reset draws are keyed by each env's own reset count, not by a per-process counter that only that shard's
+        # resets advance)
+        d = ref["dones"].reshape(ref["dones"].shape[0], -1).astype(bool)
+        one_sided = (d[:, :h].any(1) != d[:, h:].any(1)).sum()
+        assert d.any() and (n > 128 or one_sided > 0), (d.sum(), one_sided)
 
 
 # ------------------------------------------------------------------------------------------ configs[0]

@@ -515,14 +515,16 @@ def test_extras_are_step_time_snapshots():
     env.close()
 
 
-@pytest.mark.parametrize("rough", [False, True])
-def test_device_reset_path_matches_host_path(rough):
+@pytest.mark.parametrize("rough,resampling_time", [(False, 0.14), (True, 0.14), (False, 0.5), (False, 1e9)])
+def test_device_reset_path_matches_host_path(rough, resampling_time):
     """The upstream step without a host round trip (LeggedRobotEnv._step_device: device id lists and counts, the
     command curriculum's update / sample on the device, lrl_sim_curriculum_resample_dev) against the host path
     (device_resets=False: one device->host copy per step, numpy / native-host curriculum) on the same seeds and actions:
     time-outs every 25 steps, resampling every 7, thresholds that pass (the weights change, the cdf cache is exercised),
     terrain curriculum on the rough tiles.  Every buffer, the curriculum (weights, MT19937 state, episode rewards), the
-    env bins, terrain levels / origins and the logged episode means are bit-identical."""
+    env bins, terrain levels / origins and the logged episode means are bit-identical.  resampling_time = 0.5 (the
+    episode length: ep_len = min(max_episode_length, interval) is the float max_episode_length) and 1e9 (the
+    reference's eval setting: an interval past int32) resample at resets only."""
     from lrl.env import LeggedRobotEnv
     n = 256
     cfgs = []
@@ -531,7 +533,7 @@ def test_device_reset_path_matches_host_path(rough):
         lcfg.config_go1(cfg)
         cfg.env.num_envs = n
         cfg.env.episode_length_s = 0.5
-        cfg.commands.resampling_time = 0.14
+        cfg.commands.resampling_time = resampling_time
         cfg.commands.forward_curriculum_threshold = 0.05
         cfg.commands.yaw_curriculum_threshold = 0.05
         if rough:
@@ -579,3 +581,40 @@ def test_device_reset_path_matches_host_path(rough):
     assert int(_np(host._reset_u8).sum()) >= 0
     for e in envs:
         e.close()
+
+
+def test_device_path_episode_log_is_not_overwritten():
+    """on the device reset path each step publishes extras['train/episode'] / extras['env_bins'] in fresh
+    buffers, so a dict a consumer keeps (the reference runner's logger.store_metrics(**infos['train/episode'])) still
+    holds the values of its own step after later steps; before any reset is logged the key is absent, as in the
+    reference, whose extras gain it at the first reset batch."""
+    from lrl.env import LeggedRobotEnv
+    n = 256
+    cfg = lcfg.make_cfg()
+    lcfg.config_go1(cfg)
+    cfg.env.num_envs = n
+    cfg.env.episode_length_s = 0.3
+    cfg.commands.resampling_time = 0.14
+    env = LeggedRobotEnv("cuda:0", cfg=cfg, seed=3, legacy_fork=False)
+    assert env._dev_path
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    act = lambda: torch.randn(n, 12, generator=g, device="cuda:0") * 0.3
+    env.step(act())
+    assert "train/episode" not in env.extras  # no reset yet (episodes are 15 steps long, nobody fell in one step)
+    kept = []
+    for s in range(40):
+        _, _, done, ex = env.step(act())
+        if "train/episode" in ex:
+            ep = ex["train/episode"]
+            now = {k: (float(v.item()) if isinstance(v, torch.Tensor) else float(v)) for k, v in ep.items()}
+            kept.append((s, ep, now, ex["env_bins"], ex["env_bins"].cpu().numpy().copy()))
+    assert len(kept) >= 30 and kept[0][0] <= 16
+    changed = 0
+    for s, ep, now, bins, bins_now in kept:
+        later = {k: (float(v.item()) if isinstance(v, torch.Tensor) else float(v)) for k, v in ep.items()}
+        for k in now:
+            assert later[k] == now[k] or (later[k] != later[k] and now[k] != now[k]), (s, k, now[k], later[k])
+        np.testing.assert_array_equal(bins.cpu().numpy(), bins_now)
+        changed += int(now != kept[-1][2])
+    assert changed > 0  # the logged values did move over the run
+    env.close()
