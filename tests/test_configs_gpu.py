@@ -319,6 +319,9 @@ def _iteration(robot, rank, world, tmp, n=N_BENCH, rollout_only=False, legacy_fo
         snap["cuda_rng"] = torch.cuda.get_rng_state()
         snap["init"] = init.cpu()
         snap["lr"] = alg.learning_rate
+        # the update's first draw is its minibatch permutation: replay it from the same generator state
+        snap["perm"] = torch.randperm(s.values.shape[0] * s.values.shape[1], device="cuda:0").cpu()
+        torch.cuda.set_rng_state(snap["cuda_rng"])
         torch.save(snap, os.path.join(tmp, f"rollout_{robot}_{rank}.pt"))
         return orig_update()
     alg.update = update
@@ -366,6 +369,20 @@ def _rank_worker(rank, world, port, robot, tmp, out, n=N_BENCH, rollout_only=Fal
     out[rank] = _iteration(robot, rank, world, tmp, n, rollout_only, legacy_fork)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _autograd_first_grad(paths):
+    """torch autograd of the reference's loss over minibatch 0 of each saved rank rollout (test_dist_gpu's helper),
+    from the rollouts' shared initial parameters."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from test_dist_gpu import ROLL_KEYS, autograd_union_grad
+    snaps = [torch.load(p, weights_only=True) for p in paths]
+    ac = ActorCritic(42, 18, 630, 12).cuda()
+    ac.flatten_parameters()
+    with torch.no_grad():
+        ac._flat.copy_(snaps[0]["init"].cuda())
+    rolls = [{k: sn[k].cuda() for k in ROLL_KEYS} for sn in snaps]
+    return autograd_union_grad(ac, rolls, [sn["perm"].numpy() for sn in snaps])
 
 
 def _single_rank_first_grad(path):
@@ -428,10 +445,17 @@ def test_multi_rank_full_iteration_at_bench_shape(robot, world):
             assert a["lr"] == b["lr"] and len(a["lr"]) == 20
             np.testing.assert_array_equal(a["post"], b["post"])
         single = [_single_rank_first_grad(os.path.join(tmp, f"rollout_{robot}_{r}.pt")) for r in range(world)]
+        g_ref, kl_ref = _autograd_first_grad([os.path.join(tmp, f"rollout_{robot}_{r}.pt") for r in range(world)])
     for r in range(world):
         np.testing.assert_allclose(res[r]["pre"], single[r], rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(a["post"] / world, sum(single) / world, rtol=1e-6, atol=1e-8)
     assert np.abs(single[0] - single[1]).max() > 1e-4
+    # pinned to the reference's loss as well: the all-reduced gradient / world is torch autograd's
+    # gradient of the mean minibatch-0 loss over every rank's rollout (one process holding all the envs)
+    got = a["post"][:-1] / world
+    err = np.abs(got - g_ref).max()
+    assert err <= 1e-4 * np.abs(g_ref).max() + 1e-7, (err, np.abs(g_ref).max())
+    np.testing.assert_allclose(a["post"][-1] / world, kl_ref, rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.multiproc

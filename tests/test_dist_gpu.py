@@ -53,12 +53,83 @@ def _worker(rank, world, port, out):
             return r
         return orig(t, *a, **k)
     dist.all_reduce = probe
+    perms = []
+    orig_rp = torch.randperm
+
+    def rp(*a, **k):  # the update's minibatch permutation (minibatch 0 = its first N * T / 4 entries)
+        r = orig_rp(*a, **k)
+        perms.append(r.detach().cpu().numpy().copy())
+        return r
+    torch.randperm = rp
     torch.manual_seed(5)  # same minibatch permutation on both ranks (as torch.randperm is seeded alike)
-    mv, ms, ma = alg.update()
-    dist.all_reduce = orig
+    try:
+        mv, ms, ma = alg.update()
+    finally:
+        dist.all_reduce = orig
+        torch.randperm = orig_rp
     flat = ac._flat.detach().cpu().numpy().copy()
-    out[rank] = (flat, list(alg.lr_trace), [mv, ms, ma], cap[0], cap[1])
+    out[rank] = (flat, list(alg.lr_trace), [mv, ms, ma], cap[0], cap[1], perms[0])
     dist.destroy_process_group()
+
+
+def _autograd_union_grad(perms, N=256, T=24):
+    """Torch autograd of the reference's PPO loss (ppo.py:98-147) over minibatch 0 of every rank's rollout: the mean
+    of the ranks' minibatch losses, i.e. one process holding all the ranks' envs.  Returns (flat gradient of the
+    policy parameters laid out as the native flat buffer's main range, KL mean)."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.ppo import PPO
+    from test_ppo_gpu import _random_storage, init_params
+    ac = ActorCritic(42, 18, 630, 12)
+    init_params(ac)
+    alg = PPO(ac.cuda(), device="cuda:0", fused=True)
+    rolls = []
+    for r in range(len(perms)):
+        alg.init_storage(N, T, [42], [18], [630], [12])
+        _random_storage(alg, N, T, seed=11 + r)
+        rolls.append({k: getattr(alg.storage, k).clone() for k in ROLL_KEYS})
+    return autograd_union_grad(alg.actor_critic, rolls, perms)
+
+
+ROLL_KEYS = ["observations", "privileged_observations", "actions", "values", "returns", "actions_log_prob",
+             "advantages", "mu", "sigma"]
+
+
+def autograd_union_grad(ac, rolls, perms):
+    """The reference's PPO loss (ppo.py:98-147) by torch autograd on ``ac`` (flattened, its current parameters), over
+    minibatch 0 (``perm[:N * T / 4]``) of each rollout in ``rolls`` (storage tensors [T, N, ...] by ROLL_KEYS name),
+    averaged over the rollouts: the gradient one process holding every rank's envs takes.  Returns (gradient of the
+    native flat buffer's main range, float64; the KL mean)."""
+    from lrl.ppo.ppo import PPO_Args
+    net = ac.flatten_parameters()
+    loss, kls = 0.0, []
+    for roll, perm in zip(rolls, perms):
+        T, N = roll["values"].shape[:2]
+        rows = torch.as_tensor(perm[:N * T // 4], device="cuda:0")
+        fl = lambda k: roll[k].flatten(0, 1)[rows]
+        obs, priv = fl("observations"), fl("privileged_observations")
+        act, tv, ret = fl("actions"), fl("values"), fl("returns")
+        oldlp, adv, omu, osig = fl("actions_log_prob"), fl("advantages"), fl("mu"), fl("sigma")
+        ac.act(obs, priv)
+        logp = ac.get_actions_log_prob(act)
+        value = ac.evaluate(obs, priv)
+        mu, sigma, ent = ac.action_mean, ac.action_std, ac.entropy
+        with torch.no_grad():
+            kls.append(torch.sum(torch.log(sigma / osig + 1.e-5) + (torch.square(osig) + torch.square(omu - mu)) /
+                                 (2.0 * torch.square(sigma)) - 0.5, axis=-1).mean().item())
+        ratio = torch.exp(logp - torch.squeeze(oldlp))
+        surr = torch.max(-torch.squeeze(adv) * ratio,
+                         -torch.squeeze(adv) * torch.clamp(ratio, 1 - PPO_Args.clip_param, 1 + PPO_Args.clip_param)).mean()
+        vc = tv + (value - tv).clamp(-PPO_Args.clip_param, PPO_Args.clip_param)
+        vl = torch.max((value - ret).pow(2), (vc - ret).pow(2)).mean()
+        loss = loss + (surr + vl - PPO_Args.entropy_coef * ent.mean()) / len(perms)
+    ac.zero_grad(set_to_none=True)
+    loss.backward()
+    g = torch.zeros(net.kl_slot - net.main_begin, dtype=torch.float64)
+    for name, prm in ac.named_parameters():
+        off = (prm.data_ptr() - ac._flat.data_ptr()) // 4 - net.main_begin
+        if prm.grad is not None and 0 <= off < g.numel():
+            g[off:off + prm.numel()] = prm.grad.detach().double().cpu().flatten()
+    return g.numpy(), float(np.mean(kls))
 
 
 def _single_process_first_grad(seed):
@@ -111,6 +182,14 @@ def test_two_rank_native_update_keeps_replicas_identical():
         np.testing.assert_allclose(out[r][4] / world, (single[0] + single[1]) / world, rtol=1e-6, atol=1e-9)
     np.testing.assert_array_equal(a[4], b[4])
     assert np.abs(single[0] - single[1]).max() > 1e-3  # the two rollouts really give different gradients
+    # ... and pinned to the reference's loss, not only to the native update itself: the
+    # all-reduced gradient / world is torch autograd's gradient of the mean minibatch-0 loss over both rollouts
+    g_ref, kl_ref = _autograd_union_grad([a[5], b[5]])
+    got = a[4][:-1] / world
+    assert got.shape == g_ref.shape
+    err = np.abs(got - g_ref).max()
+    assert err <= 1e-4 * np.abs(g_ref).max() + 1e-7, (err, np.abs(g_ref).max())
+    np.testing.assert_allclose(a[4][-1] / world, kl_ref, rtol=1e-4, atol=1e-7)
 
 
 def _curriculum_cfg(n):
