@@ -50,7 +50,7 @@ __device__ __forceinline__ int env_block() {
 // Phase timers (build with -DLRL_ENV_PROFILE; read with lrl_debug_env_profile): per-wave shader-clock
 // cycles of the step kernel's phases, summed over waves.
 #ifdef LRL_ENV_PROFILE
-__device__ unsigned long long g_env_prof[16];
+__device__ unsigned long long g_env_prof[24];
 #define LRL_PROF_DECL unsigned long long prof_t = clock64();
 #define LRL_PROF(i)                                   \
   {                                                   \
@@ -358,7 +358,11 @@ __device__ __forceinline__ V3 closest_on_tri(V3 p, V3 a, V3 b, V3 c, bool& face)
   return a + (vb * dn) * ab + (vc * dn) * ac;
 }
 // tv: this wave's LDS scratch for the 4 x 4 vertex block, [vertex][lane] float4 (conflict-free b128 accesses)
-__device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, float margin, float4* tv, int lane) {
+__device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, float margin, float4* tv, int lane,
+                              unsigned long long* prof) {
+#ifdef LRL_ENV_PROFILE
+  const unsigned long long tq_a = clock64();
+#endif
   THit h;
   h.sep = 1e30f;
   h.n = v3(0.f, 0.f, 1.f);
@@ -412,12 +416,20 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) tv[(4 * a + b) * BLOCK + lane] = V[a][b];
+#ifdef LRL_ENV_PROFILE
+  const unsigned long long tq_b = clock64();
+  prof[16] += tq_b - tq_a;  // vertex block gathers + staging
+  prof[19] += __popc(tris);  // marked triangles (summed over lanes)
+#endif
   float best = 3.0e38f;
   V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
   bool bface = true;
   int under = -1;  // height-field side of p from the triangle under it: 1 above / on, 0 below, -1 none found
   // each lane walks its own marked triangles in order (the wave runs max-over-lanes triangles, not 18)
   while (__any((int)(tris != 0u))) {
+#ifdef LRL_ENV_PROFILE
+    prof[18] += 1;  // walk iterations (per wave: the busiest lane's count)
+#endif
     if (tris) {
       const int k = __builtin_ctz(tris);
       tris &= tris - 1u;
@@ -450,6 +462,9 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
       }
     }
   }
+#ifdef LRL_ENV_PROFILE
+  prof[17] += clock64() - tq_b;  // the triangle walk
+#endif
   const float dist = sqrtf(best), sd = dot(bn, p - ba);
   const bool above = under >= 0 ? under == 1 : sd >= 0.f;
   h.sep = (above ? dist : -dist) - r;
@@ -1454,7 +1469,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
           const int s = __builtin_ctzll(mk);
           float* row = M.base + (M.sph_off + s * NSF) * ENVS + (L >> 2);
           const THit th = terrain_query(K, v3(row[6 * ENVS], row[7 * ENVS], row[8 * ENVS]), M.sph4(s).w,
-                                        P.contact_offset, tv, lane);
+                                        P.contact_offset, tv, lane, prof);
+#ifdef LRL_ENV_PROFILE
+          prof[20] += 1;  // query rounds of this lane (lane 0: the wave's rounds)
+#endif
 #ifdef LRL_ENV_DEBUG
           g_env_dbg[((size_t)(env_block() * ENVS + (L >> 2)) * 64 + s) * 8 + 1] = th.sep;
 #endif
@@ -1934,7 +1952,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   for (int s = 0; s < K->num_spheres; ++s)
     if (sph_owner(K, s) == ql) own |= 1ull << s;
   own |= 7ull << (nsph + 3 * ql);  // this leg's joint-limit rows
-  unsigned long long prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long prof[24] = {};
   LRL_PROF_DECL
 #ifdef LRL_ENV_PROFILE
   prof_t = kt0;
@@ -2388,7 +2406,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 #ifdef LRL_ENV_PROFILE
   prof[9] = clock64() - kt0;  // the wave's whole lifetime (the phases above should sum to it)
   if (lane == 0)
-    for (int i = 0; i < 16; ++i) atomicAdd(&g_env_prof[i], prof[i]);
+    for (int i = 0; i < 24; ++i) atomicAdd(&g_env_prof[i], prof[i]);
 #endif
 }
 
@@ -2396,12 +2414,12 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 
 extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
 #ifdef LRL_ENV_PROFILE
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -2;
   if (reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[24] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
   }
-  return 16;
+  return 24;
 #else
   (void)out;
   (void)reset;
@@ -2431,16 +2449,49 @@ namespace lrl {
 // obs / priv rows from the post-reset state with the step's noise draws, the newest history slot, and the
 // last_* buffers post_physics_step sets after the reset (last_actions = actions, last_dof_vel = dof_vel,
 // last_root_vel = root velocity).  One thread per listed env.
-__global__ void observe_kernel(const KParams* __restrict__ K, KState S, const int32_t* __restrict__ ids, int32_t n,
-                               const int32_t* __restrict__ dn, uint32_t flags, int64_t step_counter) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// 16 lanes per env (OBS_LANES): lane c forms, noises, clips and stores only its 4-wide chunks of the observation row
+// (chunk i0 / 4 on lane (i0 / 4) % 16: one Philox draw each instead of the whole row's draws on one thread), reading
+// the state entries those need; lane 0 writes the base-frame velocities, the privileged row and the last_* buffers.
+// Every element's value, draw and operation order are the one-thread form's (obs_values / obs_noise_clip), so the
+// rows are bit-identical.
+constexpr int OBS_LANES = 16;
+// observation entry i of env e (obs_values' layout: [lin vel, ang vel,] gravity, [commands,] dof pos, dof vel,
+// actions, then the height rows against base height z)
+__device__ __forceinline__ float obs_entry(const lrl_env_params& P, const KState& S, int e, int i, V3 blv, V3 bav,
+                                           V3 pg) {
+  const int N = S.stride;
+  int o = 0;
+  if (P.observe_vel) {
+    if (i < 3) return (i == 0 ? blv.x : i == 1 ? blv.y : blv.z) * P.obs_scale_lin_vel;
+    if (i < 6) return (i == 3 ? bav.x : i == 4 ? bav.y : bav.z) * P.obs_scale_ang_vel;
+    o = 6;
+  }
+  if (i < o + 3) return i == o ? pg.x : i == o + 1 ? pg.y : pg.z;
+  o += 3;
+  if (P.observe_command) {
+    if (i < o + 3) return S.commands[(i - o) * N + e] * P.commands_scale[i - o];
+    o += 3;
+  }
+  if (i < o + 12) return (S.dof_pos[(i - o) * N + e] - P.default_dof_pos[i - o]) * P.obs_scale_dof_pos;
+  if (i < o + 24) return S.dof_vel[(i - o - 12) * N + e] * P.obs_scale_dof_vel;
+  if (i < o + 36) return S.actions[(i - o - 24) * N + e];
+  const int k = i - (P.num_obs - P.num_height_points);  // height row k (measure_heights)
+  return fminf(fmaxf(S.root[2 * N + e] - 0.5f - S.heights[k * N + e], -1.f), 1.f) * P.obs_scale_height;
+}
+__global__ __launch_bounds__(256) void observe_kernel(const KParams* __restrict__ K, KState S,
+                                                      const int32_t* __restrict__ ids, int32_t n,
+                                                      const int32_t* __restrict__ dn, uint32_t flags,
+                                                      int64_t step_counter) {
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = gt / OBS_LANES, c = gt % OBS_LANES;
   if (t >= (dn ? min(*dn, n) : n)) return;  // (dn: device count, n its bound)
   const int e = ids[t];
   if (e < 0 || e >= S.n) return;
   const lrl_env_params& P = K->p;
   const int N = S.stride, NO = P.num_obs;
   const uint64_t genv = (uint64_t)(S.env_offset + e);
-  float quat[4], V[3], W[3], q[12], qd[12], act[12], cmd[4], ms[12];
+  const bool inject = (flags & LRL_STEP_INJECT_UNIFORM) != 0;
+  float quat[4], V[3], W[3];
 #pragma unroll
   for (int k = 0; k < 4; ++k) quat[k] = S.root[(3 + k) * N + e];
 #pragma unroll
@@ -2448,40 +2499,48 @@ __global__ void observe_kernel(const KParams* __restrict__ K, KState S, const in
     V[k] = S.root[(7 + k) * N + e];
     W[k] = S.root[(10 + k) * N + e];
   }
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    q[j] = S.dof_pos[j * N + e];
-    qd[j] = S.dof_vel[j * N + e];
-    act[j] = S.actions[j * N + e];
-    ms[j] = S.motor_strength[j * N + e];
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) cmd[k] = S.commands[k * N + e];
   const V3 blv = quat_rotate_inverse(quat, v3(V[0], V[1], V[2]));
   const V3 bav = quat_rotate_inverse(quat, v3(W[0], W[1], W[2]));
   const V3 pg = quat_rotate_inverse(quat, v3(0.f, 0.f, -1.f));
+  float* row = S.obs + (size_t)e * NO;
+  float* h = (flags & LRL_STEP_HISTORY) ? S.hist + (size_t)e * (K->num_history * NO) + (K->num_history - 1) * NO
+                                        : nullptr;
+  for (int i0 = 4 * c; i0 < NO; i0 += 4 * OBS_LANES) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i0 + k < NO ? obs_entry(P, S, e, i0 + k, blv, bav, pg) : 0.f;
+    if (P.add_noise) {  // (obs_noise_clip's chunk i0 / 4)
+      lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter,
+                               (LRL_RNG_OBS_NOISE << 16) ^ (uint32_t)(step_counter >> 32), (uint32_t)(i0 >> 2), S.seed);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + k;
+        if (i < NO) {
+          float u = inject ? (e < S.n ? S.inj_noise[(size_t)e * NO + i] : 0.5f) : lrl_u01(r.v[k]);
+          v[k] += (2.f * u - 1.f) * P.noise_vec[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k < NO) {
+        const float x = fminf(fmaxf(v[k], -P.clip_obs), P.clip_obs);
+        row[i0 + k] = x;
+        if (h) h[i0 + k] = x;
+      }
+  }
+  if (c != 0) return;
+  float ms[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) ms[j] = S.motor_strength[j * N + e];
   S.base_lin_vel[e] = blv.x; S.base_lin_vel[N + e] = blv.y; S.base_lin_vel[2 * N + e] = blv.z;
   S.base_ang_vel[e] = bav.x; S.base_ang_vel[N + e] = bav.y; S.base_ang_vel[2 * N + e] = bav.z;
   S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
-  float* ob = S.obs + (size_t)e * NO;
-  obs_values(P, blv, bav, pg, cmd, q, qd, act, ob);
-  if (P.measure_heights) {  // the step's measured_heights (taken before the reset) against the new base height
-    const int NP = P.num_height_points, NB = NO - NP;
-    const float z = S.root[2 * N + e];
-    for (int k = 0; k < NP; ++k)
-      ob[NB + k] = fminf(fmaxf(z - 0.5f - S.heights[k * N + e], -1.f), 1.f) * P.obs_scale_height;
-  }
-  obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, ob, 0, 1);
   priv_row(P, S, e, S.payload[e], v3(S.com[e], S.com[N + e], S.com[2 * N + e]), ms, S.priv + (size_t)e * LRL_NUM_PRIV);
-  if (flags & LRL_STEP_HISTORY) {
-    const int H = K->num_history * NO;
-    float* h = S.hist + (size_t)e * H + (H - NO);
-    for (int i = 0; i < NO; ++i) h[i] = ob[i];
-  }
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    S.last_actions[j * N + e] = act[j];
-    S.last_dof_vel[j * N + e] = qd[j];
+    S.last_actions[j * N + e] = S.actions[j * N + e];
+    S.last_dof_vel[j * N + e] = S.dof_vel[j * N + e];
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -2506,7 +2565,7 @@ extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int
 extern "C" hipError_t lrl_launch_observe(const KParams* K, const KState* S, const int32_t* ids, int32_t n,
                                          const int32_t* dn, uint32_t flags, int64_t step_counter, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(lrl::observe_kernel, dim3((n + 127) / 128), dim3(128), 0, stream, K, *S, ids, n, dn, flags,
-                     step_counter);
+  hipLaunchKernelGGL(lrl::observe_kernel, dim3((int)(((int64_t)n * lrl::OBS_LANES + 255) / 256)), dim3(256), 0, stream,
+                     K, *S, ids, n, dn, flags, step_counter);
   return hipGetLastError();
 }

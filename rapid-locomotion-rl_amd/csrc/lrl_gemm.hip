@@ -1026,8 +1026,7 @@ struct X6Op {
 // TAG: trace tag only (the weight-gradient shape, tn_shape_tag): each of the update's large weight gradients gets its own
 // symbol so a kernel trace / PMC pass keys its launches apart; the code is the same for every value
 template <int BM, int BN, int LAYOUT, int EPI, bool FAST, bool BGATHER, int TAG = 0>
-__global__ __launch_bounds__(GTHREADS, BM * BN > 128 * 128 ? 2 : 3) void gemm_x6_kernel(GemmP p) {
-  // (3 waves / SIMD: 3 workgroups per CU with 48 KB of LDS; the 256 x 128 tile (74 KB): 2)
+__global__ __launch_bounds__(GTHREADS, 3) void gemm_x6_kernel(GemmP p) {  // 3 waves / SIMD: 3 workgroups per CU (LDS 48 KB)
   constexpr bool AKC = (LAYOUT & 1) == 0, BKC = (LAYOUT & 2) == 0;
   constexpr int PA = BM * XBK, PB = BN * XBK, STG = 3 * (PA + PB);
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -1089,7 +1088,7 @@ __global__ __launch_bounds__(GTHREADS, BM * BN > 128 * 128 ? 2 : 3) void gemm_x6
         acc[i][j] = c;
       }
   };
-  if constexpr (LRL_X6_PIPE && FAST && BM * BN <= 128 * 128) {  // (the 256 x 128 tile: no room for 2 register sets)
+  if constexpr (LRL_X6_PIPE && FAST) {
   // Software pipeline: slice s + 1 waits split-ready in registers while slice s is multiplied, so its split (VALU)
   // and LDS stores interleave with slice s's MFMAs in one scheduling region; slice s + 2 is in flight meanwhile.
   float va[2][OA::NV], vb[2][OB::NV];
@@ -1277,42 +1276,6 @@ static int launch_x6_tile(const GemmP& p, int layout, int epi, int groups, hipSt
   return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
 }
 
-// NT / NN products on the 256 x 128 tile (wave tile 128 x 64: 4 x 2 MFMA tiles, the split of each staged element
-// shared by twice the MFMAs of the 128 x 128 tile); same per-element k order and product order, so bit-identical
-template <int BM, int BN>
-static int launch_x6_big(const GemmP& p, int layout, int epi, int groups, hipStream_t st) {
-  dim3 grid(((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * groups);
-  const bool bkc = (layout & 2) == 0;
-  const bool interior = p.M % BM == 0 && p.N % BN == 0 && p.K % XBK == 0 && p.avec == 4 && (!bkc || p.bvec == 4);
-#define LRL_X6B(L, E)                                                                                       \
-  do {                                                                                                      \
-    if (interior) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, L, E, true, false>), grid, dim3(GTHREADS), 0, st, p); \
-    else hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, L, E, false, false>), grid, dim3(GTHREADS), 0, st, p);        \
-  } while (0)
-  if (layout == GEMM_NT) {
-    if (epi == EPI_STORE) LRL_X6B(GEMM_NT, EPI_STORE);
-    else if (epi == EPI_BIAS) LRL_X6B(GEMM_NT, EPI_BIAS);
-    else if (epi == EPI_BIAS_ELU) LRL_X6B(GEMM_NT, EPI_BIAS_ELU);
-    else return LRL_E_INVALID;
-  } else if (layout == GEMM_NN) {
-    if (epi == EPI_STORE) LRL_X6B(GEMM_NN, EPI_STORE);
-    else if (epi == EPI_DELU) LRL_X6B(GEMM_NN, EPI_DELU);
-    else return LRL_E_INVALID;
-  } else {
-    return LRL_E_INVALID;
-  }
-#undef LRL_X6B
-  return hipGetLastError() == hipSuccess ? 0 : LRL_E_HIP;
-}
-// LRL_X6_BIG (development switch): 1 = the 256 x 128 tile for the large NT / NN products
-static int x6_big_mode() {
-  static const int m = [] {
-    const char* e = getenv("LRL_X6_BIG");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
 // x6 path switch: LRL_GEMM_X6=0 keeps every product on the fp32 MFMA kernels (A/B comparisons)
 static bool x6_enabled() {
   static const int on = [] {
@@ -1360,12 +1323,6 @@ static int try_x6(const GemmP& p, int layout, int epi, int groups, hipStream_t s
     const int bm = wg128 >= 512 ? 128 : 64;
     // the same tile on the LDS-DMA kernel where the tiles are interior
     if (int dr = try_x6d(p, layout, epi, groups, bm, bn, st)) return dr;
-    if (x6_big_mode() >= 1 && bm == 128 && bn == 128 && p.M % 256 == 0 && p.avec == 4 && p.a_rows == nullptr &&
-        (layout == GEMM_NT || x6_big_mode() == 2) &&
-        (int64_t)(p.M / 256) * (p.N / 128) * groups >= 256) {
-      rc = launch_x6_big<256, 128>(p, layout, epi, groups, st);
-      return rc ? rc : 1;
-    }
     if (bm == 128 && bn == 128) rc = launch_x6_tile<128, 128>(p, layout, epi, groups, st);
     else if (bm == 128) rc = launch_x6_tile<128, 64>(p, layout, epi, groups, st);
     else if (bn == 128) rc = launch_x6_tile<64, 128>(p, layout, epi, groups, st);

@@ -34,11 +34,11 @@ runner = R.Runner(env, device="cuda:0", seed=1234)
 runner.learn(2, init_at_random_ep_len=True)
 torch.cuda.synchronize()
 L = _abi.lib()
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 24)()
 L.lrl_debug_env_profile(buf, 1)
 runner.learn(iters)
 torch.cuda.synchronize()
-assert L.lrl_debug_env_profile(buf, 0) == 16, "library built without LRL_ENV_PROFILE"
+assert L.lrl_debug_env_profile(buf, 0) >= 16, "library built without LRL_ENV_PROFILE"
 K = 24 * iters
 waves = (n + 15) // 16
 names = ["kin+dyn+detect", "schur+free acc", "delassus+warm", "PGS", "integrate", "start+state load", "post-physics",

@@ -25,7 +25,7 @@ if which == "go1_rough":
 env = LeggedRobotEnv("cuda:0", cfg=cfg, num_envs=n)
 env.reset()
 L = _abi.lib()
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 24)()
 g = torch.Generator(device="cuda:0").manual_seed(0)
 for _ in range(50):
     env.step(float(os.environ.get("LRL_ASTD", "0.5")) * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
@@ -35,7 +35,7 @@ K = 100
 for _ in range(K):
     env.step(float(os.environ.get("LRL_ASTD", "0.5")) * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
 torch.cuda.synchronize()
-assert L.lrl_debug_env_profile(buf, 0) == 16, "library built without LRL_ENV_PROFILE"
+assert L.lrl_debug_env_profile(buf, 0) >= 16, "library built without LRL_ENV_PROFILE"
 waves = (n + 15) // 16  # quad layout: 16 envs per wave
 names = ["kin+dyn+detect", "schur+free acc", "delassus+warm", "PGS", "integrate", "start+state load", "post-physics",
          "tiles+history", "PD torques"]
@@ -50,5 +50,9 @@ if which != "go1_rough" and buf[14]:
 if which == "go1_rough" and buf[15]:
     print(f"  terrain queries {buf[14] / waves / K:10.0f} cycles/wave/step  ({buf[15] / waves / K:.1f} per lane, "
           f"{buf[14] / buf[15]:.0f} cycles each; part of kin+dyn+detect)")
+if which == "go1_rough" and buf[20]:
+    print(f"  query rounds    {buf[20] / waves / K:10.2f} per wave and step; per round: gathers {buf[16] / buf[20]:.0f} "
+          f"cycles, walk {buf[17] / buf[20]:.0f} cycles over {buf[18] / buf[20]:.1f} iterations "
+          f"({buf[17] / max(buf[18], 1):.0f} cycles each); lane 0 marked {buf[19] / buf[20]:.1f} triangles per query")
 print(f"total {tot / waves / K:.0f} cycles/wave/step (wave lifetime {buf[9] / waves / K:.0f}); "
       f"resets/step {env._reset_u8.float().mean().item():.3f}")
