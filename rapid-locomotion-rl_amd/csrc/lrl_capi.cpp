@@ -326,7 +326,7 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   lds_contacts += params->terrain_mesh ? 16 * LRL_ENV_LANES * 16 : LRL_NUM_DOF * 19 * wg_envs * 4;
   lds_contacts += (4 * (int)(sizeof(KLeg) / 4) + 5 * model->num_spheres) * 4;  // staged model tables (Lds::ktab)
   lds_contacts += (40 + s->hk.self_npairs + 1) * 4;  // + the self-collision groups and pairs
-  if (params->terrain_mesh) lds_contacts += LRL_ENV_LANES * 12;  // + the terrain query work list (Lds::wl)
+  if (params->terrain_mesh) lds_contacts += LRL_ENV_LANES * 20;  // + the terrain query work list (Lds::wl)
   int lds_tiles = (NO + LRL_NUM_PRIV + LRL_MAX_REWARD_TERMS) * wg_envs * 4;  // obs / priv tiles + reward rows
   s->lds_bytes = lds_contacts > lds_tiles ? lds_contacts : lds_tiles;
   if (s->lds_bytes > 160 * 1024) return fail(LRL_E_INVALID, "LDS budget exceeded (%d B)", s->lds_bytes);

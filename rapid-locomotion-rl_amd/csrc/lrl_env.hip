@@ -193,7 +193,8 @@ struct Lds {
                    // K->leg[4], then per sphere (x, y, z, radius), then per sphere its link (int)
   int nsph;
   int lim_off;     // field offset of the joint-limit rows (LIM_* map below contact_pgs_q)
-  float* wl;       // terrain query work list (after the staged tables): [BLOCK] candidate masks, [BLOCK] offsets
+  float* wl;       // terrain query work list (after the staged tables): [BLOCK] candidate masks, [BLOCK] offsets,
+                   // [BLOCK] masks of the candidates found in contact
   __device__ __forceinline__ float* wlist() const { return wl; }
   __device__ __forceinline__ const KLeg& kleg(int l) const { return reinterpret_cast<const KLeg*>(ktab)[l]; }
   __device__ __forceinline__ float4 sph4(int s) const {
@@ -335,7 +336,9 @@ __device__ __forceinline__ V3 terr_v(const float* __restrict__ vtx, int idx) {
   const float4 v = reinterpret_cast<const float4*>(vtx)[idx];
   return v3(v.x, v.y, v.z);
 }
-// closest point of triangle (a, b, c) to p (Voronoi regions, Ericson 5.1.5); face = p projects inside
+// closest point of triangle (a, b, c) to p (Voronoi regions, Ericson 5.1.5); face = p projects inside.  The region
+// ratios use the hardware reciprocal (1 ulp) instead of the IEEE division sequence (≈ 10 instructions each): a few
+// 1e-9 m at these distances, far inside the oracle's 1e-5 m nearest-triangle margin
 __device__ __forceinline__ V3 closest_on_tri(V3 p, V3 a, V3 b, V3 c, bool& face) {
   face = false;
   const V3 ab = b - a, ac = c - a, ap = p - a;
@@ -345,16 +348,17 @@ __device__ __forceinline__ V3 closest_on_tri(V3 p, V3 a, V3 b, V3 c, bool& face)
   const float d3 = dot(ab, bp), d4 = dot(ac, bp);
   if (d3 >= 0.f && d4 <= d3) return b;
   const float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + (d1 / (d1 - d3)) * ab;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + (d1 * __builtin_amdgcn_rcpf(d1 - d3)) * ab;
   const V3 cp = p - c;
   const float d5 = dot(ab, cp), d6 = dot(ac, cp);
   if (d6 >= 0.f && d5 <= d6) return c;
   const float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + (d2 / (d2 - d6)) * ac;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + (d2 * __builtin_amdgcn_rcpf(d2 - d6)) * ac;
   const float va = d3 * d6 - d5 * d4;
-  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + ((d4 - d3) / ((d4 - d3) + (d5 - d6))) * (c - b);
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f)
+    return b + ((d4 - d3) * __builtin_amdgcn_rcpf((d4 - d3) + (d5 - d6))) * (c - b);
   face = true;
-  const float dn = 1.f / (va + vb + vc);
+  const float dn = __builtin_amdgcn_rcpf(va + vb + vc);
   return a + (vb * dn) * ab + (vc * dn) * ac;
 }
 // tv: this wave's LDS scratch for the 4 x 4 vertex block, [vertex][lane] float4 (conflict-free b128 accesses)
@@ -422,8 +426,7 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   prof[19] += __popc(tris);  // marked triangles (summed over lanes)
 #endif
   float best = 3.0e38f;
-  V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
-  bool bface = true;
+  int bk = -1;     // the nearest triangle so far (its closest point / normal are formed once, after the walk)
   int under = -1;  // height-field side of p from the triangle under it: 1 above / on, 0 below, -1 none found
   // each lane walks its own marked triangles in order (the wave runs max-over-lanes triangles, not 18)
   while (__any((int)(tris != 0u))) {
@@ -452,15 +455,24 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
         const V3 q = closest_on_tri(p, va, b, cv, face);
         const V3 dq = p - q;
         const float d2 = dot(dq, dq);
-        if (d2 < best) {
-          best = d2;
-          bc = q;
-          bn = rsqrtf(a2) * nf;
-          ba = va;
-          bface = face;
-        }
+        bk = d2 < best ? k : bk;
+        best = fminf(d2, best);
       }
     }
+  }
+  // the winner's closest point, face region and unit normal: the same evaluation once more
+  V3 bc = v3(0.f, 0.f, 0.f), bn = v3(0.f, 0.f, 1.f), ba = v3(0.f, 0.f, 0.f);
+  bool bface = true;
+  if (bk >= 0) {
+    const int c = bk >> 1, di = c / 3, dj = c - 3 * di;
+    const int ia = 4 * di + dj;
+    const int ib = (bk & 1) ? ia + 4 : ia + 5, ic = (bk & 1) ? ia + 5 : ia + 1;
+    const float4 fa = tv[ia * BLOCK + lane], fb = tv[ib * BLOCK + lane], fc = tv[ic * BLOCK + lane];
+    const V3 va = v3(fa.x, fa.y, fa.z), b = v3(fb.x, fb.y, fb.z), cv = v3(fc.x, fc.y, fc.z);
+    const V3 nf = cross(b - va, cv - va);
+    bc = closest_on_tri(p, va, b, cv, bface);
+    bn = rsqrtf(dot(nf, nf)) * nf;
+    ba = va;
   }
 #ifdef LRL_ENV_PROFILE
   prof[17] += clock64() - tq_b;  // the triangle walk
@@ -1454,8 +1466,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       const int total = __shfl(inc, BLOCK - 1, BLOCK);
       uint64_t* wl_mask = reinterpret_cast<uint64_t*>(M.wlist());
       int* wl_off = reinterpret_cast<int*>(wl_mask + BLOCK);
+      uint64_t* wl_hit = reinterpret_cast<uint64_t*>(wl_off + BLOCK);  // candidates found in contact, per owner lane
       wl_mask[lane] = cand;
       wl_off[lane] = inc - cnt;
+      wl_hit[lane] = 0ull;
       __syncthreads();
       float4* tv = reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS);
       for (int j = lane; j - lane < total; j += BLOCK) {
@@ -1481,17 +1495,18 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
             row[3 * ENVS] = th.n.x;
             row[4 * ENVS] = th.n.y;
             row[5 * ENVS] = th.n.z;
+            atomicOr(reinterpret_cast<unsigned long long*>(wl_hit + L), 1ull << s);
           }
         }
       }
       __syncthreads();
-      for (uint64_t m = cand; m;) {
+      // the owners activate only their candidates found in contact (the wave walks max-over-lanes contacts, not
+      // max-over-lanes candidates)
+      for (uint64_t m = wl_hit[lane]; m;) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        const float sep = M.sph(s, 9);
-        if (sep < P.contact_offset)
-          activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), sep,
-                   mulT(R, v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5))));
+        activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), M.sph(s, 9),
+                 mulT(R, v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5))));
       }
 #ifdef LRL_ENV_PROFILE
       prof[15] += cnt;
