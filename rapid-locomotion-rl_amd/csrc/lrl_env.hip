@@ -224,6 +224,10 @@ struct Lds {
   __device__ __forceinline__ float Di(int l, int k) const { return leg(l, 36 + k); }
 };
 
+// reciprocal on the hardware v_rcp_f32 (1 ulp) instead of the IEEE division sequence (≈ 10 instructions): the
+// physics sub-step's divisions are all of this form; the fp64 oracle bounds the result, not bit identity
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 __device__ __forceinline__ void chol6(float* L) {
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -232,7 +236,7 @@ __device__ __forceinline__ void chol6(float* L) {
     for (int k = 0; k < j; ++k) s -= L[LI(j, k)] * L[LI(j, k)];
     float d = sqrtf(fmaxf(s, 1e-12f));
     L[LI(j, j)] = d;
-    float inv = 1.f / d;
+    float inv = frcp(d);
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       float t = L[LI(i, j)];
@@ -247,7 +251,7 @@ __device__ __forceinline__ void chol6(float* L) {
 __device__ __forceinline__ void chol_to_inverse6(float* L) {
   float Li[21];
 #pragma unroll
-  for (int j = 0; j < 6; ++j) Li[LI(j, j)] = 1.f / L[LI(j, j)];
+  for (int j = 0; j < 6; ++j) Li[LI(j, j)] = frcp(L[LI(j, j)]);
 #pragma unroll
   for (int i = 1; i < 6; ++i)
 #pragma unroll
@@ -286,7 +290,7 @@ __device__ __forceinline__ void sym3inv(const float* D, float* Di) {
   float a = D[0], b = D[3], c = D[4], d = D[1], e = D[5], f = D[2];
   float c00 = d * f - e * e, c01 = c * e - b * f, c02 = b * e - c * d;
   float det = a * c00 + b * c01 + c * c02;
-  float id = 1.f / det;
+  float id = frcp(det);
   Di[0] = c00 * id;
   Di[3] = c01 * id;
   Di[4] = c02 * id;
@@ -379,7 +383,12 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   // clamped for the load; cells off the grid are never marked), staged in LDS for the triangle walk
   const float4* __restrict__ vtx = reinterpret_cast<const float4*>(K->terr_vtx);
   const float hmax = K->terr_hmax[ci * Cn + cj];
-  if (p.z - r - margin > hmax) return h;  // (before the block: a lane that leaves here issues none of its 16 gathers)
+  if (p.z - r - margin > hmax) {  // (before the block: a lane that leaves here issues none of its 16 gathers)
+#ifdef LRL_ENV_PROFILE
+    prof[21] += 1;  // queries that end at the max-height test
+#endif
+    return h;
+  }
   float4 V[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
@@ -605,7 +614,7 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
       W[d][e] = w;
       W[e][d] = w;
     }
-  const float id = 1.f / (W[1][1] * W[2][2] - W[1][2] * W[2][1]);
+  const float id = frcp(W[1][1] * W[2][2] - W[1][2] * W[2][1]);
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
 #pragma unroll
@@ -616,7 +625,7 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
     M.sph(s, SF_H + 3 * d) = h[d].x; M.sph(s, SF_H + 3 * d + 1) = h[d].y; M.sph(s, SF_H + 3 * d + 2) = h[d].z;
     M.sph(s, SF_E + 3 * d) = ev[d].x; M.sph(s, SF_E + 3 * d + 1) = ev[d].y; M.sph(s, SF_E + 3 * d + 2) = ev[d].z;
   }
-  M.sph(s, 3) = 1.f / W[0][0];
+  M.sph(s, 3) = frcp(W[0][0]);
   M.sph(s, 4) = W[1][0];
   M.sph(s, 5) = W[2][0];
   M.sph(s, 6) = W[2][2] * id;  // (W_tt)^-1: 11, 12, 22
@@ -783,7 +792,7 @@ __device__ __forceinline__ void limit_setup(const Lds& M, const float* Si, int r
   row[LIM_E * ENVS] = sg * c0;
   row[(LIM_E + 1) * ENVS] = sg * c1;
   row[(LIM_E + 2) * ENVS] = sg * c2;
-  row[LIM_IW * ENVS] = 1.f / w;
+  row[LIM_IW * ENVS] = frcp(w);
 }
 
 // warm start of a limit row in its owner lane with the carried impulse: v_b += lam z (summed over the quad by the
@@ -933,7 +942,7 @@ __device__ __forceinline__ float self_geom_c(const KParams* __restrict__ K, V3 c
   if (!box) {
     const V3 d = ca - cb;
     const float dd = dot(d, d), dist = sqrtf(dd);
-    n = dd > 1e-18f ? (1.f / dist) * d : v3(0.f, 0.f, 1.f);
+    n = dd > 1e-18f ? frcp(dist) * d : v3(0.f, 0.f, 1.f);
     x = 0.5f * ((ca - ra * n) + (cb + rb * n));
     return dist - ra - rb;
   }
@@ -944,7 +953,7 @@ __device__ __forceinline__ float self_geom_c(const KParams* __restrict__ K, V3 c
   const float dd = dot(d, d);
   if (dd > 0.f) {  // centre outside the box: nearest surface point
     const float dist = sqrtf(dd);
-    n = (1.f / dist) * d;
+    n = frcp(dist) * d;
     x = q + bc;
     return dist - ra;
   }
@@ -1042,7 +1051,7 @@ __device__ __forceinline__ SelfGate self_gate(const KParams* __restrict__ K, con
 __device__ void self_detect(const KParams* __restrict__ K, const Lds& M, const SphLegs& SL, int ql, unsigned live,
                             float dt, float rest, uint64_t& active, uint64_t& sown) {
   const lrl_env_params& P = K->p;
-  const float co = P.contact_offset;
+  const float co = P.contact_offset, idt = frcp(dt);
   const int* G = M.sgrp() + 10 * ql;
   const uint64_t freem = free_spheres(M, quad_or(active));
   const int cap = min(LRL_SELF_SLOTS, __builtin_popcountll(freem) >> 1);  // the env's slots
@@ -1093,7 +1102,7 @@ __device__ void self_detect(const KParams* __restrict__ K, const Lds& M, const S
           if (j <= ka) u0 += dot(cross(M.a(la, j), x - M.o(la, j)), n) * M.leg(la, 45 + j);
           if (lb >= 0 && j <= kb) u0 -= dot(cross(M.a(lb, j), x - M.o(lb, j)), n) * M.leg(lb, 45 + j);
         }
-        float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+        float tgt = sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity);
         if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
         const SRow row = self_row(M, freem, slot);
         row[SR_N + 0] = n.x; row[SR_N + 1] = n.y; row[SR_N + 2] = n.z;
@@ -1174,7 +1183,7 @@ __device__ void self_setup(const Lds& M, const float* Si, const M3& R, uint64_t 
     }
   // a relative Jacobian of zero (contact point on the joint axes) leaves an inert row
   const float det = W[1][1] * W[2][2] - W[1][2] * W[2][1];
-  const float id = det > 1e-12f ? 1.f / det : 0.f;
+  const float id = det > 1e-12f ? frcp(det) : 0.f;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
 #pragma unroll
@@ -1190,7 +1199,7 @@ __device__ void self_setup(const Lds& M, const float* Si, const M3& R, uint64_t 
     row[SR_F + 3 * d] = fw.x; row[SR_F + 3 * d + 1] = fw.y; row[SR_F + 3 * d + 2] = fw.z;
     row[SR_LAM + d] = 0.f;
   }
-  row[SR_IW] = W[0][0] > 1e-12f ? 1.f / W[0][0] : 0.f;
+  row[SR_IW] = W[0][0] > 1e-12f ? frcp(W[0][0]) : 0.f;
   row[SR_IW + 1] = W[1][0];
   row[SR_IW + 2] = W[2][0];
   row[SR_IW + 3] = W[2][2] * id;
@@ -1259,7 +1268,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
   const SphLegs SL = sph_legs(K);
   const lrl_env_params& P = K->p;
-  const float dt = P.sim_dt;
+  const float dt = P.sim_dt, idt = frcp(dt);
   const M3 R = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
   const V3 wb = mulT(R, v3(st.W[0], st.W[1], st.W[2]));
   const V3 vb = mulT(R, v3(st.V[0], st.V[1], st.V[2])) - cross(wb, cb);
@@ -1301,7 +1310,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       for (int j = 0; j < 3; ++j) u = u + st.qd[j] * c[j];
     }
     const float u0 = dot(nb, u);
-    float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+    float tgt = sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity);
     if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
     M.sph(s, 9) = tgt;
   };
@@ -1346,7 +1355,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
           if (j <= link) u = u + st.qd[j] * cross(aa[j], x - oo[j]);
       }
       const float u0 = dot(Rz, u);
-      float tgt = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+      float tgt = sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity);
       if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
       M.sph(s, 9) = tgt;
     }
@@ -1527,7 +1536,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         active |= 1ull << (M.nsph + 3 * ql + j);
         float* const row = M.lm(3 * ql + j);
         row[LIM_SG * ENVS] = up ? -1.f : 1.f;
-        row[LIM_B * ENVS] = sep >= 0.f ? -sep / dt : fminf(-P.baumgarte * sep / dt, P.max_depenetration_velocity);
+        row[LIM_B * ENVS] = sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity);
       }
     }
   }
@@ -1742,7 +1751,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   if (th > 1e-12f) {
     float sn, cs;
     sincosf(0.5f * th, &sn, &cs);
-    const float k = sn / wn;
+    const float k = sn * frcp(wn);
     dq[0] = w.x * k; dq[1] = w.y * k; dq[2] = w.z * k; dq[3] = cs;
   } else {
     dq[0] = 0.5f * dt * w.x; dq[1] = 0.5f * dt * w.y; dq[2] = 0.5f * dt * w.z; dq[3] = 1.f;
@@ -1750,7 +1759,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   const float x1 = st.quat[0], y1 = st.quat[1], z1 = st.quat[2], w1 = st.quat[3];
   float nq[4] = {w1 * dq[0] + x1 * dq[3] + y1 * dq[2] - z1 * dq[1], w1 * dq[1] - x1 * dq[2] + y1 * dq[3] + z1 * dq[0],
                  w1 * dq[2] + x1 * dq[1] - y1 * dq[0] + z1 * dq[3], w1 * dq[3] - x1 * dq[0] - y1 * dq[1] - z1 * dq[2]};
-  const float inv = 1.f / sqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+  const float inv = rsqrtf(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
 #pragma unroll
   for (int k = 0; k < 4; ++k) st.quat[k] = nq[k] * inv;
   const M3 R2 = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
