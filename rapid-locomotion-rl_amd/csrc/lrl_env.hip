@@ -418,10 +418,16 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
       const bool cell = i >= 0 && i <= R - 2 && j >= 0 && j <= Cn - 2;
       const float4 A = V[di][dj], B = V[di][dj + 1], Cc = V[di + 1][dj], D = V[di + 1][dj + 1];
       // t = 0: (v(i,j), v(i+1,j+1), v(i,j+1)) = (A, D, B);  t = 1: (v(i,j), v(i+1,j), v(i+1,j+1)) = (A, Cc, D)
-      const bool t0 = cell && p.x >= fminf(fminf(A.x, D.x), B.x) - g && p.x <= fmaxf(fmaxf(A.x, D.x), B.x) + g &&
-                      p.y >= fminf(fminf(A.y, D.y), B.y) - g && p.y <= fmaxf(fmaxf(A.y, D.y), B.y) + g;
-      const bool t1 = cell && p.x >= fminf(fminf(A.x, Cc.x), D.x) - g && p.x <= fmaxf(fmaxf(A.x, Cc.x), D.x) + g &&
-                      p.y >= fminf(fminf(A.y, Cc.y), D.y) - g && p.y <= fmaxf(fmaxf(A.y, Cc.y), D.y) + g;
+      // ... and that p is not more than g above everywhere (its distance exceeds g, so it decides no contact),
+      // except a triangle whose plain bounding box holds p's xy (it may be the one under p, which sets the side)
+      auto mark = [&](float4 a, float4 b, float4 c) {
+        const float x0 = fminf(fminf(a.x, b.x), c.x), x1 = fmaxf(fmaxf(a.x, b.x), c.x);
+        const float y0 = fminf(fminf(a.y, b.y), c.y), y1 = fmaxf(fmaxf(a.y, b.y), c.y);
+        const bool in = p.x >= x0 && p.x <= x1 && p.y >= y0 && p.y <= y1;
+        const bool high = p.z - g > fmaxf(fmaxf(a.z, b.z), c.z);
+        return cell && p.x >= x0 - g && p.x <= x1 + g && p.y >= y0 - g && p.y <= y1 + g && (in || !high);
+      };
+      const bool t0 = mark(A, D, B), t1 = mark(A, Cc, D);
       const int k = 2 * (3 * di + dj);
       tris |= (t0 ? 1u << k : 0u) | (t1 ? 2u << k : 0u);
     }
