@@ -1486,6 +1486,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       wl_off[lane] = inc - cnt;
       wl_hit[lane] = 0ull;
       __syncthreads();
+#ifdef LRL_ENV_PROFILE
+      prof[22] += clock64() - tq0;  // scan + work-list publication
+#endif
       float4* tv = reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS);
       for (int j = lane; j - lane < total; j += BLOCK) {
         if (j < total) {
@@ -1515,6 +1518,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         }
       }
       __syncthreads();
+#ifdef LRL_ENV_PROFILE
+      const unsigned long long ta0 = clock64();
+#endif
       // the owners activate only their candidates found in contact (the wave walks max-over-lanes contacts, not
       // max-over-lanes candidates)
       for (uint64_t m = wl_hit[lane]; m;) {
@@ -1523,6 +1529,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), M.sph(s, 9),
                  mulT(R, v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5))));
       }
+#ifdef LRL_ENV_PROFILE
+      prof[23] += clock64() - ta0;  // activation of the contacts
+#endif
 #ifdef LRL_ENV_PROFILE
       prof[15] += cnt;
 #endif

@@ -55,5 +55,7 @@ if which == "go1_rough" and buf[20]:
           f"cycles, walk {buf[17] / buf[20]:.0f} cycles over {buf[18] / buf[20]:.1f} iterations "
           f"({buf[17] / max(buf[18], 1):.0f} cycles each); lane 0 marked {buf[19] / buf[20]:.1f} triangles per query, "
           f"{buf[21] / buf[20]:.2f} of its queries ended at the max-height test")
+    print(f"  scan+publish    {buf[22] / waves / K:10.0f} cycles/wave/step; activation {buf[23] / waves / K:.0f}; "
+          f"rounds outside the query {(buf[14] - buf[22] - buf[23] - buf[16] - buf[17]) / waves / K:.0f}")
 print(f"total {tot / waves / K:.0f} cycles/wave/step (wave lifetime {buf[9] / waves / K:.0f}); "
       f"resets/step {env._reset_u8.float().mean().item():.3f}")
