@@ -32,11 +32,27 @@
 // cross-lane shuffles; the Gauss-Seidel sweep and the integration run redundantly in the 4 lanes (so
 // every lane holds the full env state); post-physics runs in lane 0 of each env.
 #define QL 4
+// Plane build (lrl_env_flat.hip includes this file with LRL_ENV_FLAT_TU): 4 envs per wave, 16 lanes per env = 4
+// mirrored quads.  Every quad of an env runs the quad code above on the same data (identical values, identical
+// stores), and the per-sphere work — ground detection and Delassus row setup — is split over the 4 quads (a lane
+// takes every 4th of the spheres its leg owns), so those loops run a quarter of the spheres per lane; the wave's
+// loops over max-over-envs contact counts run over 4 envs instead of 16; 1,024 single-wave workgroups fill every
+// SIMD of the chip (the 16-env form leaves 3 of each CU's 4 SIMDs idle).  The terrain-mesh build keeps 16 envs per
+// wave: its rows do not fit 4 workgroups' LDS per CU.
+#ifdef LRL_ENV_FLAT_TU
+#define ENVS LRL_ENV_WG_ENVS_FLAT
+#define LRL_ENV_NS flat
+#else
 #define ENVS (BLOCK / QL)
+#define LRL_ENV_NS mesh
+#endif
+#define MIRROR (BLOCK / (QL * ENVS))  // quads per env
+static_assert(MIRROR == 1 || MIRROR == 4, "an env has one quad or four mirrored quads");
 #define NSF 67  // LDS fields per contact sphere (map above contact_setup)
 #define LIMF 19  // LDS fields per joint-limit row (map above limit_setup)
 
 namespace lrl {
+inline namespace LRL_ENV_NS {
 
 // XCD-aware env blocks: the hardware deals workgroup ids round-robin over the 8 XCDs, so block b is renumbered to
 // the env block it covers with consecutive env blocks on one XCD.  A wave's SoA field access is 16 envs x 4 B = half
@@ -691,6 +707,41 @@ __device__ __forceinline__ uint64_t quad_or(uint64_t v) {
   hi |= qperm<0x4E>(hi);
   return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
+// OR over the env's lanes: the quad, then (MIRROR 4) the env's 4 quads = one DPP row of 16 lanes: row_mirror pairs
+// quad q with quad 3 - q, row_half_mirror quad 0 with 1 and 2 with 3 (after the quad OR every lane of a quad holds
+// the same value, so the lane pairing inside the quads does not matter)
+__device__ __forceinline__ uint64_t env_or(uint64_t v) {
+  v = quad_or(v);
+  if constexpr (MIRROR > 1) {
+    int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    lo |= qperm<0x140>(lo);
+    hi |= qperm<0x140>(hi);
+    lo |= qperm<0x141>(lo);
+    hi |= qperm<0x141>(hi);
+    v = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+  }
+  return v;
+}
+// sum over the env's lanes (used where at most one lane holds a non-zero term, or small integers: exact in any order)
+__device__ __forceinline__ float env_sum(float v) {
+  v = quad_sum(v);
+  if constexpr (MIRROR > 1) {
+    v += qperm<0x140>(v);
+    v += qperm<0x141>(v);
+  }
+  return v;
+}
+// mirrored quad qi of this lane (0 with one quad per env)
+__device__ __forceinline__ int mirror_quad() { return MIRROR > 1 ? (int)((threadIdx.x >> 2) & (MIRROR - 1)) : 0; }
+// the spheres / limit rows of `own` that mirrored quad qi detects and builds rows for: every MIRROR-th in bit order
+__device__ __forceinline__ uint64_t own_split(uint64_t own, int qi) {
+  if constexpr (MIRROR == 1) return own;
+  uint64_t r = 0;
+  int k = 0;
+  for (uint64_t m = own; m; m &= m - 1ull, ++k)
+    if ((k & (MIRROR - 1)) == qi) r |= m & (~m + 1ull);
+  return r;
+}
 // The Gauss-Seidel update with the base velocity spread over the env's quad: lane q holds v_b[q] (vo0) and, for
 // q < 2, v_b[q + 4] (vo1, 0 in lanes 2 and 3), and owns component q < 3 of the leg accumulators Y_L.  Each lane
 // forms its part of the three contact-velocity rows, one quad sum gives every lane the same u, the cone
@@ -1077,7 +1128,7 @@ __device__ void self_detect(const KParams* __restrict__ K, const Lds& M, const S
   const int c0 = quad_bcast_i(cnt, 0), c1 = quad_bcast_i(cnt, 1), c2 = quad_bcast_i(cnt, 2);
   if (stats) {
     const int total = c0 + c1 + c2 + quad_bcast_i(cnt, 3);
-    if (ql == 0 && total > 0) {  // per env and sub-step: pairs in contact, pairs without a slot
+    if (ql == 0 && mirror_quad() == 0 && total > 0) {  // per env and sub-step: pairs in contact, pairs without a slot
       atomicAdd(stats + 0, 1u);
       atomicAdd(stats + 1, (uint32_t)total);
       if (total > cap) {
@@ -1268,7 +1319,7 @@ __device__ __forceinline__ void self_pgs_q(const Lds& M, uint64_t freem, int k, 
 
 template <bool TERR>
 __device__ void substep(const KParams* __restrict__ K, Body& st, const float* tau3, float mb, const float* Ib, V3 cb,
-                        float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own,
+                        float mu, float rest, const Lds& M, uint64_t& active, int ql, uint64_t own, uint64_t odet,
                         float mu_s, float rest_s, unsigned long long* prof) {
   LRL_PROF_DECL
   const uint64_t prev_active = active;  // spheres in contact during the previous sub-step (warm start)
@@ -1367,10 +1418,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     }
   };
   for (int s = ql; s < K->base_sph_end; s += QL)
-  {
-    const float4 sp = M.sph4(s);
-    detect(s, v3(sp.x, sp.y, sp.z), sp.w, -1, 0, nullptr, nullptr);
-  }
+    if (MIRROR == 1 || ((odet >> s) & 1ull)) {
+      const float4 sp = M.sph4(s);
+      detect(s, v3(sp.x, sp.y, sp.z), sp.w, -1, 0, nullptr, nullptr);
+    }
 
   // ---- this lane's leg ----
   SI Aleg;     // composite inertia of the leg about the base origin
@@ -1405,7 +1456,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       const int sb = sel4(SL.b, l);
       const int se = sel4(SL.e, l);
       for (int s = sb; s < se; ++s)
-        if (M.slink(s) == j) {
+        if (M.slink(s) == j && (MIRROR == 1 || ((odet >> s) & 1ull))) {
           const float4 sp = M.sph4(s);
           const V3 x = o + mul(Rj, v3(sp.x, sp.y, sp.z));
           detect(s, x, sp.w, l, j, aa, oo);
@@ -1564,7 +1615,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   for (int k = 0; k < 6; ++k) A.i[k] += quad_sum(Aleg.i[k]);
   Cb = Cb + SV{v3(quad_sum(Cleg.a.x), quad_sum(Cleg.a.y), quad_sum(Cleg.a.z)),
                v3(quad_sum(Cleg.l.x), quad_sum(Cleg.l.y), quad_sum(Cleg.l.z))};
-  active = quad_or(active);
+  active = env_or(active);
+  if constexpr (MIRROR > 1) __syncthreads();  // sphere centres / targets of the other quads' detections
   LRL_PROF(0)  // kinematics, composite inertias, leg blocks, RNEA, contact detection
   // base block A (6x6) + Schur complement, Cholesky in registers
   Sch[LI(0, 0)] += A.i[0]; Sch[LI(1, 1)] += A.i[1]; Sch[LI(2, 2)] += A.i[2];
@@ -1655,7 +1707,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   // Delassus rows of the active spheres, each in the lane that owns the sphere (only spheres active in some
   // env of the wave are visited)
   // (each lane walks its own active spheres: the 4 legs' rows are built at the same time)
-  for (uint64_t m = active & own; __any((int)(m != 0ull));) {
+  for (uint64_t m = active & odet; __any((int)(m != 0ull));) {
     if (m) {
       const int s = __builtin_ctzll(m);
       m &= m - 1ull;
@@ -1903,7 +1955,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   extern __shared__ float lds[];
   const lrl_env_params& P = K->p;
   const int lane = threadIdx.x;
-  const int es = lane >> 2, ql = lane & 3;  // env slot, owned leg
+  const int es = lane / (QL * MIRROR), ql = lane & 3;  // env slot, owned leg
   const int blk = env_block();
   const int e = blk * ENVS + es;
   const int N = S.stride;
@@ -1991,6 +2043,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   for (int s = 0; s < K->num_spheres; ++s)
     if (sph_owner(K, s) == ql) own |= 1ull << s;
   own |= 7ull << (nsph + 3 * ql);  // this leg's joint-limit rows
+  const uint64_t odet = own_split(own, mirror_quad());  // of those, the ones this quad detects / builds rows for
   unsigned long long prof[24] = {};
   LRL_PROF_DECL
 #ifdef LRL_ENV_PROFILE
@@ -2029,7 +2082,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       tau3[j] = fminf(fmaxf(t, -lim3[j]), lim3[j]);
     }
     LRL_PROF(8)  // PD torques
-    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, mu_s, rest_s, prof);
+    if (physics) substep<TERR>(K, st, tau3, mb, Ib, cb, mu, rest, M, active, ql, own, odet, mu_s, rest_s, prof);
 #ifdef LRL_ENV_PROFILE
     prof_t = clock64();
 #endif
@@ -2071,9 +2124,9 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 #pragma unroll
   for (int f = 0; f < 4; ++f) ff[f][0] = ff[f][1] = ff[f][2] = 0.f;
   const float inv_dt = 1.f / P.sim_dt;
-  // bodies spread over the env's 4 lanes, then OR / sums over the quad (each foot is one lane's body, so its
-  // force sums exactly with three zeros)
-  for (int b = ql; b < K->num_bodies; b += QL) {
+  // bodies spread over the env's lanes, then OR / sums over them (each foot is one lane's body, so its force sums
+  // exactly with zeros)
+  for (int b = lane & (QL * MIRROR - 1); b < K->num_bodies; b += QL * MIRROR) {
     float fx = 0.f, fy = 0.f, fz = 0.f;
     if (physics) {
       for (int s = K->body_sph_begin[b]; s < K->body_sph_end[b]; ++s)
@@ -2124,13 +2177,12 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     for (int f = 0; f < 4; ++f)
       if (fs == f) { ff[f][0] = fx; ff[f][1] = fy; ff[f][2] = fz; }
   }
-  rst |= qperm<0xB1>(rst);
-  rst |= qperm<0x4E>(rst);
-  collision = quad_sum(collision);
+  rst = env_or((uint64_t)rst) != 0ull;
+  collision = env_sum(collision);
 #pragma unroll
   for (int f = 0; f < 4; ++f)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) ff[f][c] = quad_sum(ff[f][c]);
+    for (int c = 0; c < 3; ++c) ff[f][c] = env_sum(ff[f][c]);
   __syncthreads();  // LDS contact rows are dead from here on; the obs tile reuses them
   LRL_PROF(10)  // contact forces per body
   const int NO = P.num_obs;
@@ -2159,8 +2211,8 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     }
     hsum = quad_sum(hsum);
   }
-  // post-physics, observations and the state write-back: lane 0 of each env
-  if (ql == 0) {
+  // post-physics, observations and the state write-back: lane 0 of each env (of its first quad)
+  if (ql == 0 && mirror_quad() == 0) {
 
   // ---- post_physics_step ----
   int32_t eplen = S.episode_length[e] + 1;
@@ -2417,9 +2469,10 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   S.time_out[e] = (uint8_t)tout;
   S.rew[e] = rew;
   }  // ql == 0
-  // observation noise + clip, the row's 4-entry chunks spread over the env's 4 lanes
+  // observation noise + clip, the row's 4-entry chunks spread over the env's lanes
   __syncthreads();
-  obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, otile + es * NO, ql, QL);
+  obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, otile + es * NO,
+                 lane & (QL * MIRROR - 1), QL * MIRROR);
 
   LRL_PROF(6)  // contact forces + post_physics_step + SoA write-back
   // ---- AoS tiles (obs, priv) and the history shift: coalesced over the wave's contiguous rows ----
@@ -2449,11 +2502,50 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 #endif
 }
 
+}  // namespace LRL_ENV_NS
 }  // namespace lrl
 
-extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
+#ifdef LRL_ENV_FLAT_TU
+// the plane build's entry points (lrl_env_flat.hip); lrl_launch_env_step & co. below dispatch to them
+extern "C" int lrl_debug_env_profile_flat(unsigned long long* out, int reset) {
 #ifdef LRL_ENV_PROFILE
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[24] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 24;
+#else
+  (void)out;
+  (void)reset;
+  return 0;
+#endif
+}
+
+extern "C" hipError_t lrl_env_kernel_setup_flat(int lds_bytes) {
+  return hipFuncSetAttribute((const void*)lrl::env_step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             lds_bytes);
+}
+
+extern "C" hipError_t lrl_launch_env_step_flat(const KParams* K, const KState* S, int lds_bytes, const float* actions,
+                                               uint32_t flags, int64_t step_counter, hipStream_t stream) {
+  hipLaunchKernelGGL(lrl::env_step_kernel<false>, dim3(S->stride / ENVS), dim3(BLOCK), lds_bytes, stream, K, *S,
+                     actions, flags, step_counter);
+  return hipGetLastError();
+}
+#else
+extern "C" int lrl_debug_env_profile_flat(unsigned long long* out, int reset);
+extern "C" hipError_t lrl_env_kernel_setup_flat(int lds_bytes);
+extern "C" hipError_t lrl_launch_env_step_flat(const KParams* K, const KState* S, int lds_bytes, const float* actions,
+                                               uint32_t flags, int64_t step_counter, hipStream_t stream);
+
+// the sum of the two builds' timers (a simulation runs one of them)
+extern "C" int lrl_debug_env_profile(unsigned long long* out, int reset) {
+#ifdef LRL_ENV_PROFILE
+  unsigned long long f[24];
+  if (lrl_debug_env_profile_flat(f, reset) != 24) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lrl::g_env_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -2;
+  for (int i = 0; i < 24; ++i) out[i] += f[i];
   if (reset) {
     unsigned long long z[24] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lrl::g_env_prof), z, sizeof(z)) != hipSuccess) return -2;
@@ -2476,14 +2568,14 @@ extern "C" int lrl_debug_env_buffer(float* buf) {
 }
 
 extern "C" hipError_t lrl_env_kernel_setup(int lds_bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)lrl::env_step_kernel<false>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  hipError_t e = lrl_env_kernel_setup_flat(lds_bytes);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)lrl::env_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              lds_bytes);
 }
 
 namespace lrl {
+inline namespace LRL_ENV_NS {
 // compute_observations for envs just reset inside a step (upstream semantics, legged_robot.py:177-184):
 // obs / priv rows from the post-reset state with the step's noise draws, the newest history slot, and the
 // last_* buffers post_physics_step sets after the reset (last_actions = actions, last_dof_vel = dof_vel,
@@ -2587,17 +2679,14 @@ __global__ __launch_bounds__(256) void observe_kernel(const KParams* __restrict_
     S.last_root_vel[(3 + k) * N + e] = W[k];
   }
 }
+}  // namespace LRL_ENV_NS
 }  // namespace lrl
 
 extern "C" hipError_t lrl_launch_env_step(const KParams* K, const KState* S, int lds_bytes, const float* actions,
                                           uint32_t flags, int64_t step_counter, int terrain_mesh, hipStream_t stream) {
-  int blocks = S->stride / ENVS;
-  if (terrain_mesh)
-    hipLaunchKernelGGL(lrl::env_step_kernel<true>, dim3(blocks), dim3(BLOCK), lds_bytes, stream, K, *S, actions, flags,
-                       step_counter);
-  else
-    hipLaunchKernelGGL(lrl::env_step_kernel<false>, dim3(blocks), dim3(BLOCK), lds_bytes, stream, K, *S, actions,
-                       flags, step_counter);
+  if (!terrain_mesh) return lrl_launch_env_step_flat(K, S, lds_bytes, actions, flags, step_counter, stream);
+  hipLaunchKernelGGL(lrl::env_step_kernel<true>, dim3(S->stride / ENVS), dim3(BLOCK), lds_bytes, stream, K, *S,
+                     actions, flags, step_counter);
   return hipGetLastError();
 }
 
@@ -2608,3 +2697,4 @@ extern "C" hipError_t lrl_launch_observe(const KParams* K, const KState* S, cons
                      K, *S, ids, n, dn, flags, step_counter);
   return hipGetLastError();
 }
+#endif  // LRL_ENV_FLAT_TU

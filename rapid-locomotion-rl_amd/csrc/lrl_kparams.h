@@ -14,6 +14,10 @@
 #ifndef LRL_ENV_LANES
 #define LRL_ENV_LANES 64
 #endif
+// envs per workgroup: the terrain-mesh kernel keeps one quad per env (16 envs per wave); the plane kernel runs 4 envs
+// per wave, 16 lanes (4 mirrored quads) per env (lrl_env.hip, lrl_env_flat.hip)
+#define LRL_ENV_WG_ENVS_MESH (LRL_ENV_LANES / 4)
+#define LRL_ENV_WG_ENVS_FLAT (LRL_ENV_LANES / 16)
 
 struct KLeg {
   float xyz[3][3];   // joint origin in the parent frame

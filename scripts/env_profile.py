@@ -36,7 +36,8 @@ for _ in range(K):
     env.step(float(os.environ.get("LRL_ASTD", "0.5")) * torch.randn(n, 12, device="cuda:0", generator=g), _history=True)
 torch.cuda.synchronize()
 assert L.lrl_debug_env_profile(buf, 0) >= 16, "library built without LRL_ENV_PROFILE"
-waves = (n + 15) // 16  # quad layout: 16 envs per wave
+epw = 16 if which == "go1_rough" else 4  # envs per wave: the mesh kernel 16, the plane kernel 4 (16 lanes per env)
+waves = (n + epw - 1) // epw
 names = ["kin+dyn+detect", "schur+free acc", "delassus+warm", "PGS", "integrate", "start+state load", "post-physics",
          "tiles+history", "PD torques"]
 tot = sum(buf[:9])

@@ -5,7 +5,7 @@
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd "$ROOT/rapid-locomotion-rl_amd/csrc"
-for f in lrl_env.hip lrl_aux.hip lrl_gae.hip lrl_gemm.hip lrl_ppo.hip lrl_curriculum_dev.hip; do
+for f in lrl_env.hip lrl_env_flat.hip lrl_aux.hip lrl_gae.hip lrl_gemm.hip lrl_ppo.hip lrl_curriculum_dev.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast-honor-pragmas --cuda-device-only \
     -Rpass-analysis=kernel-resource-usage -c "$f" -o /tmp/lrl_res_$$.o 2>&1 |
     sed -n 's/.*remark: *//p' | sed 's/ \[-Rpass-analysis=kernel-resource-usage\]//' |
