@@ -399,18 +399,20 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   // clamped for the load; cells off the grid are never marked), staged in LDS for the triangle walk
   const float4* __restrict__ vtx = reinterpret_cast<const float4*>(K->terr_vtx);
   const float hmax = K->terr_hmax[ci * Cn + cj];
-  if (p.z - r - margin > hmax) {  // (before the block: a lane that leaves here issues none of its 16 gathers)
-#ifdef LRL_ENV_PROFILE
-    prof[21] += 1;  // queries that end at the max-height test
-#endif
-    return h;
-  }
+  // the block's 16 gathers are issued with the max-height word, not after its test: one memory round trip per query
+  // instead of two (a query that ends at the test has fetched its block for nothing — L2-resident terrain)
   float4 V[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int vi = min(max(ci - 1 + a, 0), R - 1);
 #pragma unroll
     for (int b = 0; b < 4; ++b) V[a][b] = vtx[vi * Cn + min(max(cj - 1 + b, 0), Cn - 1)];
+  }
+  if (p.z - r - margin > hmax) {
+#ifdef LRL_ENV_PROFILE
+    prof[21] += 1;  // queries that end at the max-height test
+#endif
+    return h;
   }
   // local frame at vertex (ci, cj): differences of nearby fp32 coordinates are exact (Sterbenz), so the walk
   // resolves distances to ~1e-8 m instead of the ~2e-6 m ulp of world coordinates 20-40 m from the origin
