@@ -319,7 +319,7 @@ def main():
     value = steps_total / elapsed
     if rank == 0:
         achieved = B_ENV * ENVS_PER_GPU / (k_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic("lrl::env_step_kernel<false>", "lrl::env_step_kernel")
+        traffic, traffic_src = pmc_traffic("lrl::flat::env_step_kernel<false>", "lrl::env_step_kernel<false>")
         # update's largest product: actor/critic layer-2 weight gradient, 2 x (256 x 512) over the minibatch rows
         mb_rows = ENVS_PER_GPU * R.RunnerArgs.num_steps_per_env // 4
         gemm_flop = 2.0 * 2 * 256 * 512 * mb_rows
@@ -356,13 +356,13 @@ def main():
             "env_step_kernel_ms": round(k_ms, 4),
             "self_contact": dict(sc, note="one untimed PPO iteration after the timed ones; a pair without a slot is "
                                           "one PhysX would solve and this solver skips in that sub-step (DESIGN.md §4)"),
-            "roofline": {"bound": "hbm", "kernel": "lrl::env_step_kernel<false> (plane ground)", "achieved": round(achieved, 3),
+            "roofline": {"bound": "hbm", "kernel": "lrl::flat::env_step_kernel<false> (plane ground)", "achieved": round(achieved, 3),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "note": f"algorithmic {B_ENV} B/env-step x {ENVS_PER_GPU} envs per launch (+ the newest history "
                                  f"slot, 168 B/env-step; the older slots move in the separate shift_history_kernel launch "
-                                 "before it); the kernel is latency-bound (4 lanes per env, one single-wave workgroup "
-                                 "per 16 envs, the slowest wave sets the launch), see DESIGN.md"},
+                                 "before it); the kernel is latency-bound (16 lanes per env = 4 mirrored quads, one single-wave "
+                                 "workgroup per 4 envs, 1,024 waves; the slowest wave sets the launch), see DESIGN.md"},
             "roofline_update_gemm": {
                 "bound": "mfma", "kernel": f"{gemm_kernel} (dW2: 2 x 256x512, {mb_rows} rows)",
                 "achieved": round(gemm_tf, 2) if gemm_tf else None, "peak": round(X6_PEAK_TF, 1),

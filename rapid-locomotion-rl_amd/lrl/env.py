@@ -498,7 +498,7 @@ class LeggedRobotEnv:
 
     @property
     def reset_buf(self):
-        return self._reset_u8.bool()
+        return self._reset_u8.view(torch.bool)
 
     @property
     def time_out_buf(self):
@@ -743,7 +743,7 @@ class LeggedRobotEnv:
         self._register_extras(ex)
         if tm is not None:
             tm.mark("extras")
-        return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
+        return self.obs_buf, self.rew_buf, self._reset_u8.view(torch.bool), self.extras
 
     # rows of lrl_sim_extras_snapshot (include/lrl.h LRL_EXTRAS_*): key -> (first row, rows)
     _EXTRAS_ROWS = 77
@@ -869,7 +869,7 @@ class LeggedRobotEnv:
         self._sums_host = None
         ep = d["ep"] = {"rew_" + k: m for k, m in zip(self.episode_sums, pub[:R].unbind(0))}
         if cfg.terrain.curriculum and self.custom_origins:
-            torch.mean(self.terrain_levels[:self.num_train_envs].float(), out=pub[R])
+            torch.mean(self.terrain_levels[:self.num_train_envs], dim=0, dtype=torch.float32, out=pub[R])  # (one kernel)
             ep["terrain_level"] = pub[R]
         if c.command_curriculum:
             self.env_command_bins_t = bins_new
@@ -892,7 +892,7 @@ class LeggedRobotEnv:
         ex["privileged_obs"] = self.privileged_obs_buf
         ex["joint_vel_target"] = torch.zeros(12)
         self._register_extras(ex)
-        return self.obs_buf, self.rew_buf, self._reset_u8.bool(), self.extras
+        return self.obs_buf, self.rew_buf, self._reset_u8.view(torch.bool), self.extras
 
     def kernel_timing(self, start):
         """Env-kernel launch time, the one definition bench.py and the scripts use: HIP events around each
