@@ -257,11 +257,13 @@ def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True,
 
 
 @pytest.mark.parametrize("robot,n,steps", [("mc", 256, 1), ("go1", 256, 1), ("mc", 4096, 1), ("go1", 4096, 1),
-                                           ("mc", 256, 24), ("go1", 256, 24), ("mc", 4096, 10)])
+                                           ("mc", 256, 24), ("go1", 256, 24), ("mc", 4096, 10), ("mc", 1001, 3),
+                                           ("go1", 37, 3)])
 def test_physics_matches_oracle(robot, n, steps):
     """The fused step kernel's physics against the fp64 oracle over 1, 10 or 24 steps (a PPO rollout's length),
-    re-synchronised to the oracle's state before every step, at test grids and at the bench's 4096-env launch grid
-    (256 workgroups).  Every env of every step within the tolerances of helpers.within_tolerance except the envs
+    re-synchronised to the oracle's state before every step, at test grids, at the bench's 4096-env launch grid
+    (1,024 four-env workgroups on the plane) and at ragged env counts (1,001 and 37: a last workgroup with padded
+    env slots).  Every env of every step within the tolerances of helpers.within_tolerance except the envs
     the oracle reports on a contact-model discontinuity (at most MAX_EXCLUDED per step)."""
     _physics_vs_oracle(robot, n, steps)
 
