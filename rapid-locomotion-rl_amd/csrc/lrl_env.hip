@@ -2057,10 +2057,11 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   // 'P': kp3 / kd3 = gains x Kp / Kd factors, tg3 = position target; 'V': kp3 / kd3 = the bare gains, tg3 = the
   // scaled action (a velocity target), lqd3 = last_dof_vel (constant over the sub-steps: post_physics_step sets it);
   // 'T': tg3 = the scaled action (a torque)
-  float kp3[3], kd3[3], tg3[3], lim3[3], tau3[3];
+  float kp3[3], kd3[3], tg3[3], lim3[3], tau3[3], act3[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int jj = 3 * ql + j;
+    act3[j] = act[jj];  // (the clipped actions of this lane's joints: its share of the state write-back)
     const bool pos = ctl == 0;
     kp3[j] = pos ? P.p_gains[jj] * kpf3[j] : P.p_gains[jj];
     kd3[j] = pos ? P.d_gains[jj] * kdf3[j] : P.d_gains[jj];
@@ -2213,16 +2214,32 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     }
     hsum = quad_sum(hsum);
   }
-  // post-physics, observations and the state write-back: lane 0 of each env (of its first quad)
-  if (ql == 0 && mirror_quad() == 0) {
-
   // ---- post_physics_step ----
-  int32_t eplen = S.episode_length[e] + 1;
+  // (every lane of the env: the base-frame velocities and the push feed the spread state write-back below)
+  const int32_t eplen = S.episode_length[e] + 1;
   const float* quat = st.quat;
-  V3 blv = quat_rotate_inverse(quat, v3(st.V[0], st.V[1], st.V[2]));
-  V3 bav = quat_rotate_inverse(quat, v3(st.W[0], st.W[1], st.W[2]));
-  V3 pg = quat_rotate_inverse(quat, v3(0.f, 0.f, -1.f));
+  const V3 blv = quat_rotate_inverse(quat, v3(st.V[0], st.V[1], st.V[2]));
+  const V3 bav = quat_rotate_inverse(quat, v3(st.W[0], st.W[1], st.W[2]));
+  const V3 pg = quat_rotate_inverse(quat, v3(0.f, 0.f, -1.f));
   const bool inject = flags & LRL_STEP_INJECT_UNIFORM;
+  // _push_robots (legged_robot.py:757-766): after the base-frame velocities above, before the rewards; the pushed
+  // root velocity is what root_states, the next step's physics and last_root_vel see
+  if (P.push_robots && eplen % P.push_interval == 0) {
+    float u0, u1;
+    if (inject) {
+      u0 = valid ? S.inj_push[(size_t)e * 2] : 0.5f;
+      u1 = valid ? S.inj_push[(size_t)e * 2 + 1] : 0.5f;
+    } else {
+      lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter, (LRL_RNG_PUSH << 16) ^ (uint32_t)(step_counter >> 32),
+                               0, S.seed);
+      u0 = lrl_u01(r.v[0]);
+      u1 = lrl_u01(r.v[1]);
+    }
+    st.V[0] = P.push_span * u0 + P.push_lo;  // (upper - lower) * torch.rand + lower
+    st.V[1] = P.push_span * u1 + P.push_lo;
+  }
+  // post-physics rewards, observations and the per-env state write-back: lane 0 of each env (of its first quad)
+  if (ql == 0 && mirror_quad() == 0) {
   float ms_e[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) ms_e[j] = S.motor_strength[j * N + e];
@@ -2257,22 +2274,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 #pragma unroll
       for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
     }
-  }
-  // _push_robots (legged_robot.py:757-766): after the base-frame velocities above, before the rewards; the pushed
-  // root velocity is what root_states, the next step's physics and last_root_vel see
-  if (P.push_robots && eplen % P.push_interval == 0) {
-    float u0, u1;
-    if (inject) {
-      u0 = valid ? S.inj_push[(size_t)e * 2] : 0.5f;
-      u1 = valid ? S.inj_push[(size_t)e * 2 + 1] : 0.5f;
-    } else {
-      lrl_u32x4 r = lrl_philox((uint32_t)genv, (uint32_t)step_counter, (LRL_RNG_PUSH << 16) ^ (uint32_t)(step_counter >> 32),
-                               0, S.seed);
-      u0 = lrl_u01(r.v[0]);
-      u1 = lrl_u01(r.v[1]);
-    }
-    st.V[0] = P.push_span * u0 + P.push_lo;  // (upper - lower) * torch.rand + lower
-    st.V[1] = P.push_span * u1 + P.push_lo;
   }
   if (P.use_terminal_body_height && st.pos[2] < P.terminal_body_height) rst = 1;
   // time-outs (legged_robot.py:196-198, commented out in the fork — Q2): upstream semantics only
@@ -2436,41 +2437,57 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   LRL_PROF(13)  // obs / priv rows
   // ---- write back the SoA state ----
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    S.root[k * N + e] = st.pos[k];
-    S.root[(7 + k) * N + e] = st.V[k];
-    S.root[(10 + k) * N + e] = st.W[k];
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) S.root[(3 + k) * N + e] = st.quat[k];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    S.dof_pos[j * N + e] = q12[j];
-    S.dof_vel[j * N + e] = qd12[j];
-    S.torques[j * N + e] = tau[j];
-    if (P.control_type == 0) S.joint_pos_target[j * N + e] = pos_target(P, act, j);  // set by 'P' only (:669)
-    S.actions[j * N + e] = act[j];
-    S.last_actions[j * N + e] = act[j];
-    S.last_dof_vel[j * N + e] = qd12[j];
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    S.last_root_vel[k * N + e] = st.V[k];
-    S.last_root_vel[(3 + k) * N + e] = st.W[k];
-  }
-#pragma unroll
   for (int f = 0; f < 4; ++f) {
     S.feet_air_time[f * N + e] = fat[f];
     S.last_contacts[f * N + e] = lc[f];
   }
-  S.base_lin_vel[e] = blv.x; S.base_lin_vel[N + e] = blv.y; S.base_lin_vel[2 * N + e] = blv.z;
-  S.base_ang_vel[e] = bav.x; S.base_ang_vel[N + e] = bav.y; S.base_ang_vel[2 * N + e] = bav.z;
-  S.projected_gravity[e] = pg.x; S.projected_gravity[N + e] = pg.y; S.projected_gravity[2 * N + e] = pg.z;
   S.episode_length[e] = eplen;
   S.reset[e] = (uint8_t)rst;
   S.time_out[e] = (uint8_t)tout;
   S.rew[e] = rew;
   }  // ql == 0
+  // the joint-indexed state rows, from the lanes that hold them: lane ql writes its leg's 3 joints (the values the
+  // quad broadcast gave the lead lane, bit for bit); with mirrored quads, quad qi takes field group qi
+  {
+    const int qi = mirror_quad();
+    auto put3 = [&](float* f, const float* v) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) f[(3 * ql + j) * N + e] = v[j];
+    };
+    if (MIRROR == 1 || qi == 0) {
+      put3(S.dof_pos, st.q);
+      put3(S.dof_vel, st.qd);
+    }
+    if (MIRROR == 1 || qi == 1) {
+      put3(S.torques, tau3);
+      if (P.control_type == 0) put3(S.joint_pos_target, tg3);  // set by 'P' only (:669); tg3 = pos_target there
+    }
+    if (MIRROR == 1 || qi == 2) {
+      put3(S.actions, act3);
+      put3(S.last_actions, act3);
+    }
+    if (MIRROR == 1 || qi == 3) put3(S.last_dof_vel, st.qd);
+  }
+  // the base rows, spread over the env's lanes (lane k of the env writes field k; every lane holds the values)
+  {
+    constexpr int EL = QL * MIRROR;
+    const int sl = lane & (EL - 1);
+    auto sel3 = [](int k, float a, float b, float c) { return k == 0 ? a : (k == 1 ? b : c); };
+    for (int k = sl; k < 13; k += EL) {  // root_states: pos, quat (xyzw), lin vel, ang vel
+      const float v = k < 3 ? sel3(k, st.pos[0], st.pos[1], st.pos[2])
+                    : k < 7 ? (k == 3 ? st.quat[0] : k == 4 ? st.quat[1] : k == 5 ? st.quat[2] : st.quat[3])
+                    : k < 10 ? sel3(k - 7, st.V[0], st.V[1], st.V[2]) : sel3(k - 10, st.W[0], st.W[1], st.W[2]);
+      S.root[k * N + e] = v;
+    }
+    for (int k = sl; k < 6; k += EL)
+      S.last_root_vel[k * N + e] = k < 3 ? sel3(k, st.V[0], st.V[1], st.V[2]) : sel3(k - 3, st.W[0], st.W[1], st.W[2]);
+    for (int k = sl; k < 9; k += EL) {
+      const int c = k % 3;
+      const float v = k < 3 ? sel3(c, blv.x, blv.y, blv.z) : k < 6 ? sel3(c, bav.x, bav.y, bav.z) : sel3(c, pg.x, pg.y, pg.z);
+      float* f = k < 3 ? S.base_lin_vel : k < 6 ? S.base_ang_vel : S.projected_gravity;
+      f[c * N + e] = v;
+    }
+  }
   // observation noise + clip, the row's 4-entry chunks spread over the env's lanes
   __syncthreads();
   obs_noise_clip(P, S, e, genv, step_counter, (flags & LRL_STEP_INJECT_UNIFORM) != 0, otile + es * NO,
