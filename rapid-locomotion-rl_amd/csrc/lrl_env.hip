@@ -1524,6 +1524,35 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     // own contacts (the activation reads the owner's leg rates).  Same queries, same results.
     {
       const int lane = threadIdx.x;
+      // the query's own max-height test (terrain_query: a sphere more than r + offset above its cell's max height is
+      // clear) applied to the owner's first CF candidates before they enter the work list, so the wave deals fewer
+      // queries; every load of the test issued at once (one memory round trip).  Same test, same cells: the dropped
+      // spheres are the ones whose query would have ended there (their row fields are never read: not in contact)
+      {
+        constexpr int CF = 8;
+        const float bs = K->p.border_size, ih = K->terr_inv_hs;
+        const int R = K->terr_rows, Cn = K->terr_cols;
+        int cs[CF];
+        float cz[CF], hm[CF];
+        uint64_t m = cand;
+#pragma unroll
+        for (int k = 0; k < CF; ++k) {
+          cs[k] = m ? __builtin_ctzll(m) : -1;
+          m &= m - 1ull;
+        }
+#pragma unroll
+        for (int k = 0; k < CF; ++k) {
+          const int sk = cs[k] < 0 ? 0 : cs[k];
+          const float px = M.sph(sk, 6), py = M.sph(sk, 7);
+          cz[k] = M.sph(sk, 8) - M.sph4(sk).w - P.contact_offset;
+          const int ci = min(max((int)floorf((px + bs) * ih), 0), R - 2);
+          const int cj = min(max((int)floorf((py + bs) * ih), 0), Cn - 2);
+          hm[k] = cs[k] < 0 ? 3.0e38f : K->terr_hmax[ci * Cn + cj];
+        }
+#pragma unroll
+        for (int k = 0; k < CF; ++k)
+          if (cs[k] >= 0 && cz[k] > hm[k]) cand &= ~(1ull << cs[k]);
+      }
       const int cnt = __popcll(cand);
       int inc = cnt;
 #pragma unroll
