@@ -1,6 +1,7 @@
 // lrl_env.hip — fused LeggedRobot.step for gfx950 (CDNA4).
 //
-// One env per lane, 64 envs per single-wave workgroup.  A launch performs the whole policy step
+// A quad of lanes per env (layout below: 16 envs per single-wave workgroup on the terrain mesh, 4 envs with four
+// mirrored quads each on the plane, lrl_env_flat.hip).  A launch performs the whole policy step
 // (legged_robot.py:106-137): action clip, `decimation` x {PD torques (:653-688) + one physics
 // sub-step}, post_physics_step (:139-188) with teleport (:768-791), DR redraw (:544-560, :591-593),
 // termination (:190-202), rewards (:314-340, :1506-1646), observations + noise (:342-417), the
@@ -26,7 +27,7 @@
 #include "lrl_kparams.h"
 
 #define BLOCK LRL_ENV_LANES  // lanes per workgroup (one wave; see lrl_kparams.h)
-// Quad layout: 4 lanes per env (lane & 3 = the leg it owns), 16 envs per single-wave workgroup.  The leg
+// Quad layout: 4 lanes per env (lane & 3 = the leg it owns), 16 envs per single-wave workgroup (the mesh build).  The leg
 // work (kinematics, composite inertias, leg blocks, RNEA, contact detection and Delassus rows of the leg's
 // spheres, warm-start impulses) runs leg-parallel; the base quantities are summed over the 4 lanes with
 // cross-lane shuffles; the Gauss-Seidel sweep and the integration run redundantly in the 4 lanes (so
