@@ -1056,6 +1056,61 @@ __device__ __forceinline__ SelfGate self_gate(const KParams* __restrict__ K, con
   const int e = sel4(SL.e, ql);
   const int kmax = __builtin_amdgcn_readfirstlane(K->self_kmax);  // (wave-uniform loop bound)
   const int nhip = K->self_nhip[ql];
+  if constexpr (MIRROR > 1) {
+    // mirrored quads: quad q takes the leg's spheres k = q, q + 4 (one uniform pass of the loop body per 4 spheres, the
+    // sphere index varying by lane); the box is min / max-reduced and the hits summed over the env's quads with DPP
+    // row rotations by 4 and 8 lanes (lane ql meets lane ql of every quad) — exact in any order, as the loop's form
+    const int qi = mirror_quad();
+    const float cw = co + 1e-5f, hc = 0.5f * co;
+    const float bcx = K->box_c[0], bcy = K->box_c[1], bcz = K->box_c[2];
+    const float bhx = K->box_h[0], bhy = K->box_h[1], bhz = K->box_h[2];
+    const bool box = bhx >= 0.f;
+    const int s0 = min(b, e - 1), s1 = min(b + 1, e - 1);
+    const float h0x = M.sph(s0, 0), h0y = M.sph(s0, 1), h0z = M.sph(s0, 2);
+    const float h1x = M.sph(s1, 0), h1y = M.sph(s1, 1), h1z = M.sph(s1, 2);
+    const float h0r = nhip >= 1 ? M.sph4(s0).w + cw : -1e30f, h1r = nhip >= 2 ? M.sph4(s1).w + cw : -1e30f;
+    SelfGate G;
+    G.lo = v3(1e30f, 1e30f, 1e30f);
+    G.hi = v3(-1e30f, -1e30f, -1e30f);
+    int hits = (nhip > 2 && qi == 0) ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < 8 / MIRROR; ++j)
+      if (MIRROR * j < kmax) {
+        const int k = MIRROR * j + qi;
+        const int s = min(b + k, e - 1);
+        const float cx = M.sph(s, 0), cy = M.sph(s, 1), cz = M.sph(s, 2), r = M.sph4(s).w;
+        const int lk = M.slink(s);
+        const bool use = k < kmax && b + k < e;
+        const float rg = r + hc;
+        const float xl = use ? cx - rg : 1e30f, yl = use ? cy - rg : 1e30f, zl = use ? cz - rg : 1e30f;
+        const float xh = use ? cx + rg : -1e30f, yh = use ? cy + rg : -1e30f, zh = use ? cz + rg : -1e30f;
+        G.lo = v3(fminf(G.lo.x, xl), fminf(G.lo.y, yl), fminf(G.lo.z, zl));
+        G.hi = v3(fmaxf(G.hi.x, xh), fmaxf(G.hi.y, yh), fmaxf(G.hi.z, zh));
+        const float qx = fmaxf(fabsf(cx - bcx) - bhx, 0.f), qy = fmaxf(fabsf(cy - bcy) - bhy, 0.f),
+                    qz = fmaxf(fabsf(cz - bcz) - bhz, 0.f);
+        const float rb = r + cw;
+        const bool hb = box && lk >= 1 && qx * qx + qy * qy + qz * qz < rb * rb;
+        const float ax = cx - h0x, ay = cy - h0y, az = cz - h0z, rh = h0r + r;
+        const float bx = cx - h1x, by = cy - h1y, bz = cz - h1z, ri = h1r + r;
+        const bool hh = lk == 2 && ((rh > 0.f && ax * ax + ay * ay + az * az < rh * rh) ||
+                                    (ri > 0.f && bx * bx + by * by + bz * bz < ri * ri));
+        hits += (use && (hb || hh)) ? 1 : 0;
+      }
+    auto rmin = [](float v) {
+      v = fminf(v, qperm<0x124>(v));
+      return fminf(v, qperm<0x128>(v));
+    };
+    auto rmax = [](float v) {
+      v = fmaxf(v, qperm<0x124>(v));
+      return fmaxf(v, qperm<0x128>(v));
+    };
+    G.lo = v3(rmin(G.lo.x), rmin(G.lo.y), rmin(G.lo.z));
+    G.hi = v3(rmax(G.hi.x), rmax(G.hi.y), rmax(G.hi.z));
+    hits += qperm<0x124>(hits);
+    hits += qperm<0x128>(hits);
+    G.hits = hits;
+    return G;
+  }
   float cx[8], cy[8], cz[8], r[8];
   int lk[8];
 #pragma unroll
