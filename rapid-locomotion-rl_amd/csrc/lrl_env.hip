@@ -463,17 +463,29 @@ __device__ THit terrain_query(const KParams* __restrict__ K, V3 p, float r, floa
   int bk = -1;     // the nearest triangle so far (its closest point / normal are formed once, after the walk)
   int under = -1;  // height-field side of p from the triangle under it: 1 above / on, 0 below, -1 none found
   // each lane walks its own marked triangles in order (the wave runs max-over-lanes triangles, not 18)
+  // (the next marked triangle's vertices are read while this one is tested: the LDS round trip overlaps the arithmetic;
+  // an exhausted lane re-reads its last triangle, unused)
+  auto tri_load = [&](int k, float4& fa, float4& fb, float4& fc) {
+    const int c = k >> 1, di = c / 3, dj = c - 3 * di;
+    const int ia = 4 * di + dj;  // v(i,j) in the block
+    const int ib = (k & 1) ? ia + 4 : ia + 5, ic = (k & 1) ? ia + 5 : ia + 1;
+    fa = tv[ia * BLOCK + lane];
+    fb = tv[ib * BLOCK + lane];
+    fc = tv[ic * BLOCK + lane];
+  };
+  int kn = tris ? __builtin_ctz(tris) : 0;
+  float4 na, nb, nc;
+  tri_load(kn, na, nb, nc);
   while (__any((int)(tris != 0u))) {
 #ifdef LRL_ENV_PROFILE
     prof[18] += 1;  // walk iterations (per wave: the busiest lane's count)
 #endif
     if (tris) {
-      const int k = __builtin_ctz(tris);
+      const int k = kn;
+      const float4 fa = na, fb = nb, fc = nc;
       tris &= tris - 1u;
-      const int c = k >> 1, di = c / 3, dj = c - 3 * di;
-      const int ia = 4 * di + dj;  // v(i,j) in the block
-      const int ib = (k & 1) ? ia + 4 : ia + 5, ic = (k & 1) ? ia + 5 : ia + 1;
-      const float4 fa = tv[ia * BLOCK + lane], fb = tv[ib * BLOCK + lane], fc = tv[ic * BLOCK + lane];
+      kn = tris ? __builtin_ctz(tris) : k;
+      tri_load(kn, na, nb, nc);
       const V3 va = v3(fa.x, fa.y, fa.z), b = v3(fb.x, fb.y, fb.z), cv = v3(fc.x, fc.y, fc.z);
       const V3 nf = cross(b - va, cv - va);
       const float a2 = dot(nf, nf);
