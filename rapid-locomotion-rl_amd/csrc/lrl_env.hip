@@ -1640,15 +1640,23 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       prof[22] += clock64() - tq0;  // scan + work-list publication
 #endif
       float4* tv = reinterpret_cast<float4*>(M.base + (M.sph_off + K->num_spheres * NSF) * ENVS);
+      // item j -> (owner lane L, sphere s): the last lane whose prefix is <= j, then the owner's (j - prefix)-th set bit.
+      // Located one round ahead: round r + 1's chain of dependent LDS reads runs under round r's query
+      auto locate = [&](int j, int& L, int& s) {
+        L = 0;
+#pragma unroll
+        for (int step = BLOCK / 2; step; step >>= 1)
+          if (wl_off[L + step] <= j) L += step;
+        uint64_t mk = wl_mask[L];
+        for (int q = j - wl_off[L]; q > 0; --q) mk &= mk - 1ull;
+        s = __builtin_ctzll(mk);
+      };
+      int Ln = 0, sn = 0;
+      if (lane < total) locate(lane, Ln, sn);
       for (int j = lane; j - lane < total; j += BLOCK) {
         if (j < total) {
-          int L = 0;
-#pragma unroll
-          for (int step = BLOCK / 2; step; step >>= 1)
-            if (wl_off[L + step] <= j) L += step;
-          uint64_t mk = wl_mask[L];
-          for (int q = j - wl_off[L]; q > 0; --q) mk &= mk - 1ull;
-          const int s = __builtin_ctzll(mk);
+          const int L = Ln, s = sn;
+          if (j + BLOCK < total) locate(j + BLOCK, Ln, sn);
           float* row = M.base + (M.sph_off + s * NSF) * ENVS + (L >> 2);
           const THit th = terrain_query(K, v3(row[6 * ENVS], row[7 * ENVS], row[8 * ENVS]), M.sph4(s).w,
                                         P.contact_offset, tv, lane, prof);
