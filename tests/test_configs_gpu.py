@@ -475,6 +475,7 @@ def test_rollout_does_not_depend_on_the_gpu_count(legacy_fork, n):
         mp.spawn(_rank_worker, args=(2, _port(), "mc", tmp, two, n // 2, True, legacy_fork), nprocs=2, join=True)
     ref = one[0]
     h = n // 2
+    bad = []  # every differing key, located by (step, env, field), before the assertion
     for k in STORE_KEYS + ["root", "dof_pos", "dof_vel", "contact", "hist", "origins"]:
         whole = ref[k]
         ax = 1 if k in STORE_KEYS else 0  # storage is [T, N, ...]
@@ -482,7 +483,12 @@ def test_rollout_does_not_depend_on_the_gpu_count(legacy_fork, n):
         if k == "advantages":
             np.testing.assert_allclose(parts, whole, rtol=0, atol=2e-6 * max(1.0, np.abs(whole).max()), err_msg=k)
             continue
-        np.testing.assert_array_equal(parts, whole, err_msg=k)
+        ne = parts != whole
+        if ne.any():
+            idx = np.argwhere(ne.reshape(ne.shape[:2] + (-1,)) if ne.ndim > 2 else ne)
+            cols = [np.unique(idx[:, c])[:16].tolist() for c in range(idx.shape[1])]
+            bad.append(f"{k}: {int(ne.sum())} differ, max |d| {np.abs(parts.astype(np.float64) - whole.astype(np.float64))[ne].max():.3e}, indices {cols}")
+    assert not bad, "\n".join(bad)
     assert np.abs(ref["actions"][:, :h] - ref["actions"][:, h:]).max() > 0.1  # the halves are different envs
     if not legacy_fork:  # upstream resets happened; at 512 envs some step resets envs of one shard only (ADVICE r4:
         # the reset draws are keyed by each env's own reset count, not by a per-process counter that only that shard's
