@@ -56,16 +56,26 @@ def main():
     P.lds_poison.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p]
     sink = torch.zeros(256 * 8, dtype=torch.int32, device="cuda:0")
     L = _abi.lib()
-    orig = L.lrl_sim_step
+    # every C-ABI entry point include/lrl.h declares: the LDS is poisoned on the current stream before each call
+    import re
+    names = sorted(set(re.findall(r"\b(lrl_\w+)\s*\(", open(os.path.join(ROOT, "include", "lrl.h")).read())))
+    origs = {nm: getattr(L, nm) for nm in names if hasattr(L, nm)}
     for pat in pats:
-        def step(sim, act, flags, stream, _o=orig, _p=pat):
-            assert P.lds_poison(_p, sink.data_ptr(), stream) == 0
-            return _o(sim, act, flags, stream)
-        L.lrl_sim_step = step
+        def wrap(nm, _p=pat):
+            o = origs[nm]
+
+            def call(*a):
+                st = torch.cuda.current_stream().cuda_stream
+                assert P.lds_poison(_p, sink.data_ptr(), C.c_void_p(st)) == 0
+                return o(*a)
+            return call
+        for nm in origs:
+            setattr(L, nm, wrap(nm))
         try:
             any_bad |= compare(f"poison{pat:#x}", T._iteration("mc", 0, 1, tmp, T.N_BENCH, True, True), ref)
         finally:
-            L.lrl_sim_step = orig
+            for nm, o in origs.items():
+                setattr(L, nm, o)
     assert int(sink.sum()) == 0
     # timing perturbation: another process keeps the GPU busy with GEMMs while the rollout runs (as the 2-rank
     # sharding test's ranks share the card)

@@ -5,7 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-constexpr int POISON_WORDS = 16384;  // 64 KB per workgroup; 2 resident per CU cover 128 KB, the grid covers the rest
+constexpr int POISON_WORDS = 40960;  // all 160 KiB of a CU's LDS per workgroup (one resident per CU)
 
 __global__ __launch_bounds__(256) void lds_poison_kernel(uint32_t pattern, uint32_t* sink) {
   __shared__ uint32_t buf[POISON_WORDS];
@@ -16,6 +16,6 @@ __global__ __launch_bounds__(256) void lds_poison_kernel(uint32_t pattern, uint3
 }
 
 extern "C" int lds_poison(uint32_t pattern, void* sink, void* stream) {
-  hipLaunchKernelGGL(lds_poison_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream, pattern, (uint32_t*)sink);
+  hipLaunchKernelGGL(lds_poison_kernel, dim3(256 * 4), dim3(256), 0, (hipStream_t)stream, pattern, (uint32_t*)sink);
   return (int)hipGetLastError();
 }
