@@ -163,6 +163,17 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
   if (p->num_reward_terms < 0 || p->num_reward_terms > LRL_MAX_REWARD_TERMS) return fail(LRL_E_INVALID, "reward terms");
   for (int t = 0; t < p->num_reward_terms; ++t)
     if (p->reward_term[t] < 0 || p->reward_term[t] >= LRL_R_NUM_TERMS) return fail(LRL_E_INVALID, "reward term id");
+  {  // the sum rows: each term (and the termination term) its own row below num_sum_keys (the kernel writes rows
+     // reward_slot[t] / termination_slot of episode_sums and command_sums, sized num_sum_keys + 1 / + 5)
+    uint64_t used = 0;
+    const bool term = p->termination_scale != 0.f;
+    if (p->num_sum_keys < 0 || p->num_sum_keys > 64) return fail(LRL_E_INVALID, "num_sum_keys %d", p->num_sum_keys);
+    for (int t = 0; t < p->num_reward_terms + (term ? 1 : 0); ++t) {
+      const int r = t < p->num_reward_terms ? p->reward_slot[t] : p->termination_slot;
+      if (r < 0 || r >= p->num_sum_keys || ((used >> r) & 1ull)) return fail(LRL_E_INVALID, "sum row %d of term %d", r, t);
+      used |= 1ull << r;
+    }
+  }
   if (p->measure_heights && (p->num_height_points <= 0 || p->num_height_points > LRL_MAX_HEIGHT_POINTS))
     return fail(LRL_E_INVALID, "num_height_points %d", p->num_height_points);
   if (p->terrain_mesh && p->horizontal_scale <= 0.f) return fail(LRL_E_INVALID, "horizontal_scale");

@@ -42,6 +42,7 @@ def run(out, iters=2, workload="mc"):
     g = lambda t: t.detach().cpu().numpy().copy()
     np.savez(out, root=g(e.root_states), dof_pos=g(e.dof_pos), dof_vel=g(e.dof_vel), contact=g(e.contact_forces),
              torques=g(e.torques), obs=g(e.obs_buf), priv=g(e.privileged_obs_buf), rew=g(e.rew_buf),
+             episode_sums=g(e._episode_sums), command_sums=g(e._command_sums),
              params=g(runner.alg.actor_critic._flat))
     print("saved", out)
 

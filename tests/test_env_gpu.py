@@ -626,3 +626,28 @@ def test_device_path_episode_log_is_not_overwritten():
         changed += int(now != kept[-1][2])
     assert changed > 0  # the logged values did move over the run
     env.close()
+
+
+def test_sim_create_refuses_shared_or_out_of_range_sum_rows():
+    """lrl_sim_create checks the episode / command sum rows the kernel writes: every reward term and the termination
+    term its own row below num_sum_keys (a shared or out-of-range row would be a lost update or a write past the
+    rows' arena slice)."""
+    cfg, rob, Mo, P = make("mc")
+    L = _abi.lib()
+
+    def create(P):
+        sim = C.c_void_p()
+        rc = L.lrl_sim_create(C.byref(Mo), C.byref(P), C.c_int32(16), C.c_int64(0), C.c_uint64(1), C.c_int32(0),
+                              C.byref(sim))
+        if rc == 0:
+            L.lrl_sim_destroy(sim)
+        return rc
+    assert P.num_reward_terms >= 2
+    assert create(P) == 0
+    for field, t, v in [("reward_slot", 1, None), ("reward_slot", 0, P.num_sum_keys), ("reward_slot", 0, -1)]:
+        saved = getattr(P, field)[t]
+        getattr(P, field)[t] = P.reward_slot[0] if v is None else v
+        assert create(P) != 0, (field, t, v)
+        assert b"sum row" in L.lrl_last_error()
+        getattr(P, field)[t] = saved
+    assert create(P) == 0
