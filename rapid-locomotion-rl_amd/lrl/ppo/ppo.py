@@ -164,6 +164,10 @@ class PPO:
         reduce = None
         if _world() > 1:
             def reduce(stats):
+                if dist.get_backend() == "gloo":  # gloo reduces host memory: stage through a synchronous copy rather
+                    host = stats.cpu()            # than gloo's own CUDA-tensor path (side stream + pinned buffers)
+                    dist.all_reduce(host)
+                    return host.to(stats.device)
                 dist.all_reduce(stats)
                 return stats
         self.storage.compute_returns(last_values, PPO_Args.gamma, PPO_Args.lam, reduce_stats=reduce)
