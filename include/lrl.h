@@ -552,6 +552,15 @@ int32_t lrl_ppo_timing(int32_t enable, double* total_ms, int64_t* launches);
  * mask. */
 int32_t lrl_debug_gemm_paths(int32_t disable_mask);
 
+/* Determinism probe: with mode != 0 every lrl_sim_step of `s` launches, right before its env kernel, a pass that
+ * fills every CU's LDS (mode bit 0) and / or every SIMD's VGPR and AGPR files (bit 1) with `pattern`, so an env result
+ * that depends on state the launch never wrote moves with the pattern.  mode 0 turns it off. */
+int32_t lrl_debug_sim_garbage(lrl_sim* s, uint32_t mode, uint32_t pattern);
+/* The sim's state arena (device pointer, bytes) and its step counter, for replay-based determinism checks (a test
+ * copies the arena, runs lrl_sim_step, restores the copy and the counter — lrl_sim_set_step_counter — and runs it
+ * again).  Any out-pointer may be NULL. */
+int32_t lrl_debug_sim_arena(lrl_sim* s, void** arena, int64_t* bytes, int64_t* step_counter);
+
 /* Test entry point of the GEMM the update is built from: C = op(A) op(B) with
  * layout 0 (NT: C[m][n] = sum_k A[m][k] B[n][k]), 2 (NN: sum_k A[m][k] B[k][n]),
  * 3 (TN: sum_k A[k][m] B[k][n], split over k, partials reduced in place);

@@ -413,6 +413,34 @@ __global__ void apply_commands_kernel(KState S, int32_t ncs, const int32_t* __re
   if (bins_out && i < nb) bins_out[i] = bins_in[i];
 }
 
+// Determinism probe (lrl_debug_sim_garbage): state a launch never wrote — LDS outside what the env kernel stores first,
+// VGPR / AGPR lanes it reads before defining them — holds whatever the previous wave on that CU / SIMD left, which in a
+// multi-process run is another process's data.  These kernels leave a known pattern there right before the env
+// kernel, so an env result that moves with the pattern names such a read.  Vector moves and LDS stores only.
+__global__ __launch_bounds__(64) void garbage_lds_kernel(uint32_t pat) {
+  extern __shared__ uint32_t g_lds[];
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 64) g_lds[i] = pat ^ (uint32_t)(i & 3);
+}
+#define LRL_GV(n) asm volatile("v_mov_b32 v" #n ", %0" ::"s"(pat) : "v" #n);
+#define LRL_GA(n) asm volatile("v_accvgpr_write_b32 a" #n ", %0" ::"v"(pv) : "a" #n);
+#define LRL_G10(M, d) M(d##0) M(d##1) M(d##2) M(d##3) M(d##4) M(d##5) M(d##6) M(d##7) M(d##8) M(d##9)
+#define LRL_G250(M)                                                                                                   \
+  M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) LRL_G10(M, 1) LRL_G10(M, 2) LRL_G10(M, 3) LRL_G10(M, 4)            \
+  LRL_G10(M, 5) LRL_G10(M, 6) LRL_G10(M, 7) LRL_G10(M, 8) LRL_G10(M, 9) LRL_G10(M, 10) LRL_G10(M, 11) LRL_G10(M, 12) \
+  LRL_G10(M, 13) LRL_G10(M, 14) LRL_G10(M, 15) LRL_G10(M, 16) LRL_G10(M, 17) LRL_G10(M, 18) LRL_G10(M, 19)           \
+  LRL_G10(M, 20) LRL_G10(M, 21) LRL_G10(M, 22) LRL_G10(M, 23) LRL_G10(M, 24)
+__global__ __launch_bounds__(64) void garbage_vgpr_kernel(uint32_t pat) {
+  const uint32_t pv = pat ^ threadIdx.x;  // (lane-varying in the AGPRs)
+  LRL_G250(LRL_GA)
+  LRL_GA(250) LRL_GA(251) LRL_GA(252) LRL_GA(253) LRL_GA(254) LRL_GA(255)
+  LRL_G250(LRL_GV)
+  LRL_GV(250) LRL_GV(251) LRL_GV(252) LRL_GV(253) LRL_GV(254) LRL_GV(255)
+}
+#undef LRL_GV
+#undef LRL_GA
+#undef LRL_G10
+#undef LRL_G250
+
 }  // namespace lrl
 
 extern "C" {
@@ -498,6 +526,19 @@ hipError_t lrl_launch_extras_snapshot(const KParams* K, const KState* S, const i
   static_assert(LRL_NUM_LEGS == 4, "one quarter-thread per foot");
   hipLaunchKernelGGL(lrl::extras_snapshot_kernel, dim3((S->n + 63) / 64), dim3(256), 0, st, K, *S, body_leg,
                      body_link, foot_xyz, out);
+  return hipGetLastError();
+}
+hipError_t lrl_launch_garbage(uint32_t mode, uint32_t pat, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)lrl::garbage_lds_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  // one 160 KiB workgroup per CU at a time (8 rounds over 256 CUs); 512-register waves, one per SIMD at a time
+  if (mode & 1u) hipLaunchKernelGGL(lrl::garbage_lds_kernel, dim3(2048), dim3(64), 160 * 1024, st, pat);
+  if (mode & 2u) hipLaunchKernelGGL(lrl::garbage_vgpr_kernel, dim3(8192), dim3(64), 0, st, pat);
   return hipGetLastError();
 }
 hipError_t lrl_launch_shift_history(const KState* S, int NO, int H, int append, hipStream_t st) {

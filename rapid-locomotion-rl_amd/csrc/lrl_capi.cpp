@@ -51,6 +51,7 @@ hipError_t lrl_launch_rigid_body(const KParams*, const KState*, const int32_t*, 
 hipError_t lrl_launch_extras_snapshot(const KParams*, const KState*, const int32_t*, const int32_t*, const float*, float*,
                                       hipStream_t);
 hipError_t lrl_launch_shift_history(const KState*, int, int, int, hipStream_t);
+hipError_t lrl_launch_garbage(uint32_t mode, uint32_t pat, hipStream_t st);
 hipError_t lrl_launch_randomize(const KState*, const float*, const float*, const float*, const float*, uint32_t,
                                 hipStream_t);
 }
@@ -75,6 +76,7 @@ struct lrl_sim {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
+  uint32_t garbage_mode = 0, garbage_pat = 0;  // lrl_debug_sim_garbage
 };
 
 static void quat_to_rowmajor(const float* q, float* R) {
@@ -523,6 +525,7 @@ int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* str
   if (flags & LRL_STEP_HISTORY)  // HistoryWrapper.step's shift; the env kernel appends the step's obs row
     HIPCHECK(lrl_launch_shift_history(&s->S, s->hk.p.num_obs, s->hk.p.num_history * s->hk.p.num_obs, 0,
                                       (hipStream_t)stream));
+  if (s->garbage_mode) HIPCHECK(lrl_launch_garbage(s->garbage_mode, s->garbage_pat, (hipStream_t)stream));
   std::pair<hipEvent_t, hipEvent_t>* tp = nullptr;
   if (s->timing) {
     if (s->ev_used == s->ev.size()) {
@@ -537,6 +540,22 @@ int32_t lrl_sim_step(lrl_sim* s, const float* actions, uint32_t flags, void* str
   HIPCHECK(lrl_launch_env_step(s->dk, &s->S, s->lds_bytes, actions, flags, s->step_counter, s->hk.p.terrain_mesh,
                                (hipStream_t)stream));
   if (tp) HIPCHECK(hipEventRecord(tp->second, (hipStream_t)stream));
+  return 0;
+}
+
+int32_t lrl_debug_sim_garbage(lrl_sim* s, uint32_t mode, uint32_t pattern) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  if (mode > 3u) return fail(LRL_E_INVALID, "garbage mode %u", mode);
+  s->garbage_mode = mode;
+  s->garbage_pat = pattern;
+  return 0;
+}
+
+int32_t lrl_debug_sim_arena(lrl_sim* s, void** arena, int64_t* bytes, int64_t* step_counter) {
+  if (!s) return fail(LRL_E_INVALID, "null sim");
+  if (arena) *arena = s->arena;
+  if (bytes) *bytes = (int64_t)s->arena_bytes;
+  if (step_counter) *step_counter = s->step_counter;
   return 0;
 }
 

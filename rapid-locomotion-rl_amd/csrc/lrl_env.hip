@@ -2062,7 +2062,11 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   extern __shared__ float lds[];
   const lrl_env_params& P = K->p;
   const int lane = threadIdx.x;
+#ifdef LRL_ENV_SLOT_REV  // (determinism probe build: env slots in reverse lane order)
+  const int es = ENVS - 1 - lane / (QL * MIRROR), ql = lane & 3;
+#else
   const int es = lane / (QL * MIRROR), ql = lane & 3;  // env slot, owned leg
+#endif
   const int blk = env_block();
   const int e = blk * ENVS + es;
   const int N = S.stride;

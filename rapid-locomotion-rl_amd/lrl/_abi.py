@@ -183,7 +183,8 @@ def lib():
                      "lrl_curriculum_update_weights", "lrl_rows_mean_zero", "lrl_sim_step_code",
                      "lrl_sim_apply_commands", "lrl_sim_extras_snapshot", "lrl_sim_env_lists",
                      "lrl_sim_terrain_curriculum_dev", "lrl_sim_reset_idx_dev", "lrl_sim_observe_idx_dev",
-                     "lrl_rows_mean_zero_dev", "lrl_sim_curriculum_resample_dev", "lrl_debug_gemm_paths"]:
+                     "lrl_rows_mean_zero_dev", "lrl_sim_curriculum_resample_dev", "lrl_debug_gemm_paths",
+                     "lrl_debug_sim_garbage", "lrl_debug_sim_arena"]:
             getattr(L, name).restype = C.c_int32
         L.lrl_np_sum_f64.restype = C.c_double
         L.lrl_np_sum_f64.argtypes = [C.c_void_p, C.c_int64]

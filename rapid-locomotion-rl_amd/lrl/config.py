@@ -10,12 +10,44 @@ working.  The tree is built from plain dict specs into ``Section`` namespaces (n
 """
 import copy
 import types
+import weakref
 
 ROOT = None  # filled by lrl/__init__.py: directory holding resources/
 
 
+_PATHS = {}  # id(Section) -> (weak ref, its dotted path in the tree: "terrain", "rewards.scales"), for _update's prefixes
+
+
+def _update_fields(obj, names, own_paths, d=None, **kwargs):
+    """params_proto's ``_update(deps)`` (scripts/play.py:30-44 restores a run's parameters with it): every key of
+    ``d`` / ``kwargs`` that names a field of ``obj`` — plainly (``mesh_type``) or under the node's own prefix
+    (``terrain.mesh_type``, ``Cfg.terrain.mesh_type``) — sets it; other keys are left for the other nodes."""
+    items = dict(d or {}, **kwargs)
+    for k, v in items.items():
+        prefix, _, leaf = str(k).rpartition(".")
+        if leaf not in names:
+            continue
+        if prefix and not any(prefix == p or prefix.endswith("." + p) for p in own_paths):
+            continue
+        setattr(obj, leaf, copy.deepcopy(v))
+
+
+class ArgsProto:
+    """Base of the algorithm argument classes (AC_Args, PPO_Args, RunnerArgs): ``Cls._update(dict)`` as params_proto's
+    PrefixProto, keys plain or prefixed with the class name."""
+
+    @classmethod
+    def _update(cls, d=None, **kwargs):
+        _update_fields(cls, {k for k in vars(cls) if not k.startswith("_")}, (cls.__name__,), d, **kwargs)
+
+
 class Section(types.SimpleNamespace):
     """A config node; attribute access like the reference's PrefixProto classes."""
+
+    def _update(self, d=None, **kwargs):
+        ref, path = _PATHS.get(id(self), (None, None))
+        path = path if ref is not None and ref() is self else None
+        _update_fields(self, set(vars(self)), (path,) if path else (), d, **kwargs)
 
     def to_dict(self):
         out = {}
@@ -24,11 +56,13 @@ class Section(types.SimpleNamespace):
         return out
 
 
-def _build(spec):
+def _build(spec, path=""):
     sec = Section()
+    if path:
+        _PATHS[id(sec)] = (weakref.ref(sec), path)
     for k, v in spec.items():
-        setattr(sec, k, _build(v) if isinstance(v, dict) and not k.endswith(("_angles", "stiffness", "damping"))
-                else copy.deepcopy(v))
+        setattr(sec, k, _build(v, f"{path}.{k}" if path else k)
+                if isinstance(v, dict) and not k.endswith(("_angles", "stiffness", "damping")) else copy.deepcopy(v))
     return sec
 
 

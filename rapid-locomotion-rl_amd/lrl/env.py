@@ -927,6 +927,11 @@ class LeggedRobotEnv:
     def get_privileged_observations(self, horizon=0):
         return self.privileged_obs_buf
 
+    def render(self, mode="rgb_array"):
+        """BaseTask.render (base_task.py:92-118) draws through the Isaac Gym viewer / camera sensors; rendering is out of
+        scope here (no viewer), so asking for a frame is an error, not a blank image."""
+        raise NotImplementedError("no viewer / camera rendering in this framework (DESIGN.md §8)")
+
     def reset(self):
         """VelocityTrackingEasyEnv.reset (:66-69): reset all, then one zero-action step."""
         self.reset_idx(torch.arange(self.num_envs, device=self.device))

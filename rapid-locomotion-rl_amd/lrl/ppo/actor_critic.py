@@ -9,12 +9,14 @@ that the nn.Module's tensors are views of (``flatten_parameters``); the update u
 import ctypes as C
 
 import torch
+
 import torch.nn as nn
 
 from .. import _abi
+from ..config import ArgsProto
 
 
-class AC_Args:
+class AC_Args(ArgsProto):
     """actor_critic.py:9-20"""
     init_noise_std = 1.0
     actor_hidden_dims = [512, 256, 128]

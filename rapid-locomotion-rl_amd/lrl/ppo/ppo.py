@@ -18,11 +18,13 @@ import ctypes as C
 import os
 
 import torch
+
 import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _abi
+from ..config import ArgsProto
 from .actor_critic import ActorCritic
 from .rollout_storage import RolloutStorage
 
@@ -32,7 +34,7 @@ from .rollout_storage import RolloutStorage
 _SNAPSHOTS = max(2, int(os.environ.get("LRL_ENC_SNAPSHOTS", "4")))
 
 
-class PPO_Args:
+class PPO_Args(ArgsProto):
     value_loss_coef = 1.0
     use_clipped_value_loss = True
     clip_param = 0.2

@@ -2,19 +2,20 @@
 
 Same constructor (``Runner(env, device)``), ``RunnerArgs`` and ``learn(num_learning_iterations,
 init_at_random_ep_len, eval_freq, eval_expert)`` signature and iteration order as the reference.
-ml_logger is replaced by a small local logger (metrics in memory + a JSON-lines file when a run
-directory is configured); checkpoints keep the reference's state-dict layout and file names
+Logging goes through ``ml_logger.logger`` as in the reference (the package's local-filesystem stand-in for the
+un-vendored ml_logger: in memory until ``logger.configure`` names a run directory), or through the ``logger`` a caller
+passes; checkpoints keep the reference's state-dict layout and file names
 (``checkpoints/ac_weights_{it:06d}.pt`` / ``ac_weights_last.pt``) plus the TorchScript exports of
 ``adaptation_module`` and ``actor_body``.
 """
 import copy
-import json
 import os
-import time
-from collections import defaultdict
 
 import torch
 
+from ml_logger import ML_Logger, logger as _ml_logger  # (rapid-locomotion-rl_amd/ml_logger, beside lrl)
+
+from ..config import ArgsProto
 from .actor_critic import ActorCritic
 from .ppo import PPO
 
@@ -24,7 +25,7 @@ from .ppo import PPO
 _SYNC_UPDATE = os.environ.get("LRL_RUNNER_SYNC", "0") == "1"
 
 
-class RunnerArgs:
+class RunnerArgs(ArgsProto):
     algorithm_class_name = "PPO"
     num_steps_per_env = 24
     max_iterations = 1500
@@ -37,44 +38,14 @@ class RunnerArgs:
     resume_path = None
 
 
-class Logger:
-    """The subset of ml_logger the runner uses."""
+class Logger(ML_Logger):
+    """A logger of its own writing under ``root`` (``Logger(run_dir)``; ``None``: metrics in memory only), for callers
+    that do not use the process-wide ``ml_logger.logger`` the reference's Runner logs through."""
 
     def __init__(self, root=None):
-        self.root = root
-        self.prefix = root or "memory"
-        self.metrics = defaultdict(list)
-        self.summaries = []
-        self._t0 = time.time()
-        self._split = time.time()
-
-    def store_metrics(self, **kw):
-        # (device scalars are kept as they are and converted when summarised: no host sync per iteration)
-        for k, v in kw.items():
-            self.metrics[k].append(v if isinstance(v, (float, torch.Tensor)) else float(v))
-
-    def since(self, _="start"):
-        return time.time() - self._t0
-
-    def split(self, _="epoch"):
-        t, self._split = time.time() - self._split, time.time()
-        return t
-
-    def log_metrics_summary(self, key_values=None):
-        s = {k: float(sum(v) / len(v)) for k, v in self.metrics.items() if v}
-        s.update(key_values or {})
-        self.summaries.append(s)
-        self.metrics.clear()
-        if self.root:
-            os.makedirs(self.root, exist_ok=True)
-            with open(os.path.join(self.root, "metrics.jsonl"), "a") as f:
-                f.write(json.dumps(s) + "\n")
-
-    def torch_save(self, obj, path):
-        if self.root:
-            full = os.path.join(self.root, path)
-            os.makedirs(os.path.dirname(full), exist_ok=True)
-            torch.save(obj, full)
+        super().__init__()
+        if root:
+            self.configure(root)
 
 
 class Runner:
@@ -93,11 +64,12 @@ class Runner:
         self.tot_time = 0
         self.current_learning_iteration = 0
         self.last_recording_it = 0
-        self.logger = logger or Logger()
+        self.logger = logger if logger is not None else _ml_logger  # (the reference: `from ml_logger import logger`)
         self.env.reset()
 
     def learn(self, num_learning_iterations, init_at_random_ep_len=False, eval_freq=100, eval_expert=False):
         lg = self.logger
+        lg.start("start", "epoch", "episode", "run", "step")
         if init_at_random_ep_len:  # lands on the wrapper, not the env, as in the reference (Q5)
             self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
                                                              high=int(self.env.max_episode_length))
@@ -115,6 +87,10 @@ class Runner:
                     obs_dict, rewards, dones, infos = self.env.step(actions)
                     obs, priv, hist = obs_dict["obs"], obs_dict["privileged_obs"], obs_dict["obs_history"]
                     self.alg.process_env_step(rewards[:n_train], dones[:n_train], infos)
+                    for key in ("train/episode", "eval/episode"):  # (__init__.py:145-151)
+                        if key in infos:
+                            with lg.Prefix(metrics=key):
+                                lg.store_metrics(**infos[key])
                 self.alg.compute_returns(obs[:n_train], priv[:n_train])
                 if it % eval_freq == 0:
                     self.env.reset_evaluation_envs()
@@ -122,8 +98,9 @@ class Runner:
             lg.store_metrics(time_elapsed=lg.since("start"), time_iter=lg.split("epoch"), adaptation_loss=ma,
                              mean_value_loss=mv, mean_surrogate_loss=ms)
             self.tot_timesteps += self.num_steps_per_env * self.env.num_envs
-            if (it + 1) % RunnerArgs.log_freq == 0:
+            if lg.every(RunnerArgs.log_freq, "iteration", start_on=1):
                 lg.log_metrics_summary(key_values={"timesteps": self.tot_timesteps, "iterations": it})
+                lg.job_running()
             if RunnerArgs.save_interval and it % RunnerArgs.save_interval == 0:
                 self.save(it)
         self.current_learning_iteration += num_learning_iterations
@@ -139,16 +116,19 @@ class Runner:
         return ac.act_student(obs[n_train:], hist[n_train:])
 
     def save(self, it):
+        """__init__.py:222-242: the state dict as checkpoints/ac_weights_{it:06d}.pt, duplicated to ac_weights_last.pt,
+        and the TorchScript adaptation module / actor body uploaded to checkpoints/ (nothing without a run directory)."""
         lg = self.logger
-        if not lg.root:
+        if not lg.run_dir:
             return
-        sd = self.alg.actor_critic.state_dict()
-        lg.torch_save(sd, f"checkpoints/ac_weights_{it:06d}.pt")
-        lg.torch_save(sd, "checkpoints/ac_weights_last.pt")
-        path = os.path.join(lg.root, "checkpoints")
-        ac = self.alg.actor_critic
-        torch.jit.script(copy.deepcopy(ac.adaptation_module).to("cpu")).save(os.path.join(path, "adaptation_module_latest.jit"))
-        torch.jit.script(copy.deepcopy(ac.actor_body).to("cpu")).save(os.path.join(path, "body_latest.jit"))
+        with lg.Sync():
+            lg.torch_save(self.alg.actor_critic.state_dict(), f"checkpoints/ac_weights_{it:06d}.pt")
+            lg.duplicate(f"checkpoints/ac_weights_{it:06d}.pt", "checkpoints/ac_weights_last.pt")
+            path = os.path.join(lg.run_dir, "checkpoints")
+            ac = self.alg.actor_critic
+            torch.jit.script(copy.deepcopy(ac.adaptation_module).to("cpu")).save(
+                os.path.join(path, "adaptation_module_latest.jit"))
+            torch.jit.script(copy.deepcopy(ac.actor_body).to("cpu")).save(os.path.join(path, "body_latest.jit"))
 
     def get_inference_policy(self, device=None):
         self.alg.actor_critic.eval()

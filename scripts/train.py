@@ -1,5 +1,9 @@
-"""Drop-in for the reference's scripts/train.py (scripts/train.py:1-54): same imports and calls,
-resolved to the MI355X implementation.  Usage: python scripts/train.py [--iterations N]"""
+"""The reference's scripts/train.py flow (scripts/train.py:1-54) on this framework: the same imports — isaacgym and
+ml_logger resolve to the package's stand-ins — and the same calls (logger.configure / log_text / log_params,
+VelocityTrackingEasyEnv, HistoryWrapper, Runner(env, device), runner.learn).  The reference's own file runs unchanged
+against the package too (tests/test_script_surface.py checks what it imports and calls); this copy only adds
+--iterations / --robot / --root so a short run can be asked for.
+usage: python scripts/train.py [--iterations N] [--robot mc|go1] [--root DIR]"""
 import argparse
 import os
 import sys
@@ -8,7 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rapid-locomotion-rl_amd"))
 
 
-def train_mc(headless=True, iterations=4000, robot="mc", run_dir=None):
+def train_mc(headless=True, iterations=4000, robot="go1"):
+    import isaacgym
+    assert isaacgym
     import torch  # noqa: F401
 
     from mini_gym.envs.base.legged_robot_config import Cfg
@@ -16,21 +22,39 @@ def train_mc(headless=True, iterations=4000, robot="mc", run_dir=None):
     from mini_gym.envs.mini_cheetah.mini_cheetah_config import config_mini_cheetah
     from mini_gym.envs.mini_cheetah.velocity_tracking import VelocityTrackingEasyEnv
     from mini_gym.envs.wrappers.history_wrapper import HistoryWrapper
-    from mini_gym_learn.ppo import Runner
-    from lrl.ppo.runner import Logger
+    from mini_gym_learn.ppo import Runner, RunnerArgs
+    from mini_gym_learn.ppo.actor_critic import AC_Args
+    from mini_gym_learn.ppo.ppo import PPO_Args
+    from ml_logger import logger
 
-    (config_mini_cheetah if robot == "mc" else config_go1)(Cfg)
+    (config_mini_cheetah if robot == "mc" else config_go1)(Cfg)  # (the reference's file: config_go1)
     env = VelocityTrackingEasyEnv(sim_device="cuda:0", headless=headless, cfg=Cfg)
+    logger.log_params(AC_Args=vars(AC_Args), PPO_Args=vars(PPO_Args), RunnerArgs=vars(RunnerArgs), Cfg=vars(Cfg))
     env = HistoryWrapper(env)
-    runner = Runner(env, device="cuda:0", logger=Logger(run_dir))
+    runner = Runner(env, device="cuda:0")
     runner.learn(num_learning_iterations=iterations, init_at_random_ep_len=True, eval_freq=100)
     return runner
 
 
 if __name__ == "__main__":
+    from pathlib import Path
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--iterations", type=int, default=4000)
-    ap.add_argument("--robot", default="mc", choices=["mc", "go1"])
-    ap.add_argument("--run-dir", default=None)
+    ap.add_argument("--robot", default="go1", choices=["mc", "go1"])
+    ap.add_argument("--root", default=None, help="run root (default: <package>/runs, as MINI_GYM_ROOT_DIR/runs)")
     a = ap.parse_args()
-    train_mc(iterations=a.iterations, robot=a.robot, run_dir=a.run_dir)
+    from ml_logger import logger
+    from mini_gym import MINI_GYM_ROOT_DIR
+
+    stem = Path(__file__).stem
+    logger.configure(logger.utcnow(f"rapid-locomotion/%Y-%m-%d/{stem}/%H%M%S.%f"),
+                     root=Path(a.root or f"{MINI_GYM_ROOT_DIR}/runs").resolve())
+    logger.log_text("""
+                charts:
+                - yKey: train/episode/rew_total/mean
+                  xKey: iterations
+                - yKey: train/episode/command_area/mean
+                  xKey: iterations
+                """, filename=".charts.yml", dedent=True)
+    train_mc(headless=True, iterations=a.iterations, robot=a.robot)
