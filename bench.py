@@ -212,6 +212,41 @@ def init_world(args):
     return world, rank, local, backend
 
 
+def device_identity(local_dev):
+    """(host, PCI bus / device id, UUID) of a visible device: what tells two ranks' GPUs apart."""
+    import socket
+    p = torch.cuda.get_device_properties(local_dev)
+    uuid = str(getattr(p, "uuid", ""))
+    pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    return socket.gethostname(), pci, uuid
+
+
+def check_rank_devices(world, rank, local_dev, backend):
+    """Every rank names its device (stderr) and, with RCCL, the ranks gather them: two ranks on one physical GPU is an
+    error (RCCL's ring over xGMI needs one rank per GPU; a duplicate would also double-count a GPU in the scaling line).
+    Returns the per-rank device list for the JSON line."""
+    ident = device_identity(local_dev)
+    print(f"[bench rank {rank}/{world}] pid {os.getpid()} cuda:{local_dev} host {ident[0]} pci {ident[1]} "
+          f"uuid {ident[2]} backend {backend if world > 1 else None}", file=sys.stderr, flush=True)
+    if world == 1:
+        return [{"rank": 0, "device": local_dev, "pci": ident[1]}]
+    got = [None] * world
+    dist.all_gather_object(got, (rank, local_dev, ident))
+    devices = [{"rank": r, "device": d, "host": h, "pci": pci, "uuid": u} for r, d, (h, pci, u) in sorted(got)]
+    if backend == "nccl":
+        seen = {}
+        for e in devices:
+            key = (e["host"], e["pci"], e["uuid"])
+            if key in seen:
+                raise SystemExit(f"bench.py: ranks {seen[key]} and {e['rank']} share GPU {key} — one rank per GPU")
+            seen[key] = e["rank"]
+        if rank == 0:
+            print(f"[bench] RCCL world {dist.get_world_size()}: " + ", ".join(f"r{e['rank']}=cuda:{e['device']}"
+                                                                              f"@{e['pci']}" for e in devices),
+                  file=sys.stderr, flush=True)
+    return devices
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,6 +292,7 @@ def main():
     local_dev = local % ndev
     torch.cuda.set_device(local_dev)
     dev = f"cuda:{local_dev}"
+    devices = check_rank_devices(world, rank, local_dev, backend)
 
     from lrl import config as lcfg
     from lrl.env import LeggedRobotEnv
@@ -349,7 +385,7 @@ def main():
                        "envs_per_gpu": ENVS_PER_GPU, "global_envs": world * ENVS_PER_GPU,
                        "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
                        "parallelism": f"dp{world}", "world_size": world,
-                       "backend": (backend if world > 1 else None),
+                       "backend": (backend if world > 1 else None), "devices": devices,
                        "policy": "ActorCritic 42/18/630->12, random init; teacher PPO + student adaptation update"},
             "ppo_iters_per_s": round(args.steps / elapsed, 3),
             "env_only_env_steps_per_s_per_gpu": round(env_only, 1),

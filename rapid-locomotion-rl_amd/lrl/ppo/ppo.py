@@ -55,6 +55,20 @@ def _world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def _all_reduce_(t):
+    """Sum ``t`` over the ranks, in place.  RCCL reduces device memory directly; gloo (the CPU / one-GPU rehearsals)
+    reduces host memory, so a device tensor is staged through a synchronous host copy rather than gloo's own
+    CUDA-tensor path (its side stream and pinned staging buffers are one more ordering to reason about) — every call
+    site (gradients, KL, advantage statistics) goes the same way."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        host = t.cpu()
+        dist.all_reduce(host)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t)
+    return t
+
+
 class PPO:
     actor_critic: ActorCritic
 
@@ -165,13 +179,7 @@ class PPO:
             last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
         reduce = None
         if _world() > 1:
-            def reduce(stats):
-                if dist.get_backend() == "gloo":  # gloo reduces host memory: stage through a synchronous copy rather
-                    host = stats.cpu()            # than gloo's own CUDA-tensor path (side stream + pinned buffers)
-                    dist.all_reduce(host)
-                    return host.to(stats.device)
-                dist.all_reduce(stats)
-                return stats
+            reduce = _all_reduce_
         self.storage.compute_returns(last_values, PPO_Args.gamma, PPO_Args.lam, reduce_stats=reduce)
 
     def _allreduce_grads(self, params):
@@ -179,7 +187,7 @@ class PPO:
         if not grads:
             return
         flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat)
+        _all_reduce_(flat)
         flat /= _world()
         off = 0
         for g in grads:
@@ -302,7 +310,7 @@ class PPO:
                 _abi.check(L.lrl_ppo_forward_backward(C.byref(net), ptr(params), ptr(grads), C.byref(batch),
                                                       C.byref(hp), ptr(ws), ptr(ctrl), stream))
                 if world > 1:
-                    dist.all_reduce(main)
+                    _all_reduce_(main)
                 st["steps"][0] += 1
                 _abi.check(L.lrl_ppo_optimizer_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
                                                     C.c_int64(st["steps"][0]), C.c_float(scale), C.byref(hp),
@@ -323,7 +331,7 @@ class PPO:
                                                                      C.byref(batch_b), ptr(ws_b), ptr(ctrl), stream_b))
                     if world > 1:
                         with torch.cuda.stream(sb):
-                            dist.all_reduce(adapt)
+                            _all_reduce_(adapt)
                     st["steps"][1] += 1
                     _abi.check(L.lrl_ppo_adaptation_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
                                                          C.c_int64(st["steps"][1]),
@@ -380,8 +388,7 @@ class PPO:
                         - 0.5, axis=-1)
                     kl_mean = torch.mean(kl)
                     if _world() > 1:
-                        kl_mean = kl_mean.clone()
-                        dist.all_reduce(kl_mean)
+                        kl_mean = _all_reduce_(kl_mean.clone())
                         kl_mean /= _world()
                     kl_mean = kl_mean.item()
                     if kl_mean > PPO_Args.desired_kl * 2.0:
