@@ -143,7 +143,8 @@ _lib = None
 _CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 # the files and order of csrc/Makefile's SRC_HASH (SRCS then HDRS)
 _HASHED = ["lrl_env.hip", "lrl_aux.hip", "lrl_gae.hip", "lrl_gemm.hip", "lrl_ppo.hip", "lrl_capi.cpp", "lrl_curriculum.cpp",
-           "lrl_curriculum_dev.hip", "lrl_env_flat.hip", "lrl_kparams.h", "lrl_gemm.h", "../../include/lrl.h", "../../include/lrl_philox.h"]
+           "lrl_curriculum_dev.hip", "lrl_env_flat.hip", "lrl_kparams.h", "lrl_gemm.h", "../../include/lrl.h", "../../include/lrl_philox.h",
+           "Makefile"]  # (the build flags too: a library built with other flags is stale)
 
 
 def source_hash():

@@ -460,11 +460,7 @@ def test_multi_rank_full_iteration_at_bench_shape(robot, world):
 
 @pytest.mark.multiproc
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("legacy_fork,n", [
-    pytest.param(True, N_BENCH, marks=pytest.mark.xfail(
-        strict=False, reason="open (DESIGN.md §9, round 5): the 2 x 2048 run (two processes on one GPU) intermittently diverges "
-        "in a few envs from step 0 on, the 1 x 4096 run is reproducible (profiles/r5zl_sharding_*.txt)")),
-    (False, N_BENCH), (False, 512)])
+@pytest.mark.parametrize("legacy_fork,n", [(True, N_BENCH), (False, N_BENCH), (False, 512)])
 def test_rollout_does_not_depend_on_the_gpu_count(legacy_fork, n):
     """every draw is keyed by the global env id (env: env_offset; policy noise: PPO.row_offset) and the
     env origins are the global layout's, so 2 ranks x 2048 Mini Cheetah envs roll out exactly what 1 x 4096 does: a

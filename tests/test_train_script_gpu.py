@@ -21,6 +21,8 @@ def test_reference_train_flow_writes_a_run(tmp_path):
     from mini_gym_learn.ppo import RunnerArgs
     from mini_gym_learn.ppo.actor_critic import ActorCritic
     saved = copy.deepcopy(Cfg)
+    saved_args = dict(save_interval=RunnerArgs.save_interval, log_freq=RunnerArgs.log_freq)
+    RunnerArgs.save_interval, RunnerArgs.log_freq = 400, 1  # the reference's defaults (other tests zero them)
     spec = importlib.util.spec_from_file_location("lrl_scripts_train", os.path.join(ROOT, "scripts", "train.py"))
     script = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(script)
@@ -44,7 +46,9 @@ def test_reference_train_flow_writes_a_run(tmp_path):
         want = {k: v.cpu() for k, v in runner.alg.actor_critic.state_dict().items()}
         assert list(got) == list(want) and all(torch.equal(got[k], want[k]) for k in want)
         runner.env.env.close()
+        assert len(logger.load_pkl("metrics.pkl")) == 2  # log_freq 1: one summary per iteration
     finally:
+        RunnerArgs.save_interval, RunnerArgs.log_freq = saved_args["save_interval"], saved_args["log_freq"]
         logger.configure(None)
         Cfg.__dict__.clear()
         Cfg.__dict__.update(saved.__dict__)
