@@ -298,7 +298,9 @@ int32_t lrl_sim_reset_idx(lrl_sim* sim, const int32_t* env_ids, int32_t n, void*
  *                x_init_range, y_init_range, (k, 2)) with xy_lo = x_init_range and xy_span = float32(y_init_range -
  *                x_init_range) rounded from the python-float difference — in that float32 order.
  * The uniforms (motor-strength / Kp / Kd redraws of _randomize_dof_props :544-560, then x, y) come from the
- * sim's counter RNG, or with flags & LRL_STEP_INJECT_UNIFORM from the lrl_sim_inject_reset_uniforms buffer. */
+ * sim's counter RNG, or with flags & LRL_STEP_INJECT_UNIFORM from the lrl_sim_inject_reset_uniforms buffer.
+ * env_ids must be distinct (as the reference's torch.arange / nonzero() id lists are): one thread resets each listed
+ * env and bumps that env's reset counter (the key of its draws), so an id listed twice would race on both. */
 int32_t lrl_sim_reset_idx_ex(lrl_sim* sim, const int32_t* env_ids, int32_t n, int32_t root_mode, float xy_lo,
                              float xy_span, float x_off, float y_off, uint32_t flags, void* stream);
 /* Injected reset uniforms for parity tests: u [n, 5] f32 device, row t = (motor strength, Kp, Kd, x, y) of the

@@ -197,11 +197,31 @@ class ML_Logger:
             self.metrics[key].append(v)
 
     def log_metrics_summary(self, key_values=None, default_stats="mean", **_):
-        s = {}
+        """``{key}/{stat}`` over everything stored since the last summary, plus ``key_values``; device scalars (the
+        Runner stores its losses and episode means without a host sync) are reduced on their device and fetched in one
+        copy, not one sync per stored value."""
+        s, dev_keys, dev_stats = {}, [], []
         for k, vs in self.metrics.items():
-            if vs:
+            if not vs:
+                continue
+            tens = [v for v in vs if hasattr(v, "detach")]
+            if tens and len(tens) == len(vs):
+                import torch
+                t = torch.stack([v.detach().reshape(()).to(torch.float64) for v in tens])
+                dev_keys.append(k)
+                dev_stats.append(getattr(torch, default_stats)(t))
+            else:
                 arr = np.array([float(v) for v in vs], dtype=np.float64)
                 s[f"{k}/{default_stats}"] = float(getattr(np, default_stats)(arr))
+        if dev_stats:
+            import torch
+            by_dev = {}
+            for k, v in zip(dev_keys, dev_stats):
+                by_dev.setdefault(v.device, []).append((k, v))
+            for items in by_dev.values():
+                vals = torch.stack([v for _, v in items]).tolist()  # (one device -> host copy per device)
+                for (k, _), x in zip(items, vals):
+                    s[f"{k}/{default_stats}"] = float(x)
         s.update(key_values or {})
         self.summaries.append(s)
         self.metrics.clear()
