@@ -1828,6 +1828,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   if (__any((int)(sown != 0ull)))
     for (uint64_t m = sown >> (M.nsph + LRL_NUM_DOF); m; m &= m - 1ull)
       self_setup(M, Sch, R, free_spheres(M, active), __builtin_ctzll(m));
+  // (mirrored quads: the warm start below reads the z / e rows another quad's lanes just built — one LDS fence, as at the
+  // leg pass's end, so no compiler reordering can move those reads above the builds)
+  if constexpr (MIRROR > 1) __syncthreads();
   // warm start: spheres in contact in the previous sub-step keep their impulse (world frame); the owner
   // lanes apply them in parallel and the base-velocity changes are summed over the quad
   {
@@ -1993,12 +1996,13 @@ __device__ __forceinline__ float height_sample(const KParams* __restrict__ K, co
 // ------------------------------------------------------------------------------------------------
 // the fused step kernel
 // ------------------------------------------------------------------------------------------------
-// compute_observations (legged_robot.py:342-417) in two parts: obs_values writes the row's values;
-// obs_noise_clip adds U[-1,1] x noise_vec from the counter RNG keyed by (env, step counter, 4-entry chunk)
-// and clips, for chunks c0, c0 + cstep, ... (the step kernel spreads the chunks over an env's 4 lanes; a
-// re-evaluation after a reset draws the same noise)
-__device__ __forceinline__ void obs_values(const lrl_env_params& P, V3 blv, V3 bav, V3 pg, const float* cmd,
-                                           const float* q, const float* qd, const float* act, float* ob) {
+// compute_observations (legged_robot.py:342-417) in two parts: the row's values — obs_base_values writes its base
+// entries ([lin vel, ang vel,] gravity, [commands]), the step kernel's quads write the dof positions / velocities and the
+// actions after them (each lane its leg's joints) — then obs_noise_clip adds U[-1,1] x noise_vec from the counter RNG
+// keyed by (env, step counter, 4-entry chunk) and clips, for chunks c0, c0 + cstep, ... (the step kernel spreads the
+// chunks over an env's lanes; a re-evaluation after a reset draws the same noise)
+__device__ __forceinline__ void obs_base_values(const lrl_env_params& P, V3 blv, V3 bav, V3 pg, const float* cmd,
+                                                float* ob) {
   int o = 0;
   if (P.observe_vel) {
     ob[o++] = blv.x * P.obs_scale_lin_vel; ob[o++] = blv.y * P.obs_scale_lin_vel; ob[o++] = blv.z * P.obs_scale_lin_vel;
@@ -2009,12 +2013,6 @@ __device__ __forceinline__ void obs_values(const lrl_env_params& P, V3 blv, V3 b
 #pragma unroll
     for (int k = 0; k < 3; ++k) ob[o++] = cmd[k] * P.commands_scale[k];
   }
-#pragma unroll
-  for (int j = 0; j < 12; ++j) ob[o + j] = (q[j] - P.default_dof_pos[j]) * P.obs_scale_dof_pos;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) ob[o + 12 + j] = qd[j] * P.obs_scale_dof_vel;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) ob[o + 24 + j] = act[j];
 }
 __device__ __forceinline__ void obs_noise_clip(const lrl_env_params& P, const KState& S, int e, uint64_t genv,
                                                int64_t step_counter, bool inject, float* ob, int c0, int cstep) {
@@ -2090,7 +2088,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     st.hi[j] = K->dof_hi[3 * ql + j];
     st.llam[j] = 0.f;
   }
-  float act[12], tau[12];
+  float act[12];
   {
     const float c = P.clip_actions;
 #pragma unroll
@@ -2199,16 +2197,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     prof_t = clock64();
 #endif
   }
-  // the last sub-step's torques and the joint state of all 12 joints (rewards, obs, buffers): from the quad's 4 lanes
-  float q12[12], qd12[12];
-#pragma unroll
-  for (int l = 0; l < 4; ++l)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      tau[3 * l + j] = quad_bcast(tau3[j], l);
-      q12[3 * l + j] = quad_bcast(st.q[j], l);
-      qd12[3 * l + j] = quad_bcast(st.qd[j], l);
-    }
 #ifdef LRL_ENV_PROFILE
   prof_t = clock64();
 #endif
@@ -2217,12 +2205,18 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
   float cmd[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) cmd[k] = S.commands[k * N + e];
-  float la[12], lqd[12], fat[4];
+  // the joint-indexed reward inputs of this lane's leg (the joint terms are summed over the quad, below)
+  float la3[3], lqdp3[3], slo3[3], shi3[3], dvl3[3], ddp3[3], fat[4];
   uint8_t lc[4];
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    la[j] = S.last_actions[j * N + e];
-    lqd[j] = S.last_dof_vel[j * N + e];
+  for (int j = 0; j < 3; ++j) {
+    const int jj = 3 * ql + j;
+    la3[j] = S.last_actions[jj * N + e];
+    lqdp3[j] = S.last_dof_vel[jj * N + e];
+    slo3[j] = P.soft_dof_pos_lower[jj];
+    shi3[j] = P.soft_dof_pos_upper[jj];
+    dvl3[j] = P.dof_vel_limits[jj];
+    ddp3[j] = P.default_dof_pos[jj];
   }
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
@@ -2347,6 +2341,77 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     st.V[0] = P.push_span * u0 + P.push_lo;  // (upper - lower) * torch.rand + lower
     st.V[1] = P.push_span * u1 + P.push_lo;
   }
+  // termination (legged_robot.py:190-202): the contact test above, the body height, and (upstream) the time-out
+  if (P.use_terminal_body_height && st.pos[2] < P.terminal_body_height) rst = 1;
+  // time-outs (legged_robot.py:196-198, commented out in the fork — Q2): upstream semantics only
+  const int tout = (P.auto_reset && eplen > P.max_episode_length) ? 1 : 0;
+  rst |= tout;
+  // ---- the reward terms' values (:1506-1646), in every lane of the env ----
+  // The terms over the 12 joints are summed from each lane's own leg (its 3 joints, in joint order) and then over the
+  // quad ((leg 0 + leg 1) + (leg 2 + leg 3)): a quarter of the sequential form's work, and no 12-wide copies of the joint
+  // state in every lane; the other terms are a few operations each, the same in every lane.  The lead lane then adds the
+  // active terms in the configured order (below).
+  float jt[10];  // torques, energy, energy expenditure, dof_vel, dof_acc, action_rate, dof_pos / dof_vel / torque limits,
+                 // stand_still (before its command gate)
+  {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) jt[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float tq = tau3[j], q = st.q[j], qd = st.qd[j];
+      jt[0] += sq(tq);
+      jt[1] += tq * qd;
+      jt[2] += fmaxf(tq * qd, 0.f);
+      jt[3] += sq(qd);
+      jt[4] += sq((lqdp3[j] - qd) / P.dt);
+      jt[5] += sq(la3[j] - act3[j]);
+      float o = -fminf(q - slo3[j], 0.f);
+      o += fmaxf(q - shi3[j], 0.f);
+      jt[6] += o;
+      jt[7] += fminf(fmaxf(fabsf(qd) - dvl3[j] * P.soft_dof_vel_limit, 0.f), 1.f);
+      jt[8] += fmaxf(fabsf(tq) - lim3[j] * P.soft_torque_limit, 0.f);
+      jt[9] += fabsf(q - ddp3[j]);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) jt[k] = quad_sum(jt[k]);
+  }
+  bool has_air = false;  // _reward_feet_air_time updates feet_air_time / last_contacts only when it is a term
+  for (int t = 0; t < P.num_reward_terms; ++t) has_air |= P.reward_term[t] == LRL_R_FEET_AIR_TIME;
+  float air = 0.f;
+  if (has_air) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      int c = ff[f][2] > 1.0f;
+      int filt = c || lc[f];
+      lc[f] = (uint8_t)c;
+      float first = (fat[f] > 0.f && filt) ? 1.f : 0.f;
+      fat[f] = fat[f] + P.dt;
+      air += (fat[f] - 0.5f) * first;
+      if (filt) fat[f] = 0.f;
+    }
+  }
+  const float cnorm = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
+  // the observation row's values (compute_observations :342-417) into the LDS tile, spread over the env's quads: quad 0
+  // the dof positions, 1 the dof velocities, 2 the actions (each lane its leg's 3 joints), quad 3's lead lane the base
+  // entries; the same expressions, so the same values as one lane writing the row
+  {
+    float* ob = otile + es * NO;
+    const int o = (P.observe_vel ? 6 : 0) + 3 + (P.observe_command ? 3 : 0);
+    const int qi = mirror_quad();  // (one quad per env on the terrain mesh: it writes all four groups)
+    if (MIRROR == 1 || qi == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ob[o + 3 * ql + j] = (st.q[j] - ddp3[j]) * P.obs_scale_dof_pos;
+    }
+    if (MIRROR == 1 || qi == 1) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ob[o + 12 + 3 * ql + j] = st.qd[j] * P.obs_scale_dof_vel;
+    }
+    if (MIRROR == 1 || qi == 2) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ob[o + 24 + 3 * ql + j] = act3[j];
+    }
+    if ((MIRROR == 1 || qi == 3) && ql == 0) obs_base_values(P, blv, bav, pg, cmd, ob);
+  }
   // post-physics rewards, observations and the per-env state write-back: lane 0 of each env (of its first quad)
   if (ql == 0 && mirror_quad() == 0) {
   float ms_e[12];
@@ -2384,10 +2449,6 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       for (int j = 0; j < 12; ++j) S.kd[j * N + e] = v;
     }
   }
-  if (P.use_terminal_body_height && st.pos[2] < P.terminal_body_height) rst = 1;
-  // time-outs (legged_robot.py:196-198, commented out in the fork — Q2): upstream semantics only
-  const int tout = (P.auto_reset && eplen > P.max_episode_length) ? 1 : 0;
-  rst |= tout;
 
   LRL_PROF(11)  // post-physics loads, teleport, DR redraw
   // rewards
@@ -2404,79 +2465,29 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
       case LRL_R_BASE_HEIGHT:  // mean(z - measured_heights) (:1518-1521); measured_heights = 0 without a scan
         r = sq((P.measure_heights ? hsum / (float)P.num_height_points : st.pos[2]) - P.base_height_target);
         break;
-      case LRL_R_TORQUES:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += sq(tau[j]);
-        break;
-      case LRL_R_ENERGY:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += tau[j] * qd12[j];
-        break;
-      case LRL_R_ENERGY_EXPENDITURE:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += fmaxf(tau[j] * qd12[j], 0.f);
-        break;
-      case LRL_R_DOF_VEL:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += sq(qd12[j]);
-        break;
-      case LRL_R_DOF_ACC:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += sq((lqd[j] - qd12[j]) / P.dt);
-        break;
-      case LRL_R_ACTION_RATE:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += sq(la[j] - act[j]);
-        break;
+      case LRL_R_TORQUES: r = jt[0]; break;
+      case LRL_R_ENERGY: r = jt[1]; break;
+      case LRL_R_ENERGY_EXPENDITURE: r = jt[2]; break;
+      case LRL_R_DOF_VEL: r = jt[3]; break;
+      case LRL_R_DOF_ACC: r = jt[4]; break;
+      case LRL_R_ACTION_RATE: r = jt[5]; break;
       case LRL_R_COLLISION: r = collision; break;
       case LRL_R_SURVIVAL: r = rst ? 0.f : 1.f; break;
-      case LRL_R_DOF_POS_LIMITS:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) {
-          float o = -fminf(q12[j] - P.soft_dof_pos_lower[j], 0.f);
-          o += fmaxf(q12[j] - P.soft_dof_pos_upper[j], 0.f);
-          r += o;
-        }
-        break;
-      case LRL_R_DOF_VEL_LIMITS:
-#pragma unroll
-        for (int j = 0; j < 12; ++j)
-          r += fminf(fmaxf(fabsf(qd12[j]) - P.dof_vel_limits[j] * P.soft_dof_vel_limit, 0.f), 1.f);
-        break;
-      case LRL_R_TORQUE_LIMITS:
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += fmaxf(fabsf(tau[j]) - P.torque_limits[j] * P.soft_torque_limit, 0.f);
-        break;
+      case LRL_R_DOF_POS_LIMITS: r = jt[6]; break;
+      case LRL_R_DOF_VEL_LIMITS: r = jt[7]; break;
+      case LRL_R_TORQUE_LIMITS: r = jt[8]; break;
       case LRL_R_TRACKING_LIN_VEL: {
         float err = sq(cmd[0] - blv.x) + sq(cmd[1] - blv.y);
         r = expf(-err / P.tracking_sigma);
       } break;
       case LRL_R_TRACKING_ANG_VEL: r = expf(-sq(cmd[2] - bav.z) / P.tracking_sigma_yaw); break;
-      case LRL_R_FEET_AIR_TIME: {
-        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          int c = ff[f][2] > 1.0f;
-          int filt = c || lc[f];
-          lc[f] = (uint8_t)c;
-          float first = (fat[f] > 0.f && filt) ? 1.f : 0.f;
-          fat[f] = fat[f] + P.dt;
-          r += (fat[f] - 0.5f) * first;
-          if (filt) fat[f] = 0.f;
-        }
-        r = r * (cn > 0.1f ? 1.f : 0.f);
-      } break;
+      case LRL_R_FEET_AIR_TIME: r = air * (cnorm > 0.1f ? 1.f : 0.f); break;  // (feet state updated above)
       case LRL_R_STUMBLE:
 #pragma unroll
         for (int f = 0; f < 4; ++f)
           if (sqrtf(ff[f][0] * ff[f][0] + ff[f][1] * ff[f][1]) > 5.f * fabsf(ff[f][2])) r = 1.f;
         break;
-      case LRL_R_STAND_STILL: {
-        float cn = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]);
-#pragma unroll
-        for (int j = 0; j < 12; ++j) r += fabsf(q12[j] - P.default_dof_pos[j]);
-        r = r * (cn < 0.1f ? 1.f : 0.f);
-      } break;
+      case LRL_R_STAND_STILL: r = jt[9] * (cnorm < 0.1f ? 1.f : 0.f); break;
       case LRL_R_FEET_CONTACT_FORCES:
 #pragma unroll
         for (int f = 0; f < 4; ++f) r += fmaxf(nrm3(ff[f][0], ff[f][1], ff[f][2]) - P.max_contact_force, 0.f);
@@ -2540,8 +2551,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
 
   // observations / privileged observations -> LDS tiles [env slot][.]
   LRL_PROF(12)  // rewards, termination, episode / command sums
-  obs_values(P, blv, bav, pg, cmd, q12, qd12, act, otile + es * NO);
-  priv_row(P, S, e, payload, cb, ms_e, ptile + es * LRL_NUM_PRIV);
+  priv_row(P, S, e, payload, cb, ms_e, ptile + es * LRL_NUM_PRIV);  // (the obs row's values: spread above)
 
   LRL_PROF(13)  // obs / priv rows
   // ---- write back the SoA state ----
@@ -2711,10 +2721,10 @@ inline namespace LRL_ENV_NS {
 // 16 lanes per env (OBS_LANES): lane c forms, noises, clips and stores only its 4-wide chunks of the observation row
 // (chunk i0 / 4 on lane (i0 / 4) % 16: one Philox draw each instead of the whole row's draws on one thread), reading
 // the state entries those need; lane 0 writes the base-frame velocities, the privileged row and the last_* buffers.
-// Every element's value, draw and operation order are the one-thread form's (obs_values / obs_noise_clip), so the
-// rows are bit-identical.
+// Every element's value, draw and operation order are the step kernel's (obs_base_values + its quads' joint entries /
+// obs_noise_clip), so the rows are bit-identical.
 constexpr int OBS_LANES = 16;
-// observation entry i of env e (obs_values' layout: [lin vel, ang vel,] gravity, [commands,] dof pos, dof vel,
+// observation entry i of env e (the step kernel's layout: [lin vel, ang vel,] gravity, [commands,] dof pos, dof vel,
 // actions, then the height rows against base height z)
 __device__ __forceinline__ float obs_entry(const lrl_env_params& P, const KState& S, int e, int i, V3 blv, V3 bav,
                                            V3 pg) {
