@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define LRL_ABI_VERSION 4
+#define LRL_ABI_VERSION 5
 
 #define LRL_OK 0
 #define LRL_E_INVALID (-1)  /* bad argument / unsupported configuration */
@@ -193,6 +193,12 @@ typedef struct lrl_env_params {
   int32_t push_robots;
   int32_t push_interval;
   float push_lo, push_span;
+  /* Cfg.sim.physx.solver_type (legged_robot_config.py:247; 1 = TGS): the contact / limit solve runs solver_iterations
+   * sub-iterations of h = sim_dt / solver_iterations, each sweeping the rows once with targets from the separations
+   * moved by the motion so far, and positions integrate the accumulated motion.  0 = PGS: the
+   * iterations sweep the whole sub-step with the start targets.  Plane ground only (the terrain-mesh build solves
+   * with PGS and the host passes 0 there). */
+  int32_t solver_tgs;
 } lrl_env_params;
 
 /* ------------------------------------------------------------------------------------------

@@ -332,7 +332,8 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
   HIPCHECK(hipMemcpy(s->d_foot_xyz, model->foot_xyz, sizeof(float) * 12, hipMemcpyHostToDevice));
   // env step kernel LDS: wg_envs envs per workgroup: leg blocks + contact rows, or the obs tiles
   const int wg_envs = params->terrain_mesh ? LRL_ENV_WG_ENVS_MESH : LRL_ENV_WG_ENVS_FLAT;
-  int lds_contacts = (4 * 51 + model->num_spheres * 67) * wg_envs * 4;  // LEGF, NSF of lrl_env.hip
+  const int legf = params->terrain_mesh ? LRL_LEGF_MESH : LRL_LEGF_FLAT, nsf = params->terrain_mesh ? LRL_NSF_MESH : LRL_NSF_FLAT;
+  int lds_contacts = (4 * legf + model->num_spheres * nsf) * wg_envs * 4;  // LEGF, NSF of lrl_env.hip
   // terrain query vertex block, float4 [16][lanes]; the joint-limit rows (12 x 19 fields per env) alias it after the
   // queries, and have their own region on the plane
   lds_contacts += params->terrain_mesh ? 16 * LRL_ENV_LANES * 16 : LRL_NUM_DOF * 19 * wg_envs * 4;

@@ -49,7 +49,7 @@
 #endif
 #define MIRROR (BLOCK / (QL * ENVS))  // quads per env
 static_assert(MIRROR == 1 || MIRROR == 4, "an env has one quad or four mirrored quads");
-#define NSF 67  // LDS fields per contact sphere (map above contact_setup)
+#define NSF (MIRROR > 1 ? LRL_NSF_FLAT : LRL_NSF_MESH)  // LDS fields per contact sphere (map above contact_setup)
 #define LIMF 19  // LDS fields per joint-limit row (map above limit_setup)
 
 namespace lrl {
@@ -198,7 +198,9 @@ __device__ __forceinline__ float sv_get(const SV& s, int r) {
 //   36..41 D^-1 (00 11 22 01 02 12)   42..44 per-joint bias / solve scratch
 //   45..47 leg joint rates at the start of the contact solve   48..50 Y = sum of D^-1 p_l over the
 //   impulses applied to this leg (lazy propagation: qd_l = qd0_l + Y_l - K_l (v_b - v_b0))
-#define LEGF 51
+//   51..53 (plane build, TGS) dz = sum over the sub-iterations of h (q0_l + Y_l) = the leg's joint motion + K_l dx_b
+#define LEGF (MIRROR > 1 ? LRL_LEGF_FLAT : LRL_LEGF_MESH)
+#define LF_DZ 51
 #define LI(r, c) ((r) * ((r) + 1) / 2 + (c))
 
 #define KLEGF ((int)(sizeof(KLeg) / sizeof(float)))  // floats of one leg's model table
@@ -556,12 +558,15 @@ __device__ __forceinline__ void contact_frame(V3 n, V3& t1, V3& t2) {
 //          g_d = [x x n_d, n_d] - K_L^T h_d   (the same row maps an impulse to the base: r = sum_d lambda_d g_d)
 //   31..39 h_d = C_L^T n_d (joint-rate row; C_L = joint directions of the carrying joints)
 //   40..57 z_d = S^-1 g_d (base-velocity change per unit impulse)   58..66 e_d = D_L^-1 h_d (change of Y_L)
+//   (plane build, TGS) field 9 holds the sub-step-start separation instead of the velocity target, 67 the restitution
+//   target (-1e30 without one); each sub-iteration forms the target from sep_0 + J_n dx (below)
 // so one Gauss-Seidel update is u_d = g_d . v_b + h_d . (q0_L + Y_L), the cone projection, and
 // v_b += sum_d dlambda_d z_d,  Y_L += sum_d dlambda_d e_d  — short independent dot products.
 #define SF_G 13
 #define SF_H 31
 #define SF_Z 40
 #define SF_E 58
+#define SF_BR 67
 
 // apply a world-frame impulse change dl = (n, t1, t2) of sphere s (leg lsel) to v_b and Y_lsel (every read
 // before the first store, so the rows arrive in one LDS round trip)
@@ -762,7 +767,23 @@ __device__ __forceinline__ uint64_t own_split(uint64_t own, int qi) {
 // forms its part of the three contact-velocity rows, one quad sum gives every lane the same u, the cone
 // projection runs in all four lanes, and each lane updates only what it owns — a quarter of the row reads and
 // fused multiply-adds of the redundant form, and no lane reads what another lane writes (no barrier).
-__device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, float mu, int q, float& vo0, float& vo1) {
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+// TGS (plane build, solver_type 1): the sub-iteration's motion so far, dx = (dx_b spread over the quad as v_b is, dz of
+// the legs in LDS), and what turns a separation into a target (h = dt / iterations)
+struct Tgs {
+  float dxo0, dxo1, ih, baum, maxdep;
+};
+// target of a row whose separation moved from sep0 by the quad's share ds of J_n dx: -sep/h, or Baumgarte below contact
+__device__ __forceinline__ float tgs_target(const Tgs& T, float sep0, float ds) {
+  const float sp = sep0 + quad_sum(ds);
+  return sp >= 0.f ? -sp * T.ih : fminf(-T.baum * sp * T.ih, T.maxdep);
+}
+template <bool TGS>
+__device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, float mu, int q, float& vo0, float& vo1,
+                                              const Tgs& T) {
   const int L = lsel < 0 ? 0 : lsel;
   const bool hj = q < 3;
   const int qh = hj ? q : 2;  // lane 3 reads lane 2's fields and zeroes them by selection (no divergent branches)
@@ -785,9 +806,16 @@ __device__ __forceinline__ void contact_pgs_q(const Lds& M, int s, int lsel, flo
   }
   const float y45 = lg[45 * ENVS], y48 = lg[48 * ENVS];
   const float iWnn = rs[3 * ENVS], Wt1n = rs[4 * ENVS], Wt2n = rs[5 * ENVS];
-  const float i11 = rs[6 * ENVS], i12 = rs[7 * ENVS], i22 = rs[8 * ENVS], b = rs[9 * ENVS];
+  const float i11 = rs[6 * ENVS], i12 = rs[7 * ENVS], i22 = rs[8 * ENVS], b9 = rs[9 * ENVS];
   const float ln0 = rs[10 * ENVS], lt10 = rs[11 * ENVS], lt20 = rs[12 * ENVS];
   const float yq = hj ? y45 + y48 : 0.f;
+  float b;
+  if constexpr (TGS) {  // field 9 = sep0, the restitution target a floor under the sub-iteration's target
+    const float dz = lg[LF_DZ * ENVS];
+    b = fmaxf(tgs_target(T, b9, g0[0] * T.dxo0 + g1[0] * T.dxo1 + (hj ? hv[0] * dz : 0.f)), rs[SF_BR * ENVS]);
+  } else {
+    b = b9;
+  }
   float u[3];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
@@ -889,7 +917,9 @@ __device__ __forceinline__ void limit_apply(const Lds& M, int r, int L, float la
 
 // Gauss-Seidel update of limit row r (leg L, joint j) with the base velocity spread over the quad as in
 // contact_pgs_q: lane q owns v_b[q], v_b[q + 4] (q < 2) and component q of Y_L; lane j adds sigma (q0 + Y)_j
-__device__ __forceinline__ void limit_pgs_q(const Lds& M, int r, int q, float& vo0, float& vo1) {
+// (TGS: LIM_B holds the sub-step-start separation; the row's J dx = g . dx_b + sigma dz_j)
+template <bool TGS>
+__device__ __forceinline__ void limit_pgs_q(const Lds& M, int r, int q, float& vo0, float& vo1, const Tgs& T) {
   const int L = (r * 11) >> 5;  // r / 3 for r < 12
   const int j = r - 3 * L;
   const bool hj = q < 3;
@@ -902,7 +932,12 @@ __device__ __forceinline__ void limit_pgs_q(const Lds& M, int r, int q, float& v
   const float z0 = rq[LIM_Z * ENVS], z1 = rq[(LIM_Z + 4) * ENVS];
   const float ev = row[(LIM_E + qh) * ENVS];
   const float y45 = lg[45 * ENVS], y48 = lg[48 * ENVS];
-  const float iw = row[LIM_IW * ENVS], b = row[LIM_B * ENVS], l0 = row[LIM_LAM * ENVS], sg = row[LIM_SG * ENVS];
+  const float iw = row[LIM_IW * ENVS], b9 = row[LIM_B * ENVS], l0 = row[LIM_LAM * ENVS], sg = row[LIM_SG * ENVS];
+  float b;
+  if constexpr (TGS)
+    b = tgs_target(T, b9, g0 * T.dxo0 + g1 * T.dxo1 + (q == j ? sg * lg[LF_DZ * ENVS] : 0.f));
+  else
+    b = b9;
   float a = g0 * vo0 + g1 * vo1;
   a += q == j ? sg * (y45 + y48) : 0.f;
   const float u = quad_sum(a);
@@ -1396,6 +1431,10 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   const SphLegs SL = sph_legs(K);
   const lrl_env_params& P = K->p;
   const float dt = P.sim_dt, idt = frcp(dt);
+  // TGS (legged_robot_config.py:247 solver_type 1; host: plane only) — the oracle's restatement, lrl_oracle.c
+  // physics_substep: N sub-iterations of h = dt / N, targets from the separations moved by the motion so far, positions
+  // from the accumulated motion
+  const bool tgs = MIRROR > 1 && P.solver_tgs != 0 && P.solver_iterations > 0;
   const M3 R = quat_mat(st.quat[0], st.quat[1], st.quat[2], st.quat[3]);
   const V3 wb = mulT(R, v3(st.W[0], st.W[1], st.W[2]));
   const V3 vb = mulT(R, v3(st.V[0], st.V[1], st.V[2])) - cross(wb, cb);
@@ -1482,8 +1521,16 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
           if (j <= link) u = u + st.qd[j] * cross(aa[j], x - oo[j]);
       }
       const float u0 = dot(Rz, u);
+      const bool bounce = u0 < -P.bounce_threshold_velocity && rest > 0.f;
+      if constexpr (MIRROR > 1) {
+        if (tgs) {  // separation and restitution target; the sub-iterations form the targets
+          M.sph(s, 9) = sep;
+          M.sph(s, SF_BR) = bounce ? -rest * u0 : -1e30f;
+          return;
+        }
+      }
       float tgt = sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity);
-      if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
+      if (bounce) tgt = fmaxf(tgt, -rest * u0);
       M.sph(s, 9) = tgt;
     }
   };
@@ -1709,7 +1756,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         active |= 1ull << (M.nsph + 3 * ql + j);
         float* const row = M.lm(3 * ql + j);
         row[LIM_SG * ENVS] = up ? -1.f : 1.f;
-        row[LIM_B * ENVS] = sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity);
+        row[LIM_B * ENVS] =
+            tgs ? sep : (sep >= 0.f ? -sep * idt : fminf(-P.baumgarte * sep * idt, P.max_depenetration_velocity));
       }
     }
   }
@@ -1809,6 +1857,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       for (int r = 0; r < 6; ++r) k += M.Kx(l, j, r) * vb0[r];
       M.leg(l, 45 + j) = nu[6 + j] + k;
       M.leg(l, 48 + j) = 0.f;
+      if constexpr (MIRROR > 1) M.leg(l, LF_DZ + j) = 0.f;
     }
   }
   // Delassus rows of the active spheres, each in the lane that owns the sphere (only spheres active in some
@@ -1862,6 +1911,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   }
   __syncthreads();  // contact rows and leg accumulators of every owner lane are read by the whole quad
   LRL_PROF(2)  // Delassus rows + warm start
+  float dxb[6];  // (TGS) the base's accumulated motion over the sub-step's sub-iterations
   // projected Gauss-Seidel, sphere order = model order (base, legs 0..3)
   // (each env walks its own active spheres in model order; the wave runs max-over-envs sphere updates,
   // not the union of the 16 envs' contact sets)
@@ -1872,30 +1922,59 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     vo1 = ql == 1 ? vbc[5] : (ql == 0 ? vo1 : 0.f);
     const uint64_t sact = active >> (M.nsph + LRL_NUM_DOF);  // self-contact slots of the env
     const uint64_t cact = active & ~(sact << (M.nsph + LRL_NUM_DOF));
-    for (int it = 0; it < P.solver_iterations; ++it) {
-      for (uint64_t m = cact; __any((int)(m != 0ull));) {
-        if (m) {
-          const int s = __builtin_ctzll(m);
-          m &= m - 1ull;
-          if (s >= M.nsph)
-            limit_pgs_q(M, s - M.nsph, ql, vo0, vo1);
-          else
-            contact_pgs_q(M, s, sph_leg_of(SL, s), mu, ql, vo0, vo1);
-        }
-      }
-      if (__any((int)(sact != 0ull)))  // self-contact slots after the contacts and limits
-        for (uint64_t m = sact; __any((int)(m != 0ull));) {
+    const float h = dt / (float)(P.solver_iterations > 0 ? P.solver_iterations : 1);
+    Tgs T{0.f, 0.f, frcp(h), P.baumgarte, P.max_depenetration_velocity};
+    auto sweeps = [&](auto tgs_c) {
+      constexpr bool TG = decltype(tgs_c)::value;
+      for (int it = 0; it < P.solver_iterations; ++it) {
+        for (uint64_t m = cact; __any((int)(m != 0ull));) {
           if (m) {
-            const int k = __builtin_ctzll(m);
+            const int s = __builtin_ctzll(m);
             m &= m - 1ull;
-            self_pgs_q(M, free_spheres(M, active), k, mu_s, ql, vo0, vo1);
+            if (s >= M.nsph)
+              limit_pgs_q<TG>(M, s - M.nsph, ql, vo0, vo1, T);
+            else
+              contact_pgs_q<TG>(M, s, sph_leg_of(SL, s), mu, ql, vo0, vo1, T);
           }
         }
+        if (__any((int)(sact != 0ull)))  // self-contact slots after the contacts and limits
+          for (uint64_t m = sact; __any((int)(m != 0ull));) {
+            if (m) {
+              const int k = __builtin_ctzll(m);
+              m &= m - 1ull;
+              self_pgs_q(M, free_spheres(M, active), k, mu_s, ql, vo0, vo1);
+            }
+          }
+        if constexpr (TG) {  // dx += h nu: lane q advances its share of dx_b and component q of every leg's dz
+          T.dxo0 += h * vo0;
+          T.dxo1 += h * vo1;
+          if (ql < 3) {
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+              float* const lg = M.lp(l) + ql * ENVS;
+              lg[LF_DZ * ENVS] += h * (lg[45 * ENVS] + lg[48 * ENVS]);
+            }
+          }
+        }
+      }
+    };
+    if constexpr (MIRROR > 1) {
+      if (tgs)
+        sweeps(BoolC<true>{});
+      else
+        sweeps(BoolC<false>{});
+    } else {
+      sweeps(BoolC<false>{});
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) vbc[r] = quad_bcast(vo0, r);
+    for (int r = 0; r < 4; ++r) {
+      vbc[r] = quad_bcast(vo0, r);
+      dxb[r] = quad_bcast(T.dxo0, r);
+    }
     vbc[4] = quad_bcast(vo1, 0);
     vbc[5] = quad_bcast(vo1, 1);
+    dxb[4] = quad_bcast(T.dxo1, 0);
+    dxb[5] = quad_bcast(T.dxo1, 1);
   }
   __syncthreads();  // the leg accumulators each lane owned are read by the whole quad below
   if (P.joint_limits) {  // this leg's limit impulses, carried to the next sub-step in registers
@@ -1912,26 +1991,51 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     nu[7] = q.y;
     nu[8] = q.z;
   }
-  // semi-implicit integration
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    st.qd[j] = nu[6 + j];
-    st.q[j] += dt * st.qd[j];
-  }
-  const V3 vw = mul(R, v3(nu[3], nu[4], nu[5]));
-  st.pos[0] += dt * vw.x;
-  st.pos[1] += dt * vw.y;
-  st.pos[2] += dt * vw.z;
+  // semi-implicit integration (TGS: positions move by the accumulated motion dx — joints dz - K dx_b — and the
+  // rotation by exp(dx_w); velocities end at the last sweep's either way)
   const V3 w = v3(nu[0], nu[1], nu[2]);
-  const float wn = sqrtf(dot(w, w)), th = wn * dt;
   float dq[4];
-  if (th > 1e-12f) {
-    float sn, cs;
-    sincosf(0.5f * th, &sn, &cs);
-    const float k = sn * frcp(wn);
-    dq[0] = w.x * k; dq[1] = w.y * k; dq[2] = w.z * k; dq[3] = cs;
+  if (tgs) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float k = 0.f;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) k += M.Kx(ql, j, r) * dxb[r];
+      st.qd[j] = nu[6 + j];
+      st.q[j] += M.leg(ql, LF_DZ + j) - k;
+    }
+    const V3 dp = mul(R, v3(dxb[3], dxb[4], dxb[5]));
+    st.pos[0] += dp.x;
+    st.pos[1] += dp.y;
+    st.pos[2] += dp.z;
+    const float th = sqrtf(dxb[0] * dxb[0] + dxb[1] * dxb[1] + dxb[2] * dxb[2]);
+    if (th > 1e-12f) {
+      float sn, cs;
+      sincosf(0.5f * th, &sn, &cs);
+      const float k = sn * frcp(th);
+      dq[0] = dxb[0] * k; dq[1] = dxb[1] * k; dq[2] = dxb[2] * k; dq[3] = cs;
+    } else {
+      dq[0] = 0.5f * dxb[0]; dq[1] = 0.5f * dxb[1]; dq[2] = 0.5f * dxb[2]; dq[3] = 1.f;
+    }
   } else {
-    dq[0] = 0.5f * dt * w.x; dq[1] = 0.5f * dt * w.y; dq[2] = 0.5f * dt * w.z; dq[3] = 1.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      st.qd[j] = nu[6 + j];
+      st.q[j] += dt * st.qd[j];
+    }
+    const V3 vw = mul(R, v3(nu[3], nu[4], nu[5]));
+    st.pos[0] += dt * vw.x;
+    st.pos[1] += dt * vw.y;
+    st.pos[2] += dt * vw.z;
+    const float wn = sqrtf(dot(w, w)), th = wn * dt;
+    if (th > 1e-12f) {
+      float sn, cs;
+      sincosf(0.5f * th, &sn, &cs);
+      const float k = sn * frcp(wn);
+      dq[0] = w.x * k; dq[1] = w.y * k; dq[2] = w.z * k; dq[3] = cs;
+    } else {
+      dq[0] = 0.5f * dt * w.x; dq[1] = 0.5f * dt * w.y; dq[2] = 0.5f * dt * w.z; dq[3] = 1.f;
+    }
   }
   const float x1 = st.quat[0], y1 = st.quat[1], z1 = st.quat[2], w1 = st.quat[3];
   float nq[4] = {w1 * dq[0] + x1 * dq[3] + y1 * dq[2] - z1 * dq[1], w1 * dq[1] - x1 * dq[2] + y1 * dq[3] + z1 * dq[0],

@@ -18,6 +18,13 @@
 // per wave, 16 lanes (4 mirrored quads) per env (lrl_env.hip, lrl_env_flat.hip)
 #define LRL_ENV_WG_ENVS_MESH (LRL_ENV_LANES / 4)
 #define LRL_ENV_WG_ENVS_FLAT (LRL_ENV_LANES / 16)
+// LDS fields per leg block / per contact-sphere row of the env kernel (lrl_env.hip): the plane build carries the TGS
+// solver's extra fields (the leg's accumulated joint-space motion dz, a contact's restitution target), the terrain-mesh
+// build has no room for them (its 16-env workgroup fills the CU's LDS) and solves with PGS
+#define LRL_LEGF_MESH 51
+#define LRL_LEGF_FLAT 54
+#define LRL_NSF_MESH 67
+#define LRL_NSF_FLAT 68
 
 struct KLeg {
   float xyz[3][3];   // joint origin in the parent frame

@@ -73,6 +73,7 @@ class LrlEnvParams(C.Structure):
         ("obs_scale_height", f32), ("num_train_envs", i32), ("teleport_x_offset_eval", f32), ("dr_span", f32 * 3),
         ("joint_limits", i32), ("joint_limit_margin", f32), ("self_collisions", i32),
         ("push_robots", i32), ("push_interval", i32), ("push_lo", f32), ("push_span", f32),
+        ("solver_tgs", i32),
     ]
 
 

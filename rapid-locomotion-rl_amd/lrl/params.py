@@ -99,13 +99,15 @@ def body_sets(cfg, robot):
 
 
 def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte=0.2, terrain_mesh=0,
-                 joint_limits=True, joint_limit_margin=0.02, self_collisions=None):
+                 joint_limits=True, joint_limit_margin=0.02, self_collisions=None, solver_type=None):
     """terrain_mesh: 1 when the sim collides with a generated height field / trimesh (lrl_sim_set_terrain),
     0 for the plane z = 0 (mesh_type 'plane', or a trimesh whose heights are all zero).
     joint_limits: enforce the URDF joint position limits in the contact solve (Isaac Gym / PhysX always enforces
     them for limited revolute joints: the reference has no switch); joint_limit_margin: activation window, rad.
     self_collisions: None follows Cfg.asset.self_collisions (0 = enabled, Isaac Gym's filter semantics: both presets
-    enable it, mini_cheetah_config.py:44, go1_config.py:44); True / False override."""
+    enable it, mini_cheetah_config.py:44, go1_config.py:44); True / False override.
+    solver_type: None follows Cfg.sim.physx.solver_type (1 = TGS, legged_robot_config.py:247; 0 = PGS); the
+    terrain-mesh build always solves with PGS."""
     dt = derived(cfg)
     P = _abi.LrlEnvParams()
     dof_names = robot["dof_names"]
@@ -220,5 +222,6 @@ def build_params(cfg, robot, auto_reset=False, solver_iterations=None, baumgarte
         # torch_rand_float(-max, max, (k, 2)) = (max - -max) * torch.rand + -max (legged_robot.py:763-764)
         push_robots=int(bool(dr0.push_robots)), push_interval=int(cfg.domain_rand.push_interval),
         push_lo=-push_max, push_span=push_max - (-push_max),
+        solver_tgs=int((physx.solver_type if solver_type is None else solver_type) == 1 and not terrain_mesh),
     )
     return P

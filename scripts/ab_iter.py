@@ -21,6 +21,8 @@ iters = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 tag = sys.argv[2] if len(sys.argv) > 2 else os.environ.get("LRL_LIB", "default")
 cfg = lcfg.make_cfg()
 lcfg.config_mini_cheetah(cfg)
+if "LRL_SOLVER_TYPE" in os.environ:  # 1 = TGS (the presets), 0 = PGS
+    cfg.sim.physx.solver_type = int(os.environ["LRL_SOLVER_TYPE"])
 cfg.env.num_envs = 4096
 R.RunnerArgs.save_interval = 0
 R.RunnerArgs.log_freq = 10 ** 9

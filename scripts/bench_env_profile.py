@@ -19,6 +19,8 @@ iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 n = 4096
 cfg = lcfg.make_cfg()
 lcfg.config_mini_cheetah(cfg)
+if "LRL_SOLVER_TYPE" in os.environ:  # 1 = TGS (the presets), 0 = PGS
+    cfg.sim.physx.solver_type = int(os.environ["LRL_SOLVER_TYPE"])
 if len(sys.argv) > 2:
     cfg.asset.self_collisions = int(sys.argv[2])
 cfg.env.num_envs = n

@@ -35,7 +35,7 @@ def setup():
     cfg.terrain.x_offset = 0
     cfg.noise.add_noise = False
     rob = load_robot("mini_cheetah.urdf")
-    P, M = lparams.build_params(cfg, rob), lparams.build_model(rob)
+    P, M = lparams.build_params(cfg, rob, solver_type=0), lparams.build_model(rob)  # the study's switch picks the solver
     P.teleport = 0
     return cfg, P, M
 
