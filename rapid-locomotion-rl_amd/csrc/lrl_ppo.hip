@@ -107,14 +107,16 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
   // hides under (1) mu, v; (2) per (row, action): log-prob and KL terms  (3) per row: ratio, clipped surrogate,
   // clipped value loss, their gradients  (4) per (row, action): d loss / d mu, d loss / d std  (5) per column: dH3
   // and the head weight-gradient partials.  Two global round trips in all (rows, then the gathered rows).
-  constexpr int HP = 2 * HEAD_W + 1;  // odd pitch: row-per-lane reads conflict-free
+  // pitch 4 (mod 32) floats: the row-per-lane float4 reads of (1) hit distinct banks in every 8-lane group
+  constexpr int HP = 2 * HEAD_W + 4;
   constexpr int NA = HEAD_NA;
+  static_assert(NA % 4 == 0 && HEAD_W % 16 == 0, "float4 rows");
   constexpr int NG = (HEAD_ROWS * NA + HEAD_THREADS - 1) / HEAD_THREADS;  // gathered (row, action) items per thread
-  __shared__ float H[HEAD_ROWS][HP];
-  __shared__ float W4[NA + 1][HEAD_W];
+  __shared__ __attribute__((aligned(16))) float H[HEAD_ROWS][HP];
+  __shared__ __attribute__((aligned(16))) float W4[NA + 1][HEAD_W];
   __shared__ float MU[HEAD_ROWS][NA + 1];   // mu_j, then d = a_j - mu_j
   __shared__ float VP[HEAD_ROWS][8];
-  __shared__ float LP[HEAD_ROWS][NA];       // log-prob term, then d loss / d mu
+  __shared__ __attribute__((aligned(16))) float LP[HEAD_ROWS][NA];  // log-prob term, then d loss / d mu
   __shared__ float KT[HEAD_ROWS][NA];       // KL term, then d loss / d std
   __shared__ float DR[HEAD_ROWS][2];        // d loss / d logp, d loss / d v
   __shared__ float SC[HEAD_ROWS][3];        // kl, surrogate, value loss per row
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int i = t + u * HEAD_THREADS, r = i / (HEAD_W / 2), c = 4 * (i % (HEAD_W / 2));
-      H[r][c] = v[u].x; H[r][c + 1] = v[u].y; H[r][c + 2] = v[u].z; H[r][c + 3] = v[u].w;
+      *reinterpret_cast<float4*>(&H[r][c]) = v[u];
     }
   }
   for (int i = t; i < (NA + 1) * HEAD_W; i += HEAD_THREADS) {
@@ -169,16 +171,29 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
     const float* src = q == 0 ? a.adv : q == 1 ? a.old_logp : q == 2 ? a.tv : a.ret;
     gr = src[RW[r]];
   }
-  // (1) thread (r, q): actions q, q+8 and an eighth of the value dot
+  // (1) thread (r, q): actions q, q+8 and an eighth of the value dot (float4 LDS reads, the same sequential fmaf
+  // order over k as one element at a time)
   {
     const int r = t & (HEAD_ROWS - 1), q = t / HEAD_ROWS;
+    const float4* hr = reinterpret_cast<const float4*>(&H[r][0]);
+    auto dot4 = [](float s, float4 h, float4 w) {
+      s = fmaf(h.x, w.x, s);
+      s = fmaf(h.y, w.y, s);
+      s = fmaf(h.z, w.z, s);
+      return fmaf(h.w, w.w, s);
+    };
     for (int j = q; j < NA; j += 8) {
+      const float4* wr = reinterpret_cast<const float4*>(&W4[j][0]);
       float s = 0.f;
-      for (int k = 0; k < HEAD_W; ++k) s = fmaf(H[r][k], W4[j][k], s);
+#pragma unroll 8
+      for (int k4 = 0; k4 < HEAD_W / 4; ++k4) s = dot4(s, hr[k4], wr[k4]);
       MU[r][j] = s + a.b4a[j];
     }
+    const float4* wv = reinterpret_cast<const float4*>(&W4[NA][q * (HEAD_W / 8)]);
+    const float4* hv = hr + (HEAD_W + q * (HEAD_W / 8)) / 4;
     float s = 0.f;
-    for (int k = q * (HEAD_W / 8); k < (q + 1) * (HEAD_W / 8); ++k) s = fmaf(H[r][HEAD_W + k], W4[NA][k], s);
+#pragma unroll
+    for (int k4 = 0; k4 < HEAD_W / 32; ++k4) s = dot4(s, hv[k4], wv[k4]);
     VP[r][q] = s;
   }
 #pragma unroll
@@ -286,10 +301,16 @@ __global__ __launch_bounds__(HEAD_THREADS) void ppo_head_kernel(HeadArgs a) {
 #pragma unroll 2
       for (int r = 0; r < nrows; ++r) {
         const float h = H[r][k];
+        float dmr[NA];  // (row r's d loss / d mu: NA / 4 broadcast float4 reads)
+#pragma unroll
+        for (int j4 = 0; j4 < NA / 4; ++j4) {
+          const float4 v = reinterpret_cast<const float4*>(&LP[r][0])[j4];
+          dmr[4 * j4] = v.x; dmr[4 * j4 + 1] = v.y; dmr[4 * j4 + 2] = v.z; dmr[4 * j4 + 3] = v.w;
+        }
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
-          const float dm = LP[r][j];
+          const float dm = dmr[j];
           s = fmaf(dm, wk[j], s);
           accw[j] = fmaf(dm, h, accw[j]);
         }
@@ -407,7 +428,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void act_head_kernel(ActHeadArgs a) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int i = t + u * HEAD_THREADS, r = i / (HEAD_W / 2), c = 4 * (i % (HEAD_W / 2));
-      H[r][c] = v[u].x; H[r][c + 1] = v[u].y; H[r][c + 2] = v[u].z; H[r][c + 3] = v[u].w;
+      *reinterpret_cast<float4*>(&H[r][c]) = v[u];
     }
   }
   for (int i = t; i < (na + 1) * HEAD_W; i += HEAD_THREADS) {
