@@ -682,6 +682,108 @@ __global__ __launch_bounds__(GTHREADS, 2) void gemm_thin_kernel(GemmP p) {
   }
 }
 
+// The same product on 16-row tiles (v_mfma_f32_16x16x4_f32, two 16-column blocks): 1,536 tiles of the 24,576-row
+// minibatch deal evenly over the 512-workgroup persistent grid (3 each), where 768 32-row tiles leave half the
+// workgroups one tile short.  Lane (h, i) of a wave loads row i's float4 at k = 16 s + 4 h and feeds its four values
+// to four consecutive MFMA steps; its B registers hold column i (+16) at the same k.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <int LAYOUT, int EPI, int NBK>
+__global__ __launch_bounds__(GTHREADS, 2) void gemm_thin16_kernel(GemmP p) {
+  __shared__ float red[3 * 8 * 64];
+  constexpr bool BNC = (LAYOUT & 2) != 0;
+  constexpr int KS = 2 * NBK;  // 16-k blocks of a wave's quarter (32 NBK k)
+  const int N = p.N, M = p.M;
+  const int g = blockIdx.y;
+  const float* __restrict__ A = p.A + g * p.ga;
+  const float* __restrict__ B = p.B + g * p.gb;
+  float* __restrict__ C = p.C + g * p.gc;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, h = lane >> 4;
+  const int kbeg = w * 32 * NBK;
+  float breg[KS][2][4];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = kbeg + 16 * s + 4 * h + u, col = i + 16 * cb;
+        breg[s][cb][u] = col < N ? (BNC ? B[(int64_t)k * p.ldb + col] : B[(int64_t)col * p.ldb + k]) : 0.f;
+      }
+  const int mt = (M + 15) >> 4;
+  auto rowp = [&](int t) -> const float* {
+    const int row = t * 16 + i;
+    if (t >= mt || row >= M) return nullptr;
+    return A + (p.a_rows ? p.a_rows[row] : (int64_t)row) * p.lda + kbeg + 4 * h;
+  };
+  auto load = [&](const float* ar, int s0, float4* dst) {  // 4 blocks of 16 k
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      dst[v] = ar ? *reinterpret_cast<const float4*>(ar + 16 * (s0 + v)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const float* ar = rowp(blockIdx.x);
+  float4 cur[4];
+  load(ar, 0, cur);
+  for (int t = blockIdx.x; t < mt; t += gridDim.x) {
+    const float* arn = rowp(t + gridDim.x);
+    f32x4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s0 = 0; s0 < KS; s0 += 4) {
+      float4 nxt[4];
+      if (s0 + 4 < KS) load(ar, s0 + 4, nxt);
+      else load(arn, 0, nxt);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float av[4] = {cur[v].x, cur[v].y, cur[v].z, cur[v].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], breg[s0 + v][0][u], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], breg[s0 + v][1][u], acc1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) cur[v] = nxt[v];
+    }
+    ar = arn;
+    if (w > 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[((w - 1) * 8 + r) * 64 + lane] = acc0[r];
+        red[((w - 1) * 8 + 4 + r) * 64 + lane] = acc1[r];
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col = i + 16 * cb;
+        float bj = 0.f;
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) bj = col < N ? p.bias[g * p.gbias + col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = cb ? acc1[r] : acc0[r];
+          v += red[(4 * cb + r) * 64 + lane];
+          v += red[(8 + 4 * cb + r) * 64 + lane];
+          v += red[(16 + 4 * cb + r) * 64 + lane];
+          if constexpr (EPI == EPI_BIAS) v += bj;
+          if constexpr (EPI == EPI_BIAS_ELU) v = elu_f(v + bj);
+          const int orow = t * 16 + 4 * h + r;
+          if (col < N && orow < M) C[(int64_t)orow * p.ldc + col] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// (LRL_THIN16=0: development switch back to the 32-row tiles)
+static bool thin16_enabled() {
+  static const int on = [] {
+    const char* e = getenv("LRL_THIN16");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 template <int LAYOUT, int EPI, int NBK>
 static int launch_thin_k(const GemmP& p, int groups, hipStream_t st) {
   static int ncu = 0;
@@ -690,6 +792,12 @@ static int launch_thin_k(const GemmP& p, int groups, hipStream_t st) {
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return LRL_E_HIP;
     ncu = prop.multiProcessorCount;
+  }
+  if (thin16_enabled()) {
+    const int mt = (p.M + 15) / 16;
+    const int gx = std::max(1, std::min(mt, 2 * ncu / std::max(1, groups)));
+    hipLaunchKernelGGL((gemm_thin16_kernel<LAYOUT, EPI, NBK>), dim3(gx, groups), dim3(GTHREADS), 0, st, p);
+    return 0;
   }
   const int mt = (p.M + 31) / 32;
   const int gx = std::max(1, std::min(mt, 2 * ncu / std::max(1, groups)));

@@ -365,6 +365,7 @@ struct ActHeadArgs {
   float *actions, *mu, *values, *logp;
   lrl_rollout_store store;
   int store_row, do_store;
+  float* xa_out;  // ENC_ONLY: the [obs | latent | 0] rows, pitch xs
 };
 
 // rows [0, nrows) of src (pitch sld) -> dst (pitch dld), `cols` floats each, by the block's HEAD_THREADS
@@ -523,6 +524,8 @@ constexpr int FA_BIGP = 1028; // h1 pitch (2 x ac_h0 <= 1024)
 constexpr int FA_MIDP = 516;  // h2 pitch (2 x ac_h1 <= 512); priv / he2 use narrower pitches in the same region
 constexpr int FA_HW_FLOATS = (HEAD_NA + 1) * HEAD_W;  // the heads' weights, staged at the start
 constexpr int FA_LDS_FLOATS = FA_R * (FA_XP + FA_BIGP + FA_MIDP) + FA_HW_FLOATS;
+constexpr int FA_ENC_MIDP = 260;  // ENC_ONLY: priv [16][36] / he2 [16][enc_h1 + 4 <= 260]
+constexpr int FA_ENC_LDS_FLOATS = FA_R * (FA_XP + FA_XP + FA_ENC_MIDP);  // ENC_ONLY: X, he1, priv / he2 (49.9 KB)
 
 // Phase timers of the fused act (build with -DLRL_ACT_PROFILE, read with lrl_debug_act_profile): shader-clock cycles
 // per phase summed over workgroups (thread 0's view): stage, enc1..3, ac1..3, heads, sampling, storage copies
@@ -679,16 +682,19 @@ struct FusedActArgs {
   float *actions, *mu, *values, *logp;
   lrl_rollout_store store;
   int store_row, do_store;
+  float* xa_out;  // ENC_ONLY: the [obs | latent | 0] rows, pitch xs
 };
 
 // PRESET: the presets' network (18 -> 256 -> 128 -> 18 encoder, 2 x (64 -> 512 -> 256 -> 128) bodies, aligned weights):
-// every layer's run length and load width fixed at compile time; otherwise dispatched per layer
-template <bool PRESET>
+// every layer's run length and load width fixed at compile time; otherwise dispatched per layer.
+// ENC_ONLY: the rollout act's first four launches in one (ppo_prep_kernel's obs rows and the env-factor encoder's
+// three products): the X rows [obs | latent | 0] go to a.xa_out for the actor / critic chain, in FA_ENC_LDS_FLOATS
+template <bool PRESET, bool ENC_ONLY = false>
 __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
   extern __shared__ __attribute__((aligned(16))) float fa_lds[];
   float* X = fa_lds;                     // [16][FA_XP]: obs | latent | 0
   float* BIG = X + FA_R * FA_XP;         // he1 [16][FA_XP], h1 [16][FA_BIGP], h3 [16][FA_XP]
-  float* MID = BIG + FA_R * FA_BIGP;     // priv [16][36], he2 [16][enc_h1 + 4], h2 [16][FA_MIDP]
+  float* MID = BIG + FA_R * (ENC_ONLY ? FA_XP : FA_BIGP);  // priv [16][36], he2 [16][enc_h1 + 4], h2 [16][FA_MIDP]
   float* HW = MID + FA_R * FA_MIDP;      // [NA + 1][HEAD_W]: w4a rows, then w4c
   FA_PROF_DECL
   const lrl_ppo_net& nt = a.net;
@@ -703,8 +709,9 @@ __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
     const int r = e >> 5, c = e & 31;
     MID[r * PP + c] = (r < nrows && c < np) ? a.priv[(int64_t)(r0 + r) * np + c] : 0.f;
   }
-  for (int e = t; e < FA_HW_FLOATS; e += FA_THREADS)
-    HW[e] = e < HEAD_NA * HEAD_W ? a.w[nt.w4a + e] : a.w[nt.w4c + (e - HEAD_NA * HEAD_W)];
+  if constexpr (!ENC_ONLY)
+    for (int e = t; e < FA_HW_FLOATS; e += FA_THREADS)
+      HW[e] = e < HEAD_NA * HEAD_W ? a.w[nt.w4a + e] : a.w[nt.w4c + (e - HEAD_NA * HEAD_W)];
   __syncthreads();
   FA_PROF(0)
   const float* w = a.w;
@@ -726,6 +733,14 @@ __global__ __launch_bounds__(FA_THREADS) void act_fused_kernel(FusedActArgs a) {
   else fa_layer<0, false>(L);
   __syncthreads();
   FA_PROF(3)
+  if constexpr (ENC_ONLY) {  // (xs % 32 == 0: whole float4s of the row)
+    const int q4 = a.xs >> 2;
+    for (int e = t; e < nrows * q4; e += FA_THREADS) {
+      const int r = e / q4, c = 4 * (e - r * q4);
+      *reinterpret_cast<float4*>(a.xa_out + (int64_t)(r0 + r) * a.xs + c) = *reinterpret_cast<const float4*>(X + r * FA_XP + c);
+    }
+    return;
+  }
   // actor / critic bodies, both at once: [obs | latent] -> 2 x ac_h0 -> 2 x ac_h1 -> 2 x ac_h2 (ELU)
   const int nx = no + nt.latent;
   L = FaLayer{X, FA_XP, 0, a.xs, w + nt.w1, nx, nx, 2 * nt.ac_h0, 0, w + nt.b1, BIG, FA_BIGP, 0, 2 * nt.ac_h0, 1, 1,
@@ -1365,6 +1380,22 @@ static ActPlan make_act_plan(const lrl_ppo_net& n, int rows, char* base) {
 
 // The fused act's envelope (LDS pitches, tile runs that never cross a group); LRL_ACT_FUSED=1 selects it over the GEMM chain
 // (A/B timing and the tests that compare the two)
+// the encoder part of act_fused_kernel in the rollout act's chain (LRL_ACT_ENC_FUSED=0: the prep kernel + three
+// GEMM launches instead; read per call so a test can switch it inside one process)
+static bool act_enc_fused(const lrl_ppo_net& n) {
+  const char* e = getenv("LRL_ACT_ENC_FUSED");
+  if (e && e[0] == '0') return false;
+  auto run_ok = [](int Ng) {
+    if (Ng % 16) return false;
+    const int T = Ng / 16, tpw = T >= 4 ? T / 4 : 1;
+    if (T >= 4 && T % 4) return false;
+    return T % std::min(tpw, 8) == 0;
+  };
+  return xs_of(n) % 32 == 0 && xs_of(n) <= 256 && n.num_priv <= 32 && n.enc_h0 <= 256 && n.enc_h0 % 32 == 0 &&
+         n.enc_h1 % 32 == 0 && n.enc_h1 + 4 <= FA_ENC_MIDP && n.latent <= 32 && run_ok(n.enc_h0) && run_ok(n.enc_h1) &&
+         run_ok((n.latent + 15) / 16 * 16);
+}
+
 static bool fused_act_fits(const lrl_ppo_net& n) {
   const char* e = getenv("LRL_ACT_FUSED");  // (read per call: a test switches it inside one process)
   if (!(e && e[0] == '1')) return false;  // off by default until it measures faster than the chain
@@ -1456,12 +1487,28 @@ extern "C" int32_t lrl_ppo_act(const lrl_ppo_net* net, const float* params, cons
   } else {
     for (auto& q : pj) q.dst = nullptr;
   }
-  hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(n, XS)), dim3(256), 0, st, obs,
-                     (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
-  g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv, true);
-  g.with(pj[PL_E2]).nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1,
-                       nt.enc_h0, true);
-  g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1, false);
+  if (act_enc_fused(nt)) {  // X = [obs | encoder(priv) | 0] in one launch (act_fused_kernel<., true>)
+    FusedActArgs fa{};
+    fa.w = params; fa.net = nt; fa.obs = obs; fa.priv = priv; fa.n = n; fa.xs = XS; fa.xa_out = P.xa;
+    auto al = [&](int64_t off, int ld) { return ((reinterpret_cast<uintptr_t>(params + off) & 15) == 0 && ld % 4 == 0); };
+    fa.vec = (al(nt.e2w, nt.enc_h0) ? 2u : 0u) | (al(nt.e3w, nt.enc_h1) ? 4u : 0u);
+    const bool preset = nt.enc_h0 == 256 && nt.enc_h1 == 128 && nt.latent <= 32 && fa.vec == 6u;
+    if (preset)
+      hipLaunchKernelGGL((act_fused_kernel<true, true>), dim3((n + FA_R - 1) / FA_R), dim3(FA_THREADS),
+                         FA_ENC_LDS_FLOATS * sizeof(float), st, fa);
+    else
+      hipLaunchKernelGGL((act_fused_kernel<false, true>), dim3((n + FA_R - 1) / FA_R), dim3(FA_THREADS),
+                         FA_ENC_LDS_FLOATS * sizeof(float), st, fa);
+  } else {
+    hipLaunchKernelGGL(ppo_prep_kernel, dim3(prep_blocks(n, XS)), dim3(256), 0, st, obs,
+                       (const int64_t*)nullptr, n, nt.num_obs, XS, P.xa);
+    g.nt(priv, nt.num_priv, nullptr, w + nt.e1w, nt.num_priv, P.he1, nt.enc_h0, w + nt.e1b, n, nt.enc_h0, nt.num_priv,
+         true);
+    g.with(pj[PL_E2]).nt(P.he1, nt.enc_h0, nullptr, w + nt.e2w, nt.enc_h0, P.he2, nt.enc_h1, w + nt.e2b, n, nt.enc_h1,
+                         nt.enc_h0, true);
+    g.nt(P.he2, nt.enc_h1, nullptr, w + nt.e3w, nt.enc_h1, P.xa + nt.num_obs, XS, w + nt.e3b, n, nt.latent, nt.enc_h1,
+         false);
+  }
   g.with(pj[PL_W1]).nt(P.xa, XS, nullptr, w + nt.w1, nx, P.h1, 2 * nt.ac_h0, w + nt.b1, n, 2 * nt.ac_h0, XS, true);
   g.with(pj[PL_W2]).nt(P.h1, 2 * nt.ac_h0, nullptr, w + nt.w2, nt.ac_h0, P.h2, 2 * nt.ac_h1, w + nt.b2, n, nt.ac_h1,
                        nt.ac_h0, true, 2, nt.ac_h0, (int64_t)nt.ac_h1 * nt.ac_h0, nt.ac_h1, nt.ac_h1);

@@ -106,6 +106,36 @@ def test_one_launch_act_matches_gemm_chain(n, no, monkeypatch):
     assert torch.equal(sl.flatten(), lp.flatten())
 
 
+@pytest.mark.parametrize("n,no", [(4096, 42), (37, 42), (300, 235)])
+def test_act_fused_encoder_matches_encoder_chain(n, no, monkeypatch):
+    """The GEMM-chain act's first launch (act_fused_kernel<., true>: the obs rows and the env-factor encoder's three
+    layers in one workgroup per 16 rows, fp32 MFMA) against the prep kernel + three x6 / fp32 products it replaces
+    (LRL_ACT_ENC_FUSED=0): actions, means, values, log-probs to fp32 rounding, the same noise, the storage row exactly."""
+    from lrl.ppo.actor_critic import ActorCritic
+    from lrl.ppo.rollout_storage import RolloutStorage
+    monkeypatch.setenv("LRL_ACT_FUSED", "0")
+    ac = ActorCritic(no, 18, 15 * no, 12).cuda()
+    init_params(ac)
+    g = torch.Generator(device="cuda:0").manual_seed(13)
+    obs = torch.randn(n, no, device="cuda:0", generator=g)
+    priv = torch.randn(n, 18, device="cuda:0", generator=g)
+    hist = torch.randn(n, 15 * no, device="cuda:0", generator=g)
+    outs = []
+    for enc in ("1", "0"):
+        monkeypatch.setenv("LRL_ACT_ENC_FUSED", enc)
+        st = RolloutStorage(n, 2, [no], [18], [15 * no], [12], "cuda:0")
+        res = ac.act_fused(obs, priv, hist, seed=5, counter=4, store=st.store_desc(), store_row=0)
+        torch.cuda.synchronize()
+        outs.append([r.clone() for r in res] + [st.observations[0].clone(), st.privileged_observations[0].clone()])
+    (a, mu, v, lp, so, sp), (a0, mu0, v0, lp0, so0, sp0) = outs
+    torch.testing.assert_close(mu, mu0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(a, a0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(v, v0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(lp, lp0, rtol=2e-5, atol=2e-4)
+    assert torch.allclose(a - mu, a0 - mu0, rtol=0, atol=1e-6)  # the same noise
+    assert torch.equal(so, so0) and torch.equal(sp, sp0)
+
+
 @pytest.mark.parametrize("n", [4096, 1000])
 def test_act_with_weight_planes_is_bit_identical(n, monkeypatch):
     """The act's GEMM chain with its weight products on the pre-split-planes kernel (LRL_ACT_PLANES=1, gemm_x6p_kernel
