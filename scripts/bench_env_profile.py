@@ -42,12 +42,14 @@ runner.learn(iters)
 torch.cuda.synchronize()
 assert L.lrl_debug_env_profile(buf, 0) >= 16, "library built without LRL_ENV_PROFILE"
 K = 24 * iters
-waves = (n + 15) // 16
+waves = (n + 3) // 4  # the plane kernel: 4 envs per wave (16 lanes per env); profiles r6t and earlier divided by n / 16
 names = ["kin+dyn+detect", "schur+free acc", "delassus+warm", "PGS", "integrate", "start+state load", "post-physics",
          "tiles+history", "PD torques"]
 tot = sum(buf[:9])
 for i, nm in enumerate(names):
     print(f"{nm:16s} {buf[i] / waves / K:10.0f} cycles/wave/step  {100 * buf[i] / tot:5.1f}%")
+for i, nm in zip(range(10, 14), ["  contact forces", "  loads/teleport/DR", "  rewards+sums", "  obs/priv rows"]):
+    print(f"{nm:16s} {buf[i] / waves / K:10.0f} cycles/wave/step  (part of post-physics)")
 if buf[14]:
     print(f"  self detect     {buf[14] / waves / K:10.0f} cycles/wave/step; LDS pass entered "
           f"{buf[15] / waves / K:.3f} times per wave and step")

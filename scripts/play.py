@@ -35,6 +35,8 @@ def load_env(robot, num_envs, device):
               "randomize_base_mass", "randomize_Kd_factor", "randomize_Kp_factor", "randomize_com_displacement"):
         setattr(dr, k, False)
     cfg.env.num_envs = num_envs
+    if "LRL_SOLVER_TYPE" in os.environ:  # 1 = TGS (the presets' solver), 0 = PGS
+        cfg.sim.physx.solver_type = int(os.environ["LRL_SOLVER_TYPE"])
     cfg.terrain.num_rows, cfg.terrain.num_cols, cfg.terrain.border_size = 3, 5, 0
     cfg.terrain.max_init_terrain_level = min(cfg.terrain.max_init_terrain_level, cfg.terrain.num_rows - 1)
     return HistoryWrapper(LeggedRobotEnv(device, cfg=cfg)), cfg

@@ -101,3 +101,32 @@ def test_oracle_tgs_variant_matches_pgs_on_standing():
     assert np.abs(h0 - h1).max() > 0  # the variant is a different solver
     np.testing.assert_array_equal(h0, h2)
     np.testing.assert_array_equal(q0, q2)
+
+
+def test_solver_switch_follows_the_config():
+    """Cfg.sim.physx.solver_type drives lrl_env_params.solver_tgs (legged_robot_config.py:247: 1 = TGS, the presets'
+    solver; the terrain mesh solves with PGS), and the oracle's TGS under that flag is the study's switch exactly."""
+    import importlib.util
+    from lrl import params as lparams
+    from lrl.robot import load_robot
+    from helpers import ROBOT_FILES
+    cfg, rob, M, P = make("mc")
+    assert cfg.sim.physx.solver_type == 1 and P.solver_tgs == 1
+    assert lparams.build_params(cfg, load_robot(ROBOT_FILES["mc"]), solver_type=0).solver_tgs == 0
+    assert lparams.build_params(cfg, load_robot(ROBOT_FILES["mc"]), terrain_mesh=1).solver_tgs == 0
+    spec = importlib.util.spec_from_file_location("tgs_vs_pgs", os.path.join(ROOT, "scripts", "tgs_vs_pgs.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    _, P0, M0 = mod.setup()  # solver_type 0: the study's switch picks the solver
+    assert P0.solver_tgs == 0
+    res = []
+    for flag, switch in ((1, 0), (0, 1), (0, 0)):
+        P0.solver_tgs = flag
+        oracle.set_solver_tgs(switch)
+        st = mod.state(P0, M0, dz=0.15)
+        h, _, _, _ = mod.run(P0, M0, st, 10)
+        res.append((h, st["dof_pos"].copy(), st["dof_vel"].copy()))
+    oracle.set_solver_tgs(0)
+    for a, b in zip(res[0], res[1]):  # the flag and the switch: the same solver
+        np.testing.assert_array_equal(a, b)
+    assert not np.array_equal(res[0][2], res[2][2])  # and not PGS
