@@ -53,7 +53,10 @@ class _LazyExtras(dict):
 
     def set_conditional(self, key, value, present):
         """``key`` holds ``value`` if ``present()`` is true when the dict is first asked about it (membership, a read,
-        keys()); otherwise the key is absent for this step."""
+        keys()); otherwise the key is absent for this step.  Deciding calls ``present()`` — on the device reset path
+        a one-element device->host read, i.e. a stream sync — so ``len(extras)``, ``keys()`` or iteration resolves every
+        pending key and pays that sync once per step, where reading only the keys a caller needs does not; the
+        reference's Runner tests and reads ``infos["train/episode"]`` by key (mini_gym_learn/ppo/__init__.py:145-147)."""
         self._lazy.pop(key, None)
         dict.pop(self, key, None)
         self._cond[key] = (value, present)
