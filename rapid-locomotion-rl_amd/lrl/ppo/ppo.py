@@ -55,6 +55,15 @@ def _world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def _collective():
+    """Whether the update's collectives run: a world of more than one rank, or an initialised one-rank world with
+    LRL_FORCE_COLLECTIVES=1 (a test switch: one GPU then exercises the RCCL calls themselves, each reducing over one
+    rank; tests/test_rccl_world1_gpu.py)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or os.environ.get("LRL_FORCE_COLLECTIVES") == "1"
+
+
 def _all_reduce_(t):
     """Sum ``t`` over the ranks, in place.  RCCL reduces device memory directly; gloo (the CPU / one-GPU rehearsals)
     reduces host memory, so a device tensor is staged through a synchronous host copy rather than gloo's own
@@ -90,7 +99,7 @@ class PPO:
         self.row_offset = 0
         self._act_counter = 0
         self._store = None
-        self.grad_allreduce = _world() > 1
+        self.grad_allreduce = _collective()
         self._native = None  # flat grads / Adam moments / ctrl / workspace of the native update
         self.record_lr = False  # native path: keep the per-minibatch learning rates (self.lr_trace)
         self.overlap_adaptation = True  # native path: adaptation phases on a second stream (see _update_native)
@@ -178,7 +187,7 @@ class PPO:
         else:
             last_values = self.actor_critic.evaluate(last_critic_obs, last_critic_privileged_obs).detach()
         reduce = None
-        if _world() > 1:
+        if _collective():
             reduce = _all_reduce_
         self.storage.compute_returns(last_values, PPO_Args.gamma, PPO_Args.lam, reduce_stats=reduce)
 
@@ -249,6 +258,7 @@ class PPO:
         st = self._native_state(mb)
         net, hp = st["net"], st["hp"]
         world = _world()
+        coll = _collective()
         L = _abi.lib()
         ptr = lambda t: C.c_void_p(t.data_ptr())
         stream = _abi.stream_of(st["grads"].device)
@@ -309,7 +319,7 @@ class PPO:
                 batch.rows = rows.data_ptr()
                 _abi.check(L.lrl_ppo_forward_backward(C.byref(net), ptr(params), ptr(grads), C.byref(batch),
                                                       C.byref(hp), ptr(ws), ptr(ctrl), stream))
-                if world > 1:
+                if coll:
                     _all_reduce_(main)
                 st["steps"][0] += 1
                 _abi.check(L.lrl_ppo_optimizer_step(C.byref(net), ptr(params), ptr(grads), ptr(m), ptr(v),
@@ -329,7 +339,7 @@ class PPO:
                 for _ in range(PPO_Args.num_adaptation_module_substeps):
                     _abi.check(L.lrl_ppo_adaptation_forward_backward(C.byref(net), ptr(params), enc, ptr(grads),
                                                                      C.byref(batch_b), ptr(ws_b), ptr(ctrl), stream_b))
-                    if world > 1:
+                    if coll:
                         with torch.cuda.stream(sb):
                             _all_reduce_(adapt)
                     st["steps"][1] += 1
@@ -387,7 +397,7 @@ class PPO:
                         torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) / (2.0 * torch.square(sigma_b))
                         - 0.5, axis=-1)
                     kl_mean = torch.mean(kl)
-                    if _world() > 1:
+                    if _collective():
                         kl_mean = _all_reduce_(kl_mean.clone())
                         kl_mean /= _world()
                     kl_mean = kl_mean.item()
