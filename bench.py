@@ -201,6 +201,16 @@ def init_world(args):
     # one rank per GPU over RCCL ("nccl"); LRL_DIST_BACKEND=gloo rehearses the multi-rank path on CPU or with
     # several ranks sharing one GPU (ranks then use devices round-robin)
     backend = os.environ.get("LRL_DIST_BACKEND", "nccl")
+    # LRL_FORCE_COLLECTIVES=1 at one GPU: a one-rank RCCL group, and the update issues its collectives anyway (each
+    # reducing over the one rank) — the N = 1 line with the collectives' call cost in it
+    force1 = world == 1 and os.environ.get("LRL_FORCE_COLLECTIVES") == "1" and not args.world_check
+    if force1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend, rank=0, world_size=1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -273,6 +283,12 @@ def main():
         os.environ["LRL_DIST_BACKEND"] = "gloo"  # CPU tensors, no device context
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    # RCCL prints a version banner on stdout when its communicator comes up (and libraries may print too): the bench's
+    # stdout carries its one JSON line only — fd 1 goes to stderr for the rest of the run, the JSON line to the saved
+    # stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world, rank, local, backend = init_world(args)
     if args.world_check:
         seen = torch.tensor([rank], dtype=torch.int64)
@@ -284,7 +300,7 @@ def main():
             seen_ranks = [0]
         if rank == 0:
             print(json.dumps({"world_size": world, "ranks": seen_ranks, "backend": backend if world > 1 else None,
-                              "parallelism": f"dp{world}"}), flush=True)
+                              "parallelism": f"dp{world}"}), file=json_out, flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -385,7 +401,7 @@ def main():
                        "envs_per_gpu": ENVS_PER_GPU, "global_envs": world * ENVS_PER_GPU,
                        "global_batch_env_steps_per_iter": world * ENVS_PER_GPU * 24,
                        "parallelism": f"dp{world}", "world_size": world,
-                       "backend": (backend if world > 1 else None), "devices": devices,
+                       "backend": (backend if dist.is_initialized() else None), "devices": devices,
                        "policy": "ActorCritic 42/18/630->12, random init; teacher PPO + student adaptation update"},
             "ppo_iters_per_s": round(args.steps / elapsed, 3),
             "env_only_env_steps_per_s_per_gpu": round(env_only, 1),
@@ -424,8 +440,8 @@ def main():
             out["secondary"] = bench_go1_rough(dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
