@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define LRL_ABI_VERSION 5
+#define LRL_ABI_VERSION 6
 
 #define LRL_OK 0
 #define LRL_E_INVALID (-1)  /* bad argument / unsupported configuration */
@@ -62,6 +62,7 @@ extern "C" {
 #define LRL_NUM_PRIV 18
 #define LRL_SELF_SLOTS 8        /* self-contact rows per env and sub-step (solver slots) */
 #define LRL_MAX_SELF_PAIRS 256  /* candidate self-collision sphere pairs of a model */
+#define LRL_HULL_K 4            /* candidate vertices per support-table cell (lrl_model::hull_k) */
 
 /* ------------------------------------------------------------------------------------------
  * Robot model: a floating base with 4 legs x 3 revolute joints (hip, thigh, calf) and an optional
@@ -87,6 +88,18 @@ typedef struct lrl_model {
   float sphere_radius[LRL_MAX_SPHERES];
   /* joint data in asset DOF order (FL hip, thigh, calf, FR ..., RL ..., RR ...) */
   float dof_lower[LRL_NUM_DOF], dof_upper[LRL_NUM_DOF], dof_effort[LRL_NUM_DOF], dof_velocity[LRL_NUM_DOF];
+  /* ABI 6 — mesh colliders as support tables (PhysX collides a <mesh> as its convex hull).  With
+   * num_hulls > 0, a leg sphere s with sphere_hull[s] = h >= 0 meets the ground plane at the support point of hull
+   * table h in the direction of the plane's inward normal, in place of its sphere (whose centre / radius remain the
+   * self-collision stand-in); num_hulls = 0 ignores sphere_hull.  hull_table (host memory, read during
+   * lrl_sim_create only) is [num_hulls][6][hull_res][hull_res][hull_k][4]: per cube-map cell of the link-frame
+   * direction d (face 2m + (d_m < 0) of the major axis m, first of x, y, z on ties; cell floor((d_(m+1) / |d_m| + 1)
+   * hull_res / 2), floor((d_(m+2) / |d_m| + 1) hull_res / 2), clamped), hull_k candidate vertices (x, y, z, unused)
+   * in the body frame the sphere centres use; the contact point is the candidate with the largest x . d (the first on a
+   * tie); hull_k must be LRL_HULL_K.  The terrain-mesh build (terrain_mesh = 1) keeps the spheres. */
+  int32_t sphere_hull[LRL_MAX_SPHERES];
+  int32_t num_hulls, hull_res, hull_k;
+  const float* hull_table;
 } lrl_model;
 
 /* Reward terms the fused kernel implements (legged_robot.py:1506-1646); the host passes the

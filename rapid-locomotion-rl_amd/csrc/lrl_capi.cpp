@@ -70,6 +70,7 @@ struct lrl_sim {
   int32_t* d_body_link = nullptr;
   float* d_foot_xyz = nullptr;
   void* terr = nullptr;  // terrain mesh buffers (lrl_sim_set_terrain)
+  float* d_hull = nullptr;  // mesh colliders' support tables (KParams::hull_tab)
   uint32_t* self_stats = nullptr;  // lrl_sim_self_contact_stats counters
   float* d_code = nullptr;         // lrl_sim_step_code scratch [3][n]
   // lrl_sim_timing: HIP events around each env-kernel launch of lrl_sim_step (not the history-shift launch before it)
@@ -223,7 +224,18 @@ static int digest(const lrl_model* m, const lrl_env_params* p, KParams* k) {
     k->sph_link[s] = leg < 0 ? -1 : (link > 2 ? 2 : link);
     k->sph_leg[s] = leg;
     if (leg < 0) k->base_sph_end = s + 1;
+    // support tables of the mesh colliders (legs only: the base's spheres are detected before the leg frames exist)
+    const int h = m->num_hulls > 0 ? m->sphere_hull[s] : -1;
+    if (h < -1 || h >= m->num_hulls) return fail(LRL_E_INVALID, "sphere_hull[%d] = %d of %d tables", s, h, m->num_hulls);
+    if (h >= 0 && leg < 0) return fail(LRL_E_INVALID, "sphere %d: support tables are for leg links only", s);
+    k->sph_hull[s] = h;
   }
+  if (m->num_hulls < 0 || m->num_hulls > LRL_MAX_SPHERES) return fail(LRL_E_INVALID, "num_hulls %d", m->num_hulls);
+  if (m->num_hulls > 0 && (!m->hull_table || m->hull_res < 1 || m->hull_res > 64 || m->hull_k != LRL_HULL_K))
+    return fail(LRL_E_INVALID, "hull tables: table %p, hull_res %d, hull_k %d", (const void*)m->hull_table, m->hull_res,
+                m->hull_k);
+  k->hull_res = m->num_hulls > 0 ? m->hull_res : 0;
+  k->hull_k = m->num_hulls > 0 ? m->hull_k : 0;
   for (int l = 0; l < 4; ++l) {
     int b0 = -1, e0 = -1;
     for (int s = 0; s < m->num_spheres; ++s)
@@ -322,6 +334,12 @@ int32_t lrl_sim_create(const lrl_model* model, const lrl_env_params* params, int
     HIPCHECK(hipMemcpy(S.kd + (size_t)j * N, ones.data(), N * 4, hipMemcpyHostToDevice));
   }
   HIPCHECK(hipMemcpy(S.friction, ones.data(), N * 4, hipMemcpyHostToDevice));
+  if (model->num_hulls > 0) {  // the mesh colliders' support tables, read by the plane env kernel's detection
+    const size_t hb = (size_t)model->num_hulls * 6 * model->hull_res * model->hull_res * model->hull_k * 16;
+    HIPCHECK(hipMalloc(&s->d_hull, hb));
+    HIPCHECK(hipMemcpy(s->d_hull, model->hull_table, hb, hipMemcpyHostToDevice));
+    s->hk.hull_tab = s->d_hull;
+  }
   HIPCHECK(hipMalloc(&s->dk, sizeof(KParams)));
   HIPCHECK(hipMemcpy(s->dk, &s->hk, sizeof(KParams), hipMemcpyHostToDevice));
   HIPCHECK(hipMalloc(&s->d_body_leg, sizeof(int32_t) * LRL_MAX_BODIES));
@@ -486,6 +504,7 @@ int32_t lrl_sim_destroy(lrl_sim* s) {
   (void)hipFree(s->d_body_link);
   (void)hipFree(s->d_foot_xyz);
   (void)hipFree(s->terr);
+  (void)hipFree(s->d_hull);
   (void)hipFree(s->self_stats);
   (void)hipFree(s->d_code);
   for (auto& pr : s->ev) {

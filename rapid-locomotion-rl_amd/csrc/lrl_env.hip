@@ -219,9 +219,11 @@ struct Lds {
   __device__ __forceinline__ float4 sph4(int s) const {
     return reinterpret_cast<const float4*>(ktab + 4 * KLEGF)[s];
   }
-  __device__ __forceinline__ int slink(int s) const {
+  // per sphere: its link (low byte, sign-extended: -1 on the base) | (its support table + 1) << 8 (lrl_model::sphere_hull)
+  __device__ __forceinline__ int slink_raw(int s) const {
     return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 4 * nsph)[s];
   }
+  __device__ __forceinline__ int slink(int s) const { return (slink_raw(s) << 24) >> 24; }
   // self-collision groups [lane][g][begin, end) (KParams::self_grp) and pairs (KParams::self_pair), after the links
   __device__ __forceinline__ const int* sgrp() const { return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 5 * nsph); }
   __device__ __forceinline__ uint32_t spair(int p) const {
@@ -588,6 +590,41 @@ __device__ __forceinline__ void apply_impulse(const Lds& M, int s, int lsel, flo
   }
 }
 
+// A mesh collider's contact point (lrl_model::sphere_hull; lrl/robot.py support_table): the hull's support point in
+// the link-frame direction d, from the cube-map cell of d (major axis m, the first of x, y, z on ties; face 2 m +
+// (d_m < 0); u, v = the other two components over |d_m|, each cell index floor((u + 1) N / 2) clamped to [0, N)) and
+// the cell's LRL_HULL_K candidates, the one furthest along d (the first on a tie).  One aligned 64-B block per cell;
+// the tables (≈ 0.6 MB for the Mini Cheetah) stay in L2.  The division is IEEE (not frcp), so the cell is the fp64
+// oracle's except within rounding of a cell edge (lrl_oracle.c hull_support).
+__device__ __forceinline__ V3 hull_support(const KParams* __restrict__ K, int h, V3 d) {
+  const int N = K->hull_res;
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  const int m = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+  const float dm = m == 0 ? d.x : m == 1 ? d.y : d.z;
+  const float du = m == 0 ? d.y : m == 1 ? d.z : d.x;
+  const float dv = m == 0 ? d.z : m == 1 ? d.x : d.y;
+  const float adm = fabsf(dm), hn = 0.5f * (float)N;
+  const int iu = min(max((int)floorf((du / adm + 1.f) * hn), 0), N - 1);
+  const int iv = min(max((int)floorf((dv / adm + 1.f) * hn), 0), N - 1);
+  const int cell = ((2 * m + (dm < 0.f ? 1 : 0)) * N + iu) * N + iv;
+  const float4* c = reinterpret_cast<const float4*>(K->hull_tab) + ((size_t)h * 6 * N * N + cell) * LRL_HULL_K;
+  float4 v[LRL_HULL_K];
+#pragma unroll
+  for (int k = 0; k < LRL_HULL_K; ++k) v[k] = c[k];
+  V3 best = v3(v[0].x, v[0].y, v[0].z);
+  float bd = dot(best, d);
+#pragma unroll
+  for (int k = 1; k < LRL_HULL_K; ++k) {
+    const V3 p = v3(v[k].x, v[k].y, v[k].z);
+    const float pd = dot(p, d);
+    if (pd > bd) {
+      bd = pd;
+      best = p;
+    }
+  }
+  return best;
+}
+
 // One contact sphere's solver rows: g_d, h_d, z_d, e_d and the 3x3 Delassus block W_de = g_d . z_e + h_d . e_e
 // Terrain contacts (TERR): detection leaves the world normal n in fields 3..5 (free until the Delassus values
 // land there); contact_setup builds the frame (n, t1, t2) from it and parks n in fields 0..2 (the contact point
@@ -598,7 +635,9 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
   // and discard them by selection), every store at the end: one round trip instead of one per dependent read
   const int L = lsel < 0 ? 0 : lsel;
   const bool onleg = lsel >= 0;
-  const V3 x = v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2));
+  // (plane: the detection leaves the contact point in fields 6..8 — the sphere centre, or a mesh collider's support
+  // point — and the centre in 0..2 for the self-collision pairs; terrain mesh: the centre in 0..2)
+  const V3 x = TERR ? v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)) : v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8));
   V3 nw = v3(0.f, 0.f, 1.f);
   if constexpr (TERR) nw = v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5));
   V3 ax[3], og[3];
@@ -1488,7 +1527,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 
   if constexpr (TERR) hwin = terrain_window_max(K, st.pos);
   // aa / oo: the carrying leg's joint axes / origins in registers (the leg pass has them; no LDS read-back)
-  auto detect = [&](int s, V3 x, float rad, int lsel, int link, const V3* aa, const V3* oo) {
+  // x: the sphere centre; xc, rad: the contact geometry — the centre and radius, or (plane) a mesh collider's support
+  // point with radius 0 (hull_support)
+  auto detect = [&](int s, V3 x, V3 xc, float rad, int lsel, int link, const V3* aa, const V3* oo) {
     if constexpr (TERR) {
       const V3 pw = v3(st.pos[0], st.pos[1], pz) + mul(R, x);
       M.sph(s, 0) = x.x;
@@ -1508,17 +1549,20 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 #endif
       return;
     }
-    const float sep = pz + dot(Rz, x) - rad;
+    const float sep = pz + dot(Rz, xc) - rad;
     M.sph(s, 0) = x.x;  // (every centre: the self-collision pairs read them)
     M.sph(s, 1) = x.y;
     M.sph(s, 2) = x.z;
     if (sep < P.contact_offset) {
       active |= (1ull << s);
-      V3 u = cross(wb, x) + vb;
+      M.sph(s, 6) = xc.x;  // the contact point (contact_setup)
+      M.sph(s, 7) = xc.y;
+      M.sph(s, 8) = xc.z;
+      V3 u = cross(wb, xc) + vb;
       if (lsel >= 0) {
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          if (j <= link) u = u + st.qd[j] * cross(aa[j], x - oo[j]);
+          if (j <= link) u = u + st.qd[j] * cross(aa[j], xc - oo[j]);
       }
       const float u0 = dot(Rz, u);
       const bool bounce = u0 < -P.bounce_threshold_velocity && rest > 0.f;
@@ -1537,7 +1581,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   for (int s = ql; s < K->base_sph_end; s += QL)
     if (MIRROR == 1 || ((odet >> s) & 1ull)) {
       const float4 sp = M.sph4(s);
-      detect(s, v3(sp.x, sp.y, sp.z), sp.w, -1, 0, nullptr, nullptr);
+      detect(s, v3(sp.x, sp.y, sp.z), v3(sp.x, sp.y, sp.z), sp.w, -1, 0, nullptr, nullptr);
     }
 
   // ---- this lane's leg ----
@@ -1572,12 +1616,23 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       // contact detection for this link's spheres (needs only a_j', o_j' for j' <= j, already in LDS)
       const int sb = sel4(SL.b, l);
       const int se = sel4(SL.e, l);
-      for (int s = sb; s < se; ++s)
-        if (M.slink(s) == j && (MIRROR == 1 || ((odet >> s) & 1ull))) {
+      for (int s = sb; s < se; ++s) {
+        const int raw = M.slink_raw(s);
+        if ((raw & 0xff) == j && (MIRROR == 1 || ((odet >> s) & 1ull))) {
           const float4 sp = M.sph4(s);
           const V3 x = o + mul(Rj, v3(sp.x, sp.y, sp.z));
-          detect(s, x, sp.w, l, j, aa, oo);
+          V3 xc = x;
+          float rad = sp.w;
+          if constexpr (!TERR) {
+            const int h = (raw >> 8) - 1;
+            if (h >= 0) {  // a mesh collider: its support point towards the plane (direction -z, in the link frame)
+              xc = o + mul(Rj, hull_support(K, h, -1.f * mulT(Rj, Rz)));
+              rad = 0.f;
+            }
+          }
+          detect(s, x, xc, rad, l, j, aa, oo);
         }
+      }
       Rp = Rj;
       op = o;
     }
@@ -2228,7 +2283,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     int* sl = reinterpret_cast<int*>(M.ktab + 4 * KLEGF + 4 * nsph);
     for (int s = lane; s < nsph; s += BLOCK) {
       s4[s] = make_float4(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2], K->sph_rad[s]);
-      sl[s] = K->sph_link[s];
+      sl[s] = K->sph_link[s] < 0 ? -1 : (K->sph_link[s] | ((K->sph_hull[s] + 1) << 8));
     }
     if (P.self_collisions) {
       int* sg = sl + nsph;

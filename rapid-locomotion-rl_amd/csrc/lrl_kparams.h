@@ -45,6 +45,11 @@ struct KParams {
   float sph_rad[LRL_MAX_SPHERES];
   int32_t sph_link[LRL_MAX_SPHERES];  // 0..2 dynamic link inside the leg, -1 base
   int32_t sph_leg[LRL_MAX_SPHERES];   // 0..3, -1 base
+  // mesh colliders (lrl_model::sphere_hull, ABI 6): support table of sphere s (-1: the sphere itself), the tables in
+  // device memory [hull][6][hull_res][hull_res][hull_k] float4, plane build only (lrl_env.hip hull_support)
+  int32_t sph_hull[LRL_MAX_SPHERES];
+  const float* hull_tab;
+  int32_t hull_res, hull_k;
   int32_t base_sph_end;               // spheres [0, base_sph_end) are on the base
   int32_t leg_sph_begin[LRL_NUM_LEGS], leg_sph_end[LRL_NUM_LEGS];
   int32_t body_sph_begin[LRL_MAX_BODIES], body_sph_end[LRL_MAX_BODIES];

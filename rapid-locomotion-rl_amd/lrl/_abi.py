@@ -40,6 +40,8 @@ class LrlModel(C.Structure):
         ("sphere_radius", f32 * MAX_SPHERES),
         ("dof_lower", f32 * NUM_DOF), ("dof_upper", f32 * NUM_DOF), ("dof_effort", f32 * NUM_DOF),
         ("dof_velocity", f32 * NUM_DOF),
+        ("sphere_hull", i32 * MAX_SPHERES), ("num_hulls", i32), ("hull_res", i32), ("hull_k", i32),
+        ("hull_table", C.c_void_p),
     ]
 
 

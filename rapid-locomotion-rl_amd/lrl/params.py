@@ -87,6 +87,12 @@ def build_model(robot):
               dof_effort=robot["dof_effort"], dof_velocity=robot["dof_velocity"])
     if robot["num_bodies"] > _abi.MAX_BODIES or robot["num_spheres"] > _abi.MAX_SPHERES:
         raise ValueError("robot model exceeds liblrl limits")
+    if robot.get("num_hulls", 0):  # mesh colliders' support tables (lrl/robot.py support_table; ABI 6)
+        tab = np.ascontiguousarray(robot["hull_table"], np.float32)
+        _abi.fill(m, sphere_hull=robot["sphere_hull"], num_hulls=robot["num_hulls"], hull_res=robot["hull_res"],
+                  hull_k=robot["hull_k"])
+        m.hull_table = tab.ctypes.data
+        m._hull_table = tab  # (keeps the host table alive as long as the model)
     return m
 
 

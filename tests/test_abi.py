@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     lib = C.CDLL(_abi.LIB_PATH)
     missing = [s for s in _declared() if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.lrl_abi_version() == 5
+    assert lib.lrl_abi_version() == 6
 
 
 def test_library_matches_the_sources_beside_it():
