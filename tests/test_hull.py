@@ -1,6 +1,6 @@
-"""Mesh colliders as support tables (CPU): the Mini Cheetah's ab/ad and calf meshes, which PhysX collides as their convex
-hulls (mini_cheetah.urdf:119-124, 176-181), meet the plane at the support point a cube-map table gives (lrl/robot.py
-support_table).  Checked here: the tables reproduce each hull's support function within 1 mm, the
+"""Leg colliders as support tables (CPU): the Mini Cheetah's ab/ad and calf meshes, which PhysX collides as their convex
+hulls (mini_cheetah.urdf:119-124, 176-181), and the rod boxes of both presets' thighs / calves meet the plane at the
+support point a cube-map table gives (lrl/robot.py support_table).  Checked here: the tables reproduce each hull's support function within 1 mm, the
 oracle's lookup (lrl_oracle.c hull_support) picks the table's point, the model carries the tables through the C ABI,
 and (in this container only) the committed tables are the ones the builder makes from the reference's meshes."""
 import ctypes as C
@@ -28,23 +28,25 @@ def _mesh_groups(rob):
     return out
 
 
-def test_mini_cheetah_meshes_have_support_tables():
-    rob = load_robot("mini_cheetah.urdf")
-    g = _mesh_groups(rob)
-    names = [rob["body_names"][b] for b in g]
-    assert sorted(names) == sorted(f"{l}_{k}" for l in ("FL", "FR", "RL", "RR") for k in ("hip", "calf"))
-    for b, hs in g.items():  # ab/ad: one table; calf: the two halves of its capsule stand-in
-        assert len(hs) == (2 if rob["body_names"][b].endswith("calf") else 1)
-    assert rob["hull_table"].shape == (rob["num_hulls"], 6 * rob["hull_res"] ** 2, rob["hull_k"], 4)
-    assert rob["hull_k"] == 4
-    go1 = load_robot("go1.urdf")  # primitives only: no tables
-    assert go1["num_hulls"] == 0 and all(h == -1 for h in go1["sphere_hull"])
+def test_leg_meshes_and_rod_boxes_have_support_tables():
+    """Mini Cheetah: the ab/ad mesh (one table), the thigh's rod box and the calf mesh (the two halves of their capsule
+    stand-ins); Go1: the thigh and calf rod boxes.  Spheres, the capsules of the URDF cylinders (the presets'
+    replace_cylinder_with_capsule, legged_robot_config.py:133) and the base box's corners stay exact as they are."""
+    legs = ("FL", "FR", "RL", "RR")
+    for urdf, parts in (("mini_cheetah.urdf", {"hip": 1, "thigh": 2, "calf": 2}), ("go1.urdf", {"thigh": 2, "calf": 2})):
+        rob = load_robot(urdf)
+        g = _mesh_groups(rob)
+        names = {rob["body_names"][b]: len(hs) for b, hs in g.items()}
+        assert names == {f"{l}_{k}": c for l in legs for k, c in parts.items()}, urdf
+        assert rob["hull_table"].shape == (rob["num_hulls"], 6 * rob["hull_res"] ** 2, rob["hull_k"], 4)
+        assert rob["hull_k"] == 4
 
 
-def test_support_tables_within_1mm_of_the_hulls():
-    """max over 200k random directions of h_hull(d) - h_table(d), per mesh (the calf: the max over its two halves),
+@pytest.mark.parametrize("urdf", ["mini_cheetah.urdf", "go1.urdf"])
+def test_support_tables_within_1mm_of_the_hulls(urdf):
+    """max over 200k random directions of h_hull(d) - h_table(d), per collider (the calf: the max over its two halves),
     and the table never reaches past the hull (its points are hull vertices)"""
-    rob = load_robot("mini_cheetah.urdf")
+    rob = load_robot(urdf)
     D = _dirs(200_000)
     for b, hs in _mesh_groups(rob).items():
         V = np.concatenate([rob["hull_vertices"][h] for h in hs])
@@ -121,5 +123,5 @@ def test_committed_tables_are_the_builders():
     assert m["sphere_hull"] == rob["sphere_hull"]
     for h, v in enumerate(m["hull_vertices"]):
         assert np.array_equal(np.asarray(v), rob["hull_vertices"][h])
-    for h in (0, 1):  # (two of the six tables: the greedy build takes a few seconds each)
+    for h in (0, 3):  # (the FL ab/ad and calf-top tables: the greedy build takes a few seconds each)
         assert np.array_equal(support_table(np.asarray(m["hull_vertices"][h])), rob["hull_table"][h])
