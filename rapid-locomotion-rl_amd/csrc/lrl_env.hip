@@ -1616,9 +1616,16 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       // contact detection for this link's spheres (needs only a_j', o_j' for j' <= j, already in LDS)
       const int sb = sel4(SL.b, l);
       const int se = sel4(SL.e, l);
-      for (int s = sb; s < se; ++s) {
+      // mirrored quads: each lane walks only the leg's spheres its quad detects, the highest first, so the quads' spheres
+      // of one link are handled in the same round (the wave runs max-over-lanes rounds per link, not one per sphere of
+      // the link: with support-table lookups every round is a memory round trip); one quad per env: every sphere
+      const uint64_t legm = (se >= 64 ? ~0ull : (1ull << se) - 1ull) & ~((1ull << sb) - 1ull);
+      uint64_t walk = MIRROR > 1 ? (odet & legm) : legm;
+      while (walk) {
+        const int s = 63 - __builtin_clzll(walk);
+        walk &= ~(1ull << s);
         const int raw = M.slink_raw(s);
-        if ((raw & 0xff) == j && (MIRROR == 1 || ((odet >> s) & 1ull))) {
+        if ((raw & 0xff) == j) {
           const float4 sp = M.sph4(s);
           const V3 x = o + mul(Rj, v3(sp.x, sp.y, sp.z));
           V3 xc = x;

@@ -429,7 +429,7 @@ def test_multi_rank_full_iteration_at_bench_shape(robot, world):
     per rank, teacher PPO + adaptation update) as gloo ranks sharing this GPU: one full PPO iteration per rank.  The
     replicas end bit-identical (parameters, both Adam moments, learning-rate trace) and the all-reduced first gradient
     is the mean of the ranks' gradients, each recomputed by a world-1 update on that rank's saved rollout."""
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()  # (a forked server would inherit this process's HIP state)
     out = mgr.dict()
     with tempfile.TemporaryDirectory() as tmp:
         with rank_env(world):
@@ -468,7 +468,7 @@ def test_rollout_does_not_depend_on_the_gpu_count(legacy_fork, n):
     returns) and the final env state are bit-identical per global env; the advantages, normalised with all-reduced
     statistics (another summation order), agree to fp32 rounding.  With the upstream resets (legacy_fork=False) the
     reset draws too; at 512 envs some step resets envs of one shard only."""
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()  # (a forked server would inherit this process's HIP state)
     one, two = mgr.dict(), mgr.dict()
     with tempfile.TemporaryDirectory() as tmp:
         mp.spawn(_rank_worker, args=(1, 0, "mc", tmp, one, n, True, legacy_fork), nprocs=1, join=True)

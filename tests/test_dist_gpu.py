@@ -167,7 +167,7 @@ def _single_process_first_grad(seed):
 @pytest.mark.timeout(300)
 def test_two_rank_native_update_keeps_replicas_identical():
     world = 2
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()  # (a forked server would inherit this process's HIP state)
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _port(), out), nprocs=world, join=True)
     a, b = out[0], out[1]
@@ -234,7 +234,7 @@ def test_two_rank_command_curriculum_matches_one_process():
     grid-curriculum update / draw over both ranks' resampled envs, so after time-outs and resamplings the two
     64-env ranks hold exactly the commands, bins, curriculum weights and observations of one 128-env process."""
     n, world = 64, 2
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()  # (a forked server would inherit this process's HIP state)
     out = mgr.dict()
     mp.spawn(_curriculum_worker, args=(world, _port(), n, out), nprocs=world, join=True)
     ref = _run_curriculum_env(n * world, 0)
@@ -283,7 +283,7 @@ def test_two_rank_overlapped_adaptation_is_bit_identical():
     moments and the losses are bit-identical on each rank, and the ranks agree.  (gloo here; the same calls run over
     RCCL in bench.py, one GPU per rank — not exercised on this one-GPU box.)"""
     world = 2
-    mgr = mp.Manager()
+    mgr = mp.get_context("spawn").Manager()  # (a forked server would inherit this process's HIP state)
     out = mgr.dict()
     mp.spawn(_overlap_worker, args=(world, _port(), out), nprocs=world, join=True)
     for r in range(world):
