@@ -13,10 +13,11 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (MAX_EXCLUDED, POST_PHYSICS, SEP_EPS_1, VEL_EPS, golden, make, oracle_sensitivity, record_errors,
-                     perturb_state, physics_mismatch)
+from helpers import (MAX_EXCLUDED, POST_PHYSICS, ROBOT_FILES, SEP_EPS_1, VEL_EPS, golden, make, oracle_sensitivity,
+                     perturb_state, physics_mismatch, record_errors)
 from lrl import _abi
 from lrl import config as lcfg
+from lrl.robot import load_robot
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -167,7 +168,27 @@ def _self_states(rng, n, M, root, dof):
     return root, dof
 
 
-def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True, extra=None):
+def _lying_states(rng, n, P):
+    """Robots on their sides (roll +-90 deg with noise, any yaw), base just clear of the plane, legs spread: the legs of
+    the lower side lie along the ground, so the ab/ad, thigh and calf colliders (support tables on the plane, not
+    just the feet) are in contact."""
+    root = np.zeros((n, 13), np.float32)
+    root[:, 0:2] = rng.uniform(10, 60, (n, 2))
+    root[:, 2] = rng.uniform(0.10, 0.14, n)
+    roll = np.where(rng.random(n) < 0.5, 1.0, -1.0) * (np.pi / 2 + rng.normal(size=n) * 0.2)
+    pitch, yaw = rng.normal(size=n) * 0.2, rng.uniform(-np.pi, np.pi, n)
+    cr, sr, cp, sp, cy, sy = (np.cos(roll / 2), np.sin(roll / 2), np.cos(pitch / 2), np.sin(pitch / 2), np.cos(yaw / 2),
+                              np.sin(yaw / 2))
+    root[:, 3:7] = np.stack([sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+                             cr * cp * cy + sr * sp * sy], 1)
+    root[:, 7:10] = rng.normal(size=(n, 3)) * 0.1
+    root[:, 10:13] = rng.normal(size=(n, 3)) * 0.2
+    dof = np.array(P.default_dof_pos[:], np.float32)[None] + rng.normal(size=(n, 12)).astype(np.float32) * 0.3
+    dofv = rng.normal(size=(n, 12)).astype(np.float32) * 0.5
+    return root, dof, dofv
+
+
+def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True, extra=None, lying=False):
     """Kernel vs oracle physics over ``steps`` env steps, re-synchronised: before every step the oracle's state
     (root, joint positions / rates) is written into the sim, so each step is compared from identical inputs — the
     DR values, motor-strength redraws, pushes and injected draws are the same on both sides anyway.  Per step: every
@@ -180,8 +201,10 @@ def _physics_vs_oracle(robot, n, steps, limits=False, selfc=False, self_on=True,
     env = _env(robot, n, **over)
     assert P.self_collisions == int(self_on) and env._P.self_collisions == int(self_on)  # presets: asset.self_collisions 0
     assert env._P.solver_tgs == P.solver_tgs == int(cfg.sim.physx.solver_type == 1)  # presets: solver_type 1 (TGS)
-    rng = np.random.default_rng(5 + steps + (100 if limits else 0) + (200 if selfc else 0))
+    rng = np.random.default_rng(5 + steps + (100 if limits else 0) + (200 if selfc else 0) + (300 if lying else 0))
     root, dof, dofv = _random_states(rng, n, P, robot)
+    if lying:
+        root, dof, dofv = _lying_states(rng, n, P)
     act_lim = None
     if limits:
         dof, dofv, act_lim, picked = _limit_states(rng, n, P, M, root, dof, dofv)
@@ -271,6 +294,19 @@ def test_physics_matches_oracle(robot, n, steps):
     env slots).  Every env of every step within the tolerances of helpers.within_tolerance except the envs
     the oracle reports on a contact-model discontinuity (at most MAX_EXCLUDED per step)."""
     _physics_vs_oracle(robot, n, steps)
+
+
+@pytest.mark.parametrize("robot,steps", [("mc", 1), ("go1", 1), ("mc", 3), ("go1", 3)])
+def test_lying_robots_match_oracle(robot, steps):
+    """The leg colliders' support tables in contact: 1,024 robots lying on their sides, so the ab/ad /
+    thigh / calf colliders of the lower legs touch the plane, not only the feet — kernel vs oracle as above, and the
+    contact forces show those links carrying load in many envs."""
+    got, st, M = _physics_vs_oracle(robot, 1024, steps, lying=True)
+    names = load_robot(ROBOT_FILES[robot])["body_names"]
+    links = [b for b, nm in enumerate(names) if nm.endswith("_hip") or nm.endswith("_thigh")]
+    loaded = (np.linalg.norm(got["contact"][:, links], axis=-1) > 1e-3).any(axis=1)
+    print(f"{robot}: {loaded.mean() * 100:.1f} % of envs with a loaded hip / thigh collider")
+    assert loaded.mean() > 0.2
 
 
 @pytest.mark.parametrize("robot,n,steps", [("mc", 256, 10), ("go1", 256, 3), ("mc", 37, 3)])
