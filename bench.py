@@ -32,11 +32,17 @@ X6_PEAK_TF = MFMA_BF16_PEAK_TF / 6
 
 
 def pmc_traffic(*kernels):
-    """HBM bytes per launch of the first of ``kernels`` (symbol, or symbol@grid) found in the newest committed
-    PMC summary (profiles/r*_pmc.json, written by scripts/gpu_profile.sh + scripts/pmc_summary.py from
-    separate rocprofv3 --pmc passes)."""
+    """HBM bytes per launch of the first of ``kernels`` (symbol, or symbol@grid) found in the committed PMC summary
+    profiles/PMC_CURRENT names (else the newest by name: profiles/r*_pmc.json, written by scripts/gpu_profile.sh +
+    scripts/pmc_summary.py from separate rocprofv3 --pmc passes)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    cur = os.path.join(ROOT, "profiles", "PMC_CURRENT")  # the summary of the tree's own kernels, when named
+    if os.path.exists(cur):
+        with open(cur) as f:
+            named = os.path.join(ROOT, "profiles", f.read().strip())
+        if os.path.exists(named):
+            files = [p for p in files if p != named] + [named]
     for path in reversed(files):
         with open(path) as f:
             table = json.load(f)["kernels"]
