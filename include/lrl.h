@@ -96,7 +96,8 @@ typedef struct lrl_model {
    * direction d (face 2m + (d_m < 0) of the major axis m, first of x, y, z on ties; cell floor((d_(m+1) / |d_m| + 1)
    * hull_res / 2), floor((d_(m+2) / |d_m| + 1) hull_res / 2), clamped), hull_k candidate vertices (x, y, z, unused)
    * in the body frame the sphere centres use; the contact point is the candidate with the largest x . d (the first on a
-   * tie); hull_k must be LRL_HULL_K.  The terrain-mesh build (terrain_mesh = 1) keeps the spheres. */
+   * tie); hull_k must be LRL_HULL_K.  On the terrain mesh (terrain_mesh = 1) the same support point (world -z) is the
+   * triangle query's point, with radius 0. */
   int32_t sphere_hull[LRL_MAX_SPHERES];
   int32_t num_hulls, hull_res, hull_k;
   const float* hull_table;

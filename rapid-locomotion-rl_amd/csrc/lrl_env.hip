@@ -224,6 +224,9 @@ struct Lds {
     return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 4 * nsph)[s];
   }
   __device__ __forceinline__ int slink(int s) const { return (slink_raw(s) << 24) >> 24; }
+  // the terrain query's radius of sphere s: its own, or 0 for a support-table collider (its query point is the
+  // support point)
+  __device__ __forceinline__ float qrad(int s) const { return (slink_raw(s) >> 8) ? 0.f : sph4(s).w; }
   // self-collision groups [lane][g][begin, end) (KParams::self_grp) and pairs (KParams::self_pair), after the links
   __device__ __forceinline__ const int* sgrp() const { return reinterpret_cast<const int*>(ktab + 4 * KLEGF + 5 * nsph); }
   __device__ __forceinline__ uint32_t spair(int p) const {
@@ -635,9 +638,9 @@ __device__ __forceinline__ void contact_setup(const Lds& M, const float* Si, con
   // and discard them by selection), every store at the end: one round trip instead of one per dependent read
   const int L = lsel < 0 ? 0 : lsel;
   const bool onleg = lsel >= 0;
-  // (plane: the detection leaves the contact point in fields 6..8 — the sphere centre, or a mesh collider's support
-  // point — and the centre in 0..2 for the self-collision pairs; terrain mesh: the centre in 0..2)
-  const V3 x = TERR ? v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)) : v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8));
+  // (the detection / activation leaves the contact point in fields 6..8 — the sphere centre, or a collider's support
+  // point — and the centre in 0..2 for the self-collision pairs)
+  const V3 x = v3(M.sph(s, 6), M.sph(s, 7), M.sph(s, 8));
   V3 nw = v3(0.f, 0.f, 1.f);
   if constexpr (TERR) nw = v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5));
   V3 ax[3], og[3];
@@ -1504,9 +1507,9 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   // contact activation: velocity target (restitution / speculative / Baumgarte) along the normal nb (base frame)
   auto activate = [&](int s, V3 x, int lsel, int link, float sep, V3 nb) {
     active |= (1ull << s);
-    M.sph(s, 0) = x.x;
-    M.sph(s, 1) = x.y;
-    M.sph(s, 2) = x.z;
+    M.sph(s, 6) = x.x;  // the contact point (contact_setup; the query's world point there is dead now)
+    M.sph(s, 7) = x.y;
+    M.sph(s, 8) = x.z;
     V3 u = cross(wb, x) + vb;
     if (lsel >= 0) {  // (a sphere recorded by this lane: its leg is the lane's own)
       V3 c[3];
@@ -1519,7 +1522,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
     if (u0 < -P.bounce_threshold_velocity && rest > 0.f) tgt = fmaxf(tgt, -rest * u0);
     M.sph(s, 9) = tgt;
   };
-  // TERR: spheres are only recorded here (contact point, world centre in the rows' free fields 6..8); those not
+  // TERR: spheres are only recorded here (centre, world query point in the rows' free fields 6..8); those not
   // clear of the terrain window around the base (one load) are queried after the leg pass, each lane walking its
   // own list, so a wave pays max-over-lanes queries instead of every sphere of the model
   uint64_t cand = 0;
@@ -1531,10 +1534,13 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
   // point with radius 0 (hull_support)
   auto detect = [&](int s, V3 x, V3 xc, float rad, int lsel, int link, const V3* aa, const V3* oo) {
     if constexpr (TERR) {
-      const V3 pw = v3(st.pos[0], st.pos[1], pz) + mul(R, x);
+      const V3 pw = v3(st.pos[0], st.pos[1], pz) + mul(R, xc);  // (the query point: centre, or support point)
       M.sph(s, 0) = x.x;
       M.sph(s, 1) = x.y;
       M.sph(s, 2) = x.z;
+      M.sph(s, SF_G) = xc.x;  // the contact point in the base frame, for the activation (free until contact_setup)
+      M.sph(s, SF_G + 1) = xc.y;
+      M.sph(s, SF_G + 2) = xc.z;
       M.sph(s, 6) = pw.x;
       M.sph(s, 7) = pw.y;
       M.sph(s, 8) = pw.z;
@@ -1630,12 +1636,11 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
           const V3 x = o + mul(Rj, v3(sp.x, sp.y, sp.z));
           V3 xc = x;
           float rad = sp.w;
-          if constexpr (!TERR) {
-            const int h = (raw >> 8) - 1;
-            if (h >= 0) {  // a mesh collider: its support point towards the plane (direction -z, in the link frame)
-              xc = o + mul(Rj, hull_support(K, h, -1.f * mulT(Rj, Rz)));
-              rad = 0.f;
-            }
+          const int h = (raw >> 8) - 1;
+          if (h >= 0) {  // a support-table collider: its support point towards the ground (world -z, in the link frame;
+                         // on the terrain mesh the triangle query then takes that point with radius 0)
+            xc = o + mul(Rj, hull_support(K, h, -1.f * mulT(Rj, Rz)));
+            rad = 0.f;
           }
           detect(s, x, xc, rad, l, j, aa, oo);
         }
@@ -1721,7 +1726,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
         for (int k = 0; k < CF; ++k) {
           const int sk = cs[k] < 0 ? 0 : cs[k];
           const float px = M.sph(sk, 6), py = M.sph(sk, 7);
-          cz[k] = M.sph(sk, 8) - M.sph4(sk).w - P.contact_offset;
+          cz[k] = M.sph(sk, 8) - M.qrad(sk) - P.contact_offset;
           const int ci = min(max((int)floorf((px + bs) * ih), 0), R - 2);
           const int cj = min(max((int)floorf((py + bs) * ih), 0), Cn - 2);
           hm[k] = cs[k] < 0 ? 3.0e38f : K->terr_hmax[ci * Cn + cj];
@@ -1767,7 +1772,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
           const int L = Ln, s = sn;
           if (j + BLOCK < total) locate(j + BLOCK, Ln, sn);
           float* row = M.base + (M.sph_off + s * NSF) * ENVS + (L >> 2);
-          const THit th = terrain_query(K, v3(row[6 * ENVS], row[7 * ENVS], row[8 * ENVS]), M.sph4(s).w,
+          const THit th = terrain_query(K, v3(row[6 * ENVS], row[7 * ENVS], row[8 * ENVS]), M.qrad(s),
                                         P.contact_offset, tv, lane, prof);
 #ifdef LRL_ENV_PROFILE
           prof[20] += 1;  // query rounds of this lane (lane 0: the wave's rounds)
@@ -1793,7 +1798,8 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
       for (uint64_t m = wl_hit[lane]; m;) {
         const int s = __builtin_ctzll(m);
         m &= m - 1ull;
-        activate(s, v3(M.sph(s, 0), M.sph(s, 1), M.sph(s, 2)), sph_leg_of(SL, s), M.slink(s), M.sph(s, 9),
+        // (contact point: the centre, or a support-table collider's support point, as the detection left it)
+        activate(s, v3(M.sph(s, SF_G), M.sph(s, SF_G + 1), M.sph(s, SF_G + 2)), sph_leg_of(SL, s), M.slink(s), M.sph(s, 9),
                  mulT(R, v3(M.sph(s, 3), M.sph(s, 4), M.sph(s, 5))));
       }
 #ifdef LRL_ENV_PROFILE
@@ -2290,7 +2296,7 @@ __global__ __launch_bounds__(BLOCK) void env_step_kernel(const KParams* __restri
     int* sl = reinterpret_cast<int*>(M.ktab + 4 * KLEGF + 4 * nsph);
     for (int s = lane; s < nsph; s += BLOCK) {
       s4[s] = make_float4(K->sph_pos[s][0], K->sph_pos[s][1], K->sph_pos[s][2], K->sph_rad[s]);
-      sl[s] = K->sph_link[s] < 0 ? -1 : (K->sph_link[s] | ((K->sph_hull[s] + 1) << 8));
+      sl[s] = (K->sph_link[s] & 0xff) | ((K->sph_hull[s] + 1) << 8);  // (base: link byte 0xff = -1, no table)
     }
     if (P.self_collisions) {
       int* sg = sl + nsph;

@@ -195,13 +195,15 @@ def test_bench_grid_physics_step_matches_oracle(robot):
     dr = rng.random(n).astype(np.float32)
     flags = _abi.STEP_PHYSICS | _abi.STEP_INJECT_UNIFORM
     _step_raw(env, _dev(act), flags, _dev(noise), _dev(dr))
-    sp = perturb_state(st, np.random.default_rng(79))
+    rp = np.random.default_rng(79)  # (two perturbation draws, as the plane tests: one misses lopsided spreads)
+    sp, sq = perturb_state(st, rp), perturb_state(st, rp)
     m = np.zeros((n, 2))
     oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr, margins=m)
     oracle.env_step(M, P, sp, act, flags, noise_u=noise, dr_u=dr)
+    oracle.env_step(M, P, sq, act, flags, noise_u=noise, dr_u=dr)
     got = {k: _np(getattr(env, a)) for k, a in dict(root="root_states", dof_pos="dof_pos", dof_vel="dof_vel",
                                                       contact="contact_forces", obs="obs_buf").items()}
-    excl = (m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS) | oracle_sensitivity(st, sp)
+    excl = (m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS) | oracle_sensitivity(st, sp) | oracle_sensitivity(st, sq)
     record_errors(f"configs {robot} n={n} physics step", got, st, excl, sp)
     ok = within_tolerance(got, st) | excl
     print(f"{robot} n={n}: {excl.sum()} envs excluded, {(~ok).sum()} outside tolerance")
@@ -256,13 +258,15 @@ def test_configs2_full_curriculum_trimesh_step_matches_oracle():
     flags = _abi.STEP_PHYSICS | _abi.STEP_INJECT_UNIFORM
     _step_raw(env, _dev(act), flags, _dev(noise), _dev(dr))
     m = np.zeros((n, 2))
-    sp = perturb_state(st, np.random.default_rng(78))
+    rp = np.random.default_rng(78)  # (two perturbation draws, as the plane tests: one misses lopsided spreads)
+    sp, sq = perturb_state(st, rp), perturb_state(st, rp)
     oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr, margins=m)
     oracle.env_step(M, P, sp, act, flags, noise_u=noise, dr_u=dr)
+    oracle.env_step(M, P, sq, act, flags, noise_u=noise, dr_u=dr)
     got = {k: _np(getattr(env, a)) for k, a in dict(root="root_states", dof_pos="dof_pos", dof_vel="dof_vel",
                                                       contact="contact_forces", h="measured_heights").items()}
     assert (np.abs(st["contact"]).sum((1, 2)) > 0).mean() > 0.4  # the poses do touch the terrain
-    excl = (m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS) | oracle_sensitivity(st, sp)
+    excl = (m[:, 0] < SEP_EPS_1) | (m[:, 1] < VEL_EPS) | oracle_sensitivity(st, sp) | oracle_sensitivity(st, sq)
     record_errors(f"configs[2] n={n} trimesh step", got, st, excl, sp)
     ok = within_tolerance(got, st) | excl
     print(f"configs[2] n={n}: {excl.sum()} envs excluded, {(~ok).sum()} outside tolerance")

@@ -145,10 +145,11 @@ def test_rough_terrain_physics_matches_oracle(steps):
         dr = np.full(n, np.nan, np.float32)
         _step_raw(env, _dev(act), flags, _dev(noise), _dev(dr))
         margins = np.zeros((n, 2))
-        st_p = perturb_state(st, rng_p)
+        st_p, st_q = perturb_state(st, rng_p), perturb_state(st, rng_p)  # (two draws, as the plane tests)
         oracle.env_step(M, P, st, act, flags, noise_u=noise, dr_u=dr, margins=margins, common_step_counter=s + 1)
         oracle.env_step(M, P, st_p, act, flags, noise_u=noise, dr_u=dr, common_step_counter=s + 1)
-        sens = oracle_sensitivity(st, st_p)
+        oracle.env_step(M, P, st_q, act, flags, noise_u=noise, dr_u=dr, common_step_counter=s + 1)
+        sens = oracle_sensitivity(st, st_p) | oracle_sensitivity(st, st_q)
         got = {k: _np(getattr(env, a)) for k, a in dict(root="root_states", dof_pos="dof_pos", dof_vel="dof_vel",
                                                           contact="contact_forces", h="measured_heights").items()}
         # fp32 kernel vs double oracle after 4 sub-steps against the mesh, tolerances as for the plane
