@@ -1530,7 +1530,7 @@ __device__ void substep(const KParams* __restrict__ K, Body& st, const float* ta
 
   if constexpr (TERR) hwin = terrain_window_max(K, st.pos);
   // aa / oo: the carrying leg's joint axes / origins in registers (the leg pass has them; no LDS read-back)
-  // x: the sphere centre; xc, rad: the contact geometry — the centre and radius, or (plane) a mesh collider's support
+  // x: the sphere centre; xc, rad: the contact geometry — the centre and radius, or a support-table collider's support
   // point with radius 0 (hull_support)
   auto detect = [&](int s, V3 x, V3 xc, float rad, int lsel, int link, const V3* aa, const V3* oo) {
     if constexpr (TERR) {

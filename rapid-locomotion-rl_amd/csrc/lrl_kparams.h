@@ -46,7 +46,7 @@ struct KParams {
   int32_t sph_link[LRL_MAX_SPHERES];  // 0..2 dynamic link inside the leg, -1 base
   int32_t sph_leg[LRL_MAX_SPHERES];   // 0..3, -1 base
   // mesh colliders (lrl_model::sphere_hull, ABI 6): support table of sphere s (-1: the sphere itself), the tables in
-  // device memory [hull][6][hull_res][hull_res][hull_k] float4, plane build only (lrl_env.hip hull_support)
+  // device memory [hull][6][hull_res][hull_res][hull_k] float4 (lrl_env.hip hull_support; both builds)
   int32_t sph_hull[LRL_MAX_SPHERES];
   const float* hull_tab;
   int32_t hull_res, hull_k;

@@ -3,7 +3,7 @@ reads the meshes under /root/reference/resources).  PhysX collides a mesh as its
 plane (normal n) a convex body touches first at its support point in direction -n, so the quantity that decides
 ground contact is the support function h(d) = max_x x.d.  For every stand-in this prints, over 2,000 directions
 spread over the sphere (and over the lower hemisphere of the link frame alone), the largest and mean |h_hull(d) -
-h_spheres(d)|, where h_spheres(d) = max_i (c_i.d + r_i) over the stand-in's spheres.  Since round 6 the plane contacts use the support
+h_spheres(d)|, where h_spheres(d) = max_i (c_i.d + r_i) over the stand-in's spheres.  Since round 6 the ground contacts use the support
 tables instead (lrl/robot.py support_table, lrl/robots/mini_cheetah_hulls.npz): "table_*" is the same measure for
 h_table(d) = the table point's x.d (the max over the mesh's tables: the calf's two halves), over 200,000 random
 directions, against the hull of the mesh as the URDF places it in the link frame.
